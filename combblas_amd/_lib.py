@@ -1,0 +1,116 @@
+"""ctypes binding of the C-ABI in include/combblas_hip.h (libcombblas_hip.so, in-tree).
+
+There is no fallback: if the HIP library is missing the import fails loudly, so a GPU run can
+never silently take another path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcombblas_hip.so")
+
+c_int64_p = ctypes.POINTER(ctypes.c_int64)
+c_int32_p = ctypes.POINTER(ctypes.c_int32)
+
+
+class cbh_dcsc(ctypes.Structure):
+    _fields_ = [("m", ctypes.c_int64), ("n", ctypes.c_int64), ("nnz", ctypes.c_int64), ("nzc", ctypes.c_int64),
+                ("cp", ctypes.c_void_p), ("jc", ctypes.c_void_p), ("ir", ctypes.c_void_p), ("num", ctypes.c_void_p)]
+
+
+class cbh_phase_stats(ctypes.Structure):
+    _fields_ = [("flops", ctypes.c_int64), ("nnz", ctypes.c_int64), ("phases", ctypes.c_int64),
+                ("value_sum", ctypes.c_double), ("digest", ctypes.c_uint64)]
+
+
+class cbh_kernel_times(ctypes.Structure):
+    _fields_ = [("symbolic_ms", ctypes.c_double), ("numeric_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("numeric_launches", ctypes.c_int64)]
+
+
+class cbh_kernel_stat(ctypes.Structure):
+    _fields_ = [("ms", ctypes.c_double), ("launches", ctypes.c_int64), ("alg_bytes", ctypes.c_double)]
+
+
+K_SYM_LARGE, K_SYM_SMALL, K_NUM_LARGE, K_NUM_SMALL, K_MERGE_SYM, K_MERGE_NUM = range(6)
+K_NAMES = ["sym_large", "sym_small", "num_large", "num_small", "merge_sym", "merge_num"]
+
+ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
+FREE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p)
+
+# every exported symbol with its signature (restype, argtypes); tests check the header against it
+SIGNATURES = {
+    "cbh_version": (ctypes.c_char_p, []),
+    "cbh_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbh_ctx_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "cbh_ctx_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
+    "cbh_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbh_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "cbh_ctx_set_allocator": (ctypes.c_int, [ctypes.c_void_p, ALLOC_FN, FREE_FN, ctypes.c_void_p]),
+    "cbh_ctx_set_phase_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    "cbh_mat_upload": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cbh_dcsc), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_mat_wrap_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cbh_dcsc), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_mat_info": (ctypes.c_int, [ctypes.c_void_p, c_int64_p, c_int64_p, c_int64_p, c_int64_p, ctypes.POINTER(ctypes.c_int)]),
+    "cbh_mat_device_arrays": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_void_p)] * 4),
+    "cbh_mat_copy_out": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "cbh_mat_free": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "cbh_spgemm": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                  ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_spgemm_symbolic": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_int64_p, c_int64_p,
+                                           ctypes.c_void_p, ctypes.c_void_p]),
+    "cbh_merge": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                 ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_spgemm_phased": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_uint32, ctypes.POINTER(cbh_phase_stats)]),
+    "cbh_last_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cbh_kernel_times)]),
+    "cbh_ctx_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "cbh_kernel_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(cbh_kernel_stat)]),
+    "cbh_kernel_stats_reset": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbh_rmat_edges": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                                      ctypes.c_void_p]),
+    "cbh_edges_to_csc": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, c_int64_p]),
+}
+
+CBH_OK = 0
+ERRORS = {3001: "GRIDMISMATCH", 3002: "DIMMISMATCH", 3005: "MATRIXALIAS", 4001: "HIP error", 4002: "out of memory",
+          4003: "invalid argument", 4004: "device consistency check failed", 4005: "no HIP device"}
+
+CBH_KEEP_EMPTY_COLS = 0x2
+CBH_PHASE_CHECKSUM = 0x100
+
+
+class CombBLASHipError(RuntimeError):
+    def __init__(self, code, msg=""):
+        self.code = code
+        super().__init__(f"combblas_hip error {code} ({ERRORS.get(code, '?')}): {msg}")
+
+
+_lib = None
+
+
+def lib():
+    """Loads libcombblas_hip.so once. Raises ImportError when it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `python -m combblas_amd.build` "
+                              "(there is no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, ctx=None):
+    if rc != CBH_OK:
+        msg = lib().cbh_last_error(ctx).decode() if ctx else ""
+        raise CombBLASHipError(rc, msg)

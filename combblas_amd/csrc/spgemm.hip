@@ -1,0 +1,1146 @@
+// C-ABI implementation of the gfx950 semiring SpGEMM hot path (include/combblas_hip.h).
+//
+// Pipeline of one cbh_spgemm call (reference stages in brackets):
+//   densify_cp     A's DCSC -> dense column pointers        [Dcsc::ConstructAux/FillColInds, dcsc.cpp:983-1010,1282-1344]
+//   flop_kernel    flop_j, rmin_j, rmax_j per column of B    [estimateFLOP, mtSpGEMM.h:1057-1134]
+//   bin_*          columns binned by flop (symbolic) / nnz (numeric), large bins ordered by size
+//   tile_kernel<SYM>  exact nnz per column                   [estimateNNZ_Hash, mtSpGEMM.h:806-933]
+//   hipcub scan    column offsets of C                        [prefixsum, mtSpGEMM.h:23-70]
+//   tile_kernel<NUM>  values, rows ascending per column      [LocalHybridSpGEMM loop, mtSpGEMM.h:289-441]
+//   compact_cols   drop empty columns -> DCSC of C            [SpDCCols(SpTuples), SpDCCols.cpp:109-183]
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/combblas_hip.h"
+#include "semiring.h"
+#include "tile_kernel.h"
+
+using namespace cbh;
+
+// ============================================================================ context / matrices
+struct cbh_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::string err;
+  int64_t phase_budget = 0;
+  bool timing = false;
+  cbh_kernel_times times{-1, -1, -1, 0};
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  int* d_err = nullptr;  // 4 ints of device-side error flags
+  cbh_alloc_fn alloc = nullptr;
+  cbh_free_fn release = nullptr;
+  void* alloc_user = nullptr;
+  // per-launch instrumentation (cbh_ctx_enable_timing): events around every tile-kernel launch
+  struct Rec {
+    int kind;
+    size_t e0, e1;
+    double bytes;
+  };
+  std::vector<hipEvent_t> evpool;
+  size_t evused = 0;
+  std::vector<Rec> recs;
+  double k_ms[CBH_K_NKINDS] = {0};
+  int64_t k_launch[CBH_K_NKINDS] = {0};
+  double k_bytes[CBH_K_NKINDS] = {0};
+};
+
+struct cbh_mat {
+  int64_t m = 0, n = 0, nnz = 0, nzc = 0;
+  int dtype = CBH_F64;
+  int64_t* cp = nullptr;
+  int64_t* jc = nullptr;
+  int32_t* ir = nullptr;
+  void* num = nullptr;
+  bool owned = true;
+};
+
+static size_t dtype_size(int dt) {
+  switch (dt) {
+    case CBH_F64: case CBH_I64: return 8;
+    case CBH_F32: case CBH_I32: return 4;
+    case CBH_BOOL: return 1;
+  }
+  return 0;
+}
+
+#define CBH_HIP(ctx, call)                                                                       \
+  do {                                                                                           \
+    hipError_t e_ = (call);                                                                      \
+    if (e_ != hipSuccess) {                                                                      \
+      (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);                            \
+      return (e_ == hipErrorOutOfMemory || e_ == hipErrorMemoryAllocation) ? CBH_E_OOM : CBH_E_HIP; \
+    }                                                                                            \
+  } while (0)
+
+#define CBH_TRY(x)            \
+  do {                        \
+    int rc_ = (x);            \
+    if (rc_ != CBH_OK) return rc_; \
+  } while (0)
+
+static int fail(cbh_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+template <class T>
+static int dalloc(cbh_ctx* ctx, T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  const size_t bytes = ((count * sizeof(T)) + 255) & ~size_t(255);
+  if (ctx->alloc) {
+    *p = reinterpret_cast<T*>(ctx->alloc(ctx->alloc_user, (int64_t)bytes, ctx->stream));
+    if (!*p) return fail(ctx, CBH_E_OOM, "allocator callback failed for " + std::to_string(bytes) + " bytes");
+    return CBH_OK;
+  }
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(p), bytes, ctx->stream);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return fail(ctx, CBH_E_OOM, "hipMallocAsync(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+  }
+  return CBH_OK;
+}
+static void dfree(cbh_ctx* ctx, void* p) {
+  if (!p) return;
+  if (ctx->release) ctx->release(ctx->alloc_user, p, ctx->stream);
+  else (void)hipFreeAsync(p, ctx->stream);
+}
+
+// RAII holder for scratch allocations of one call.
+struct Scratch {
+  cbh_ctx* ctx;
+  std::vector<void*> ptrs;
+  explicit Scratch(cbh_ctx* c) : ctx(c) {}
+  template <class T>
+  int get(T** p, size_t count) {
+    int rc = dalloc(ctx, p, count);
+    if (rc == CBH_OK) ptrs.push_back(*p);
+    return rc;
+  }
+  ~Scratch() {
+    for (void* p : ptrs) dfree(ctx, p);
+  }
+};
+
+// ============================================================================ auxiliary kernels
+__global__ void densify_cp_kernel(const int64_t* __restrict__ jc, const int64_t* __restrict__ cp, int64_t nzc,
+                                  int64_t n, int64_t nnz, int64_t* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > n) return;
+  int64_t lo = 0, hi = nzc;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (jc[mid] < k) lo = mid + 1;
+    else hi = mid;
+  }
+  out[k] = lo < nzc ? cp[lo] : nnz;
+}
+
+// One wave per nonzero column of B: flops, and the row range any product can reach
+// (A's columns are row-sorted, so first/last entries bound them).
+__global__ __launch_bounds__(256) void flop_kernel(const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
+                                                   const int64_t* __restrict__ Bcp, const int32_t* __restrict__ Bir,
+                                                   int64_t nzc, int64_t* __restrict__ flop, int32_t* __restrict__ rmin,
+                                                   int32_t* __restrict__ rmax) {
+  const int lane = threadIdx.x & 63;
+  const int64_t col = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (col >= nzc) return;
+  int64_t f = 0;
+  int32_t mn = INT32_MAX, mx = -1;
+  for (int64_t p = Bcp[col] + lane; p < Bcp[col + 1]; p += 64) {
+    const int32_t k = Bir[p];
+    const int64_t s = Acp[k], e = Acp[k + 1];
+    if (e > s) {
+      f += e - s;
+      mn = min(mn, Air[s]);
+      mx = max(mx, Air[e - 1]);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    f += __shfl_xor(f, o);
+    mn = min(mn, __shfl_xor(mn, o));
+    mx = max(mx, __shfl_xor(mx, o));
+  }
+  if (lane == 0) {
+    flop[col] = f;
+    rmin[col] = f ? mn : 0;
+    rmax[col] = f ? mx : 0;
+  }
+}
+
+// Bins: 0 = no work, 1 = small (work <= small_cap), 2 + (kSub-1-lg) = large, lg = floor(log2 work):
+// laid out in bin order so the large list runs from the heaviest columns down.
+constexpr int kSub = 48;
+constexpr int kNB = 2 + kSub;
+
+__device__ __forceinline__ int bin_of(int64_t w, int64_t small_cap) {
+  if (w <= 0) return 0;
+  if (w <= small_cap) return 1;
+  int lg = 63 - __clzll((unsigned long long)w);
+  if (lg > kSub - 1) lg = kSub - 1;
+  return 2 + (kSub - 1 - lg);
+}
+
+// Optional per-group unit sums for the roofline (group 0 = small bin, 1 = large bins):
+// sums[g*3 + 0] = sum of B column lengths, [1] = flops, [2] = nnz(C).
+__global__ __launch_bounds__(256) void bin_count_kernel(const int64_t* __restrict__ work, int64_t n, int64_t small_cap,
+                                                        unsigned long long* __restrict__ counts,
+                                                        const int64_t* __restrict__ Bcp, const int64_t* __restrict__ flop,
+                                                        const int64_t* __restrict__ nnz,
+                                                        unsigned long long* __restrict__ sums) {
+  __shared__ unsigned int h[kNB];
+  __shared__ unsigned long long ssum[6];
+  for (int i = threadIdx.x; i < kNB; i += blockDim.x) h[i] = 0;
+  if (threadIdx.x < 6) ssum[threadIdx.x] = 0;
+  __syncthreads();
+  unsigned long long loc[6] = {0, 0, 0, 0, 0, 0};
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x) {
+    const int b = bin_of(work[c], small_cap);
+    atomicAdd(&h[b], 1u);
+    if (sums && b > 0) {
+      const int g = (b == 1) ? 0 : 1;
+      loc[g * 3 + 0] += (unsigned long long)(Bcp ? Bcp[c + 1] - Bcp[c] : 0);
+      loc[g * 3 + 1] += (unsigned long long)(flop ? flop[c] : 0);
+      loc[g * 3 + 2] += (unsigned long long)(nnz ? nnz[c] : 0);
+    }
+  }
+  if (sums)
+    for (int i = 0; i < 6; ++i)
+      if (loc[i]) atomicAdd(&ssum[i], loc[i]);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kNB; i += blockDim.x)
+    if (h[i]) atomicAdd(&counts[i], (unsigned long long)h[i]);
+  if (sums && threadIdx.x < 6 && ssum[threadIdx.x]) atomicAdd(&sums[threadIdx.x], ssum[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void bin_scatter_kernel(const int64_t* __restrict__ work, int64_t n, int64_t col0,
+                                                          int64_t small_cap, unsigned long long* __restrict__ cursor,
+                                                          int32_t* __restrict__ cols) {
+  __shared__ unsigned int h[kNB];
+  __shared__ unsigned long long base[kNB];
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int i = threadIdx.x; i < kNB; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  int b = -1;
+  unsigned int r = 0;
+  if (c < n) {
+    b = bin_of(work[c], small_cap);
+    r = atomicAdd(&h[b], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kNB; i += blockDim.x)
+    base[i] = h[i] ? atomicAdd(&cursor[i], (unsigned long long)h[i]) : 0ull;
+  __syncthreads();
+  if (b > 0) cols[base[b] + r] = (int32_t)(c + col0);
+}
+
+__global__ void fill_i64_kernel(int64_t* p, int64_t n, int64_t v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+__global__ void nz_flag_kernel(const int64_t* __restrict__ nnz, int64_t n, int64_t* __restrict__ flag) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) flag[i] = nnz[i] > 0 ? 1 : 0;
+}
+
+__global__ void compact_cols_kernel(const int64_t* __restrict__ nnz, const int64_t* __restrict__ pos,
+                                    const int64_t* __restrict__ Bjc, const int64_t* __restrict__ Ccp, int64_t n,
+                                    int64_t* __restrict__ jc, int64_t* __restrict__ cp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && nnz[i] > 0) {
+    jc[pos[i]] = Bjc[i];
+    cp[pos[i]] = Ccp[i];
+  }
+  if (i == n - 1) cp[pos[n]] = Ccp[n];
+}
+
+__global__ void widen_i32_kernel(const int32_t* __restrict__ f, int64_t* __restrict__ o, int64_t k) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < k) o[i] = f[i];
+}
+
+// merge: mark union of column ids
+__global__ void mark_cols_kernel(const int64_t* __restrict__ jc, int64_t nzc, int32_t* __restrict__ flag) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nzc) flag[jc[i]] = 1;
+}
+__global__ void union_cols_kernel(const int32_t* __restrict__ flag, const int64_t* __restrict__ idx, int64_t n,
+                                  int64_t* __restrict__ jcC) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n && flag[k]) jcC[idx[k]] = k;
+}
+__global__ void merge_seg_kernel(const int64_t* __restrict__ jc, const int64_t* __restrict__ cp, int64_t nzc,
+                                 const int64_t* __restrict__ idx, int l, int nl, int64_t* __restrict__ seg_start,
+                                 int64_t* __restrict__ seg_len) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nzc) return;
+  const int64_t c = idx[jc[i]];
+  seg_start[c * nl + l] = cp[i];
+  seg_len[c * nl + l] = cp[i + 1] - cp[i];
+}
+struct ListRows {
+  const int32_t* ir[kMaxLists];
+};
+__global__ void merge_work_kernel(const int64_t* __restrict__ seg_start, const int64_t* __restrict__ seg_len, int nl,
+                                  ListRows lr, int64_t ncols, int64_t* __restrict__ work, int32_t* __restrict__ rmin,
+                                  int32_t* __restrict__ rmax) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncols) return;
+  int64_t w = 0;
+  int32_t mn = INT32_MAX, mx = -1;
+  for (int l = 0; l < nl; ++l) {
+    const int64_t len = seg_len[c * nl + l];
+    if (len > 0) {
+      const int64_t s = seg_start[c * nl + l];
+      w += len;
+      mn = min(mn, lr.ir[l][s]);
+      mx = max(mx, lr.ir[l][s + len - 1]);
+    }
+  }
+  work[c] = w;
+  rmin[c] = w ? mn : 0;
+  rmax[c] = w ? mx : 0;
+}
+
+// checksum of one C block: wave per column; global entry index = gbase + local index
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+template <class VT>
+__global__ __launch_bounds__(256) void checksum_kernel(const int64_t* __restrict__ colid, const int64_t* __restrict__ cp,
+                                                       int64_t cbase, int64_t ncols, const int32_t* __restrict__ ir,
+                                                       const VT* __restrict__ num, int64_t gbase,
+                                                       double* __restrict__ vsum, unsigned long long* __restrict__ dig) {
+  const int lane = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  double s = 0;
+  uint64_t d = 0;
+  if (c < ncols) {
+    const uint64_t col = (uint64_t)colid[c];
+    for (int64_t p = cp[c] - cbase + lane; p < cp[c + 1] - cbase; p += 64) {
+      const VT v = num[p];
+      uint64_t bits;
+      if constexpr (sizeof(VT) == 8) bits = __builtin_bit_cast(uint64_t, v);
+      else if constexpr (sizeof(VT) == 4) bits = (uint64_t)__builtin_bit_cast(uint32_t, v);
+      else bits = (uint64_t)v;
+      s += (double)v;
+      d += mix64((uint64_t)(gbase + p) ^ mix64(col ^ mix64((uint64_t)(uint32_t)ir[p] ^ mix64(bits))));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o);
+    d += __shfl_xor(d, o);
+  }
+  if (lane == 0 && c < ncols) {
+    atomicAdd(vsum, s);
+    atomicAdd(dig, (unsigned long long)d);
+  }
+}
+
+// ============================================================================ kernel configurations
+// symbolic: small (flop <= 256) one 128-thread block per column, 512-slot table;
+//           large: 512 threads, 8192-slot key table, row tiles of <= 4096 flops.
+// numeric : small (nnz <= 256) 512(+64)-slot table; large: 4096(+64) slots, tiles of <= 2048 rows.
+constexpr int64_t kSmallCap = 256;
+struct SymSmall { static constexpr int T = 512, BS = 128, EMAX = 256; };
+struct SymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512; };
+struct NumSmall { static constexpr int T = 512, BS = 128, EMAX = 256; };
+struct NumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512; };
+
+static size_t next_event(cbh_ctx* ctx) {
+  if (ctx->evused == ctx->evpool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return (size_t)-1;
+    ctx->evpool.push_back(e);
+  }
+  return ctx->evused++;
+}
+
+// Folds the recorded launch events into the per-kind totals (call after a stream sync).
+static void flush_records(cbh_ctx* ctx) {
+  for (const auto& r : ctx->recs) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, ctx->evpool[r.e0], ctx->evpool[r.e1]) == hipSuccess) {
+      ctx->k_ms[r.kind] += ms;
+      ctx->k_launch[r.kind] += 1;
+      ctx->k_bytes[r.kind] += r.bytes;
+    }
+  }
+  ctx->recs.clear();
+  ctx->evused = 0;
+}
+
+template <class SR, class CFG, int MODE>
+static int launch_tile(cbh_ctx* ctx, const TileArgs& args, int64_t first, int64_t count, int kind = -1,
+                       double bytes = 0) {
+  if (count <= 0) return CBH_OK;
+  size_t e0 = (size_t)-1;
+  if (ctx->timing && kind >= 0) {
+    e0 = next_event(ctx);
+    if (e0 != (size_t)-1) (void)hipEventRecord(ctx->evpool[e0], ctx->stream);
+  }
+  using C = TileCfg<SR, CFG::T, CFG::BS, CFG::EMAX, MODE>;
+  auto kern = tile_kernel<SR, CFG::T, CFG::BS, CFG::EMAX, MODE>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    CBH_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)C::bytes));
+    attr_set = true;
+  }
+  TileArgs a = args;
+  a.cols = args.cols + first;
+  // grid.x limit is 2^31-1; launch in slices for safety
+  const int64_t kMaxGrid = 1ll << 30;
+  for (int64_t off = 0; off < count; off += kMaxGrid) {
+    const int64_t n = std::min(kMaxGrid, count - off);
+    TileArgs b = a;
+    b.cols = a.cols + off;
+    b.ncols = n;
+    hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(CFG::BS), C::bytes, ctx->stream, b);
+    CBH_HIP(ctx, hipGetLastError());
+  }
+  if (e0 != (size_t)-1) {
+    const size_t e1 = next_event(ctx);
+    if (e1 != (size_t)-1) {
+      (void)hipEventRecord(ctx->evpool[e1], ctx->stream);
+      ctx->recs.push_back({kind, e0, e1, bytes});
+    }
+  }
+  return CBH_OK;
+}
+
+// Bins the column slots [0, n) by work. Returns list offsets of the small and large groups.
+struct BinLists {
+  int64_t small_first = 0, small_count = 0, large_first = 0, large_count = 0;
+  double units[6] = {0, 0, 0, 0, 0, 0};  // [small|large] x [sum b_j, sum flop_j, sum nnz_j] (timing only)
+};
+// Unit sums are gathered only when the context records timings (bench/roofline); Bcp/flop/nnz
+// are indexed like `work` (already offset by col0 by the caller).
+static int make_bins(cbh_ctx* ctx, Scratch& S, const int64_t* work, int64_t n, int64_t col0, int32_t* cols,
+                     BinLists* out, const int64_t* Bcp = nullptr, const int64_t* flop = nullptr,
+                     const int64_t* nnz = nullptr) {
+  unsigned long long* counts;
+  CBH_TRY(S.get(&counts, 2 * kNB + 6));
+  unsigned long long* sums = ctx->timing ? counts + 2 * kNB : nullptr;
+  CBH_HIP(ctx, hipMemsetAsync(counts, 0, sizeof(unsigned long long) * (2 * kNB + 6), ctx->stream));
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(bin_count_kernel, dim3(std::max(grid, 1)), dim3(256), 0, ctx->stream, work, n, kSmallCap, counts,
+                     Bcp, flop, nnz, sums);
+  CBH_HIP(ctx, hipGetLastError());
+  unsigned long long h[kNB + 2 * kNB + 6];
+  CBH_HIP(ctx, hipMemcpyAsync(h, counts, sizeof(unsigned long long) * (2 * kNB + 6), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  unsigned long long off[kNB];
+  unsigned long long run = 0;
+  off[0] = 0;  // bin 0 not stored
+  for (int b = 1; b < kNB; ++b) {
+    off[b] = run;
+    run += h[b];
+  }
+  unsigned long long* cursor = counts + kNB;
+  CBH_HIP(ctx, hipMemcpyAsync(cursor, off, sizeof(off), hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(bin_scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, work, n, col0,
+                     kSmallCap, cursor, cols);
+  CBH_HIP(ctx, hipGetLastError());
+  // the host copy of `off` must outlive the async H2D copy
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (sums)
+    for (int i = 0; i < 6; ++i) out->units[i] = (double)h[2 * kNB + i];
+  out->small_first = 0;
+  out->small_count = (int64_t)h[1];
+  out->large_first = (int64_t)h[1];
+  out->large_count = (int64_t)(run - h[1]);
+  return CBH_OK;
+}
+
+static int exclusive_scan_i64(cbh_ctx* ctx, Scratch& S, const int64_t* in, int64_t* out, int64_t n) {
+  size_t tmp = 0;
+  CBH_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)n, ctx->stream));
+  void* t;
+  CBH_TRY(S.get(reinterpret_cast<char**>(&t), tmp));
+  CBH_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(t, tmp, in, out, (int)n, ctx->stream));
+  return CBH_OK;
+}
+
+static int sum_i64(cbh_ctx* ctx, Scratch& S, const int64_t* in, int64_t n, int64_t* d_out) {
+  size_t tmp = 0;
+  CBH_HIP(ctx, hipcub::DeviceReduce::Sum(nullptr, tmp, in, d_out, (int)n, ctx->stream));
+  void* t;
+  CBH_TRY(S.get(reinterpret_cast<char**>(&t), tmp));
+  CBH_HIP(ctx, hipcub::DeviceReduce::Sum(t, tmp, in, d_out, (int)n, ctx->stream));
+  return CBH_OK;
+}
+
+static inline unsigned blocks_for(int64_t n, int bs) { return (unsigned)std::max<int64_t>(1, (n + bs - 1) / bs); }
+
+static int check_err(cbh_ctx* ctx) {
+  int h[4];
+  CBH_HIP(ctx, hipMemcpyAsync(h, ctx->d_err, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->timing) flush_records(ctx);
+  if (h[0] || h[1]) {
+    CBH_HIP(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(h), ctx->stream));
+    return fail(ctx, CBH_E_INTERNAL,
+                "device consistency check failed (count mismatch " + std::to_string(h[0]) + ", split failure " +
+                    std::to_string(h[1]) + ")");
+  }
+  return CBH_OK;
+}
+
+// ============================================================================ symbolic (shared by spgemm)
+struct Plan {  // device arrays describing C = A*B column by column (B's nonzero columns)
+  int64_t nzcB = 0;
+  int64_t* Adense = nullptr;  // A.n + 1
+  int64_t* flop = nullptr;    // nzcB
+  int32_t* rmin = nullptr;
+  int32_t* rmax = nullptr;
+  int64_t* nnz = nullptr;  // nzcB + 1
+  int64_t* Ccp = nullptr;  // nzcB + 1
+  int32_t* cols = nullptr; // nzcB
+  int64_t total_flops = 0, total_nnz = 0;
+};
+
+static TileArgs spgemm_args(const cbh_mat* A, const cbh_mat* B, const Plan& P, cbh_ctx* ctx) {
+  TileArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.Acp = P.Adense;
+  a.Air = A->ir;
+  a.Anum = A->num;
+  a.Bcp = B->cp;
+  a.Bir = B->ir;
+  a.Bnum = B->num;
+  a.cols = P.cols;
+  a.rmin = P.rmin;
+  a.rmax = P.rmax;
+  a.err = ctx->d_err;
+  return a;
+}
+
+static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat* B, Plan& P) {
+  P.nzcB = B->nzc;
+  CBH_TRY(S.get(&P.Adense, A->n + 1));
+  CBH_TRY(S.get(&P.flop, P.nzcB + 1));
+  CBH_TRY(S.get(&P.rmin, P.nzcB));
+  CBH_TRY(S.get(&P.rmax, P.nzcB));
+  CBH_TRY(S.get(&P.nnz, P.nzcB + 1));
+  CBH_TRY(S.get(&P.Ccp, P.nzcB + 1));
+  CBH_TRY(S.get(&P.cols, P.nzcB));
+  int64_t* d_tot;
+  CBH_TRY(S.get(&d_tot, 2));
+  hipLaunchKernelGGL(densify_cp_kernel, dim3(blocks_for(A->n + 1, 256)), dim3(256), 0, ctx->stream, A->jc, A->cp,
+                     A->nzc, A->n, A->nnz, P.Adense);
+  hipLaunchKernelGGL(flop_kernel, dim3(blocks_for(P.nzcB, 4)), dim3(256), 0, ctx->stream, P.Adense, A->ir, B->cp, B->ir,
+                     P.nzcB, P.flop, P.rmin, P.rmax);
+  CBH_HIP(ctx, hipGetLastError());
+  CBH_TRY(sum_i64(ctx, S, P.flop, P.nzcB, d_tot));
+  CBH_HIP(ctx, hipMemsetAsync(P.nnz, 0, sizeof(int64_t) * (P.nzcB + 1), ctx->stream));
+  BinLists bl;
+  CBH_TRY(make_bins(ctx, S, P.flop, P.nzcB, 0, P.cols, &bl, B->cp, P.flop, nullptr));
+  TileArgs a = spgemm_args(A, B, P, ctx);
+  a.work = P.flop;
+  a.nnz_out = P.nnz;
+  using Dummy = PlusTimesD<int64_t>;
+  // algorithmic bytes of the symbolic pass: row ids of B and of every gathered A entry + pointers
+  const double sb_l = 4.0 * (bl.units[3] + bl.units[4]) + 16.0 * bl.large_count;
+  const double sb_s = 4.0 * (bl.units[0] + bl.units[1]) + 16.0 * bl.small_count;
+  CBH_TRY((launch_tile<Dummy, SymLarge, MODE_SYM>(ctx, a, bl.large_first, bl.large_count, CBH_K_SYM_LARGE, sb_l)));
+  CBH_TRY((launch_tile<Dummy, SymSmall, MODE_SYM>(ctx, a, bl.small_first, bl.small_count, CBH_K_SYM_SMALL, sb_s)));
+  CBH_TRY(exclusive_scan_i64(ctx, S, P.nnz, P.Ccp, P.nzcB + 1));
+  CBH_HIP(ctx, hipMemcpyAsync(d_tot + 1, P.Ccp + P.nzcB, sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
+  int64_t h[2];
+  CBH_HIP(ctx, hipMemcpyAsync(h, d_tot, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  P.total_flops = h[0];
+  P.total_nnz = h[1];
+  return check_err(ctx);
+}
+
+// numeric over column slots [c0, c1) writing C entries at Ccp[c]-cbase
+template <class SR>
+static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat* B, Plan& P, int64_t c0, int64_t c1,
+                       int64_t cbase, int32_t* Cir, void* Cnum, int64_t* launches) {
+  BinLists bl;
+  CBH_TRY(make_bins(ctx, S, P.nnz + c0, c1 - c0, c0, P.cols, &bl, B->cp + c0, P.flop + c0, P.nnz + c0));
+  TileArgs a = spgemm_args(A, B, P, ctx);
+  a.work = P.nnz;
+  a.Ccp = P.Ccp;
+  a.cbase = cbase;
+  a.Cir = Cir;
+  a.Cnum = Cnum;
+  // algorithmic bytes: (s_i+s_v) * (nnz(B) + flops + nnz(C)) + pointers
+  constexpr double eb = 4.0 + sizeof(typename SR::val_t);
+  const double nb_l = eb * (bl.units[3] + bl.units[4] + bl.units[5]) + 16.0 * bl.large_count;
+  const double nb_s = eb * (bl.units[0] + bl.units[1] + bl.units[2]) + 16.0 * bl.small_count;
+  CBH_TRY((launch_tile<SR, NumLarge, MODE_NUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
+  CBH_TRY((launch_tile<SR, NumSmall, MODE_NUM>(ctx, a, bl.small_first, bl.small_count, CBH_K_NUM_SMALL, nb_s)));
+  if (launches) *launches += (bl.large_count > 0) + (bl.small_count > 0);
+  return CBH_OK;
+}
+
+// ============================================================================ semiring dispatch
+template <class F>
+static int dispatch_sr(cbh_ctx* ctx, cbh_semiring sr, int dtype, F&& f) {
+  switch (sr) {
+    case CBH_SR_PLUS_TIMES:
+      if (dtype == CBH_F64) return f(PlusTimesD<double>{});
+      if (dtype == CBH_I64) return f(PlusTimesD<int64_t>{});
+      if (dtype == CBH_F32) return f(PlusTimesD<float>{});
+      if (dtype == CBH_I32) return f(PlusTimesD<int32_t>{});
+      if (dtype == CBH_BOOL) return f(OrAndD{});
+      break;
+    case CBH_SR_SELECT_MAX:
+      if (dtype == CBH_F64) return f(SelectMaxD<double>{});
+      if (dtype == CBH_I64) return f(SelectMaxD<int64_t>{});
+      break;
+    case CBH_SR_MIN_PLUS:
+      if (dtype == CBH_F64) return f(MinPlusD<double>{});
+      if (dtype == CBH_I64) return f(MinPlusD<int64_t>{});
+      break;
+    case CBH_SR_OR_AND:
+      if (dtype == CBH_BOOL) return f(OrAndD{});
+      break;
+    default:
+      break;
+  }
+  return fail(ctx, CBH_E_ARG, "unsupported semiring/dtype combination (sr=" + std::to_string((int)sr) +
+                                  ", dtype=" + std::to_string(dtype) + ")");
+}
+
+static int new_mat(cbh_ctx* ctx, int64_t m, int64_t n, int64_t nnz, int64_t nzc, int dtype, cbh_mat** out) {
+  cbh_mat* M = new cbh_mat;
+  M->m = m;
+  M->n = n;
+  M->nnz = nnz;
+  M->nzc = nzc;
+  M->dtype = dtype;
+  int rc = dalloc(ctx, &M->cp, nzc + 1);
+  if (rc == CBH_OK) rc = dalloc(ctx, &M->jc, nzc);
+  if (rc == CBH_OK) rc = dalloc(ctx, &M->ir, nnz);
+  if (rc == CBH_OK) rc = dalloc(ctx, reinterpret_cast<char**>(&M->num), nnz * dtype_size(dtype));
+  if (rc != CBH_OK) {
+    cbh_mat_free(ctx, M);
+    return rc;
+  }
+  *out = M;
+  return CBH_OK;
+}
+
+static int empty_result(cbh_ctx* ctx, int64_t m, int64_t n, int dtype, cbh_mat** C) {
+  CBH_TRY(new_mat(ctx, m, n, 0, 0, dtype, C));
+  CBH_HIP(ctx, hipMemsetAsync((*C)->cp, 0, sizeof(int64_t), ctx->stream));
+  return CBH_OK;
+}
+
+static int validate_pair(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B) {
+  if (!ctx || !A || !B) return fail(ctx, CBH_E_ARG, "null argument");
+  if (A == B) return fail(ctx, CBH_E_MATRIXALIAS, "A and B alias (ParFriends.h:172-179)");
+  if (A->n != B->m) return fail(ctx, CBH_E_DIMMISMATCH, "A.getncol() != B.getnrow()");
+  if (A->dtype != B->dtype) return fail(ctx, CBH_E_ARG, "A and B dtypes differ");
+  if (A->m > INT32_MAX) return fail(ctx, CBH_E_DIMMISMATCH, "local row count exceeds 32-bit row ids");
+  return CBH_OK;
+}
+
+static void ev_record(cbh_ctx* ctx, int i) {
+  if (ctx->timing) (void)hipEventRecord(ctx->ev[i], ctx->stream);
+}
+static float ev_ms(cbh_ctx* ctx, int a, int b) {
+  float ms = -1;
+  if (ctx->timing) (void)hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]);
+  return ms;
+}
+
+// ============================================================================ C-ABI
+extern "C" {
+
+const char* cbh_version(void) { return "combblas_hip 0.1 (gfx950)"; }
+
+int cbh_ctx_create(int device, cbh_ctx** out) {
+  if (!out) return CBH_E_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return CBH_E_NODEVICE;
+  if (device < 0 || device >= ndev) return CBH_E_ARG;
+  cbh_ctx* c = new cbh_ctx;
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return CBH_E_HIP;
+  }
+  c->own_stream = true;
+  for (auto& e : c->ev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      delete c;
+      return CBH_E_HIP;
+    }
+  if (hipMalloc(&c->d_err, 4 * sizeof(int)) != hipSuccess || hipMemset(c->d_err, 0, 4 * sizeof(int)) != hipSuccess) {
+    delete c;
+    return CBH_E_HIP;
+  }
+  *out = c;
+  return CBH_OK;
+}
+
+int cbh_ctx_destroy(cbh_ctx* ctx) {
+  if (!ctx) return CBH_OK;
+  (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->d_err) (void)hipFree(ctx->d_err);
+  for (auto& e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : ctx->evpool) (void)hipEventDestroy(e);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return CBH_OK;
+}
+
+int cbh_ctx_set_stream(cbh_ctx* ctx, void* s) {
+  if (!ctx) return CBH_E_ARG;
+  if (ctx->own_stream) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamDestroy(ctx->stream);
+    ctx->own_stream = false;
+  }
+  if (s) {
+    ctx->stream = reinterpret_cast<hipStream_t>(s);
+  } else {
+    CBH_HIP(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    ctx->own_stream = true;
+  }
+  return CBH_OK;
+}
+
+void* cbh_ctx_stream(cbh_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
+
+int cbh_ctx_synchronize(cbh_ctx* ctx) {
+  if (!ctx) return CBH_E_ARG;
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return CBH_OK;
+}
+
+const char* cbh_last_error(cbh_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int cbh_ctx_set_allocator(cbh_ctx* ctx, cbh_alloc_fn alloc, cbh_free_fn release, void* user) {
+  if (!ctx || (alloc == nullptr) != (release == nullptr)) return CBH_E_ARG;
+  ctx->alloc = alloc;
+  ctx->release = release;
+  ctx->alloc_user = user;
+  return CBH_OK;
+}
+
+int cbh_ctx_set_phase_budget(cbh_ctx* ctx, int64_t bytes) {
+  if (!ctx || bytes < 0) return CBH_E_ARG;
+  ctx->phase_budget = bytes;
+  return CBH_OK;
+}
+
+int cbh_kernel_stats(cbh_ctx* ctx, int kind, cbh_kernel_stat* out) {
+  if (!ctx || !out || kind < 0 || kind >= CBH_K_NKINDS) return CBH_E_ARG;
+  out->ms = ctx->k_ms[kind];
+  out->launches = ctx->k_launch[kind];
+  out->alg_bytes = ctx->k_bytes[kind];
+  return CBH_OK;
+}
+
+int cbh_kernel_stats_reset(cbh_ctx* ctx) {
+  if (!ctx) return CBH_E_ARG;
+  for (int k = 0; k < CBH_K_NKINDS; ++k) {
+    ctx->k_ms[k] = 0;
+    ctx->k_launch[k] = 0;
+    ctx->k_bytes[k] = 0;
+  }
+  return CBH_OK;
+}
+
+int cbh_ctx_enable_timing(cbh_ctx* ctx, int enable) {
+  if (!ctx) return CBH_E_ARG;
+  ctx->timing = enable != 0;
+  return CBH_OK;
+}
+
+int cbh_last_kernel_times(cbh_ctx* ctx, cbh_kernel_times* t) {
+  if (!ctx || !t) return CBH_E_ARG;
+  *t = ctx->times;
+  return CBH_OK;
+}
+
+int cbh_mat_upload(cbh_ctx* ctx, const cbh_dcsc* h, cbh_dtype dtype, cbh_mat** out) {
+  if (!ctx || !h || !out || dtype_size(dtype) == 0) return fail(ctx, CBH_E_ARG, "bad upload arguments");
+  if (h->nnz < 0 || h->nzc < 0 || h->m < 0 || h->n < 0) return fail(ctx, CBH_E_DIMMISMATCH, "negative sizes");
+  cbh_mat* M;
+  CBH_TRY(new_mat(ctx, h->m, h->n, h->nnz, h->nzc, dtype, &M));
+  const size_t vs = dtype_size(dtype);
+  if (h->nzc > 0) {
+    CBH_HIP(ctx, hipMemcpyAsync(M->cp, h->cp, sizeof(int64_t) * (h->nzc + 1), hipMemcpyHostToDevice, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(M->jc, h->jc, sizeof(int64_t) * h->nzc, hipMemcpyHostToDevice, ctx->stream));
+  } else {
+    CBH_HIP(ctx, hipMemsetAsync(M->cp, 0, sizeof(int64_t), ctx->stream));
+  }
+  if (h->nnz > 0) {
+    CBH_HIP(ctx, hipMemcpyAsync(M->ir, h->ir, sizeof(int32_t) * h->nnz, hipMemcpyHostToDevice, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(M->num, h->num, vs * h->nnz, hipMemcpyHostToDevice, ctx->stream));
+  }
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // host buffers may be released on return
+  *out = M;
+  return CBH_OK;
+}
+
+int cbh_mat_wrap_device(cbh_ctx* ctx, const cbh_dcsc* d, cbh_dtype dtype, cbh_mat** out) {
+  if (!ctx || !d || !out || dtype_size(dtype) == 0) return fail(ctx, CBH_E_ARG, "bad wrap arguments");
+  cbh_mat* M = new cbh_mat;
+  M->m = d->m;
+  M->n = d->n;
+  M->nnz = d->nnz;
+  M->nzc = d->nzc;
+  M->dtype = dtype;
+  M->cp = const_cast<int64_t*>(d->cp);
+  M->jc = const_cast<int64_t*>(d->jc);
+  M->ir = const_cast<int32_t*>(d->ir);
+  M->num = const_cast<void*>(d->num);
+  M->owned = false;
+  *out = M;
+  return CBH_OK;
+}
+
+int cbh_mat_info(const cbh_mat* M, int64_t* m, int64_t* n, int64_t* nnz, int64_t* nzc, int* dtype) {
+  if (!M) return CBH_E_ARG;
+  if (m) *m = M->m;
+  if (n) *n = M->n;
+  if (nnz) *nnz = M->nnz;
+  if (nzc) *nzc = M->nzc;
+  if (dtype) *dtype = M->dtype;
+  return CBH_OK;
+}
+
+int cbh_mat_device_arrays(const cbh_mat* M, const int64_t** cp, const int64_t** jc, const int32_t** ir,
+                          const void** num) {
+  if (!M) return CBH_E_ARG;
+  if (cp) *cp = M->cp;
+  if (jc) *jc = M->jc;
+  if (ir) *ir = M->ir;
+  if (num) *num = M->num;
+  return CBH_OK;
+}
+
+int cbh_mat_copy_out(cbh_ctx* ctx, const cbh_mat* M, int64_t* cp, int64_t* jc, int32_t* ir, void* num,
+                     int dst_on_device) {
+  if (!ctx || !M) return CBH_E_ARG;
+  const hipMemcpyKind k = dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  if (cp) CBH_HIP(ctx, hipMemcpyAsync(cp, M->cp, sizeof(int64_t) * (M->nzc + 1), k, ctx->stream));
+  if (jc && M->nzc) CBH_HIP(ctx, hipMemcpyAsync(jc, M->jc, sizeof(int64_t) * M->nzc, k, ctx->stream));
+  if (ir && M->nnz) CBH_HIP(ctx, hipMemcpyAsync(ir, M->ir, sizeof(int32_t) * M->nnz, k, ctx->stream));
+  if (num && M->nnz) CBH_HIP(ctx, hipMemcpyAsync(num, M->num, dtype_size(M->dtype) * M->nnz, k, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return CBH_OK;
+}
+
+int cbh_mat_free(cbh_ctx* ctx, cbh_mat* M) {
+  if (!M) return CBH_OK;
+  if (M->owned && ctx) {
+    dfree(ctx, M->cp);
+    dfree(ctx, M->jc);
+    dfree(ctx, M->ir);
+    dfree(ctx, M->num);
+  }
+  delete M;
+  return CBH_OK;
+}
+
+int cbh_spgemm_symbolic(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, int64_t* flops, int64_t* nnzC,
+                        int64_t* col_flops_dev, int64_t* col_nnz_dev) {
+  CBH_TRY(validate_pair(ctx, A, B));
+  if (A->nnz == 0 || B->nnz == 0) {
+    if (flops) *flops = 0;
+    if (nnzC) *nnzC = 0;
+    if (col_flops_dev && B->nzc) CBH_HIP(ctx, hipMemsetAsync(col_flops_dev, 0, sizeof(int64_t) * B->nzc, ctx->stream));
+    if (col_nnz_dev && B->nzc) CBH_HIP(ctx, hipMemsetAsync(col_nnz_dev, 0, sizeof(int64_t) * B->nzc, ctx->stream));
+    return CBH_OK;
+  }
+  Scratch S(ctx);
+  Plan P;
+  CBH_TRY(run_symbolic(ctx, S, A, B, P));
+  if (flops) *flops = P.total_flops;
+  if (nnzC) *nnzC = P.total_nnz;
+  if (col_flops_dev)
+    CBH_HIP(ctx, hipMemcpyAsync(col_flops_dev, P.flop, sizeof(int64_t) * P.nzcB, hipMemcpyDeviceToDevice, ctx->stream));
+  if (col_nnz_dev)
+    CBH_HIP(ctx, hipMemcpyAsync(col_nnz_dev, P.nnz, sizeof(int64_t) * P.nzcB, hipMemcpyDeviceToDevice, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return CBH_OK;
+}
+
+int cbh_spgemm(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh_mat* B, uint32_t flags, cbh_mat** C) {
+  CBH_TRY(validate_pair(ctx, A, B));
+  if (!C) return fail(ctx, CBH_E_ARG, "null output");
+  *C = nullptr;
+  ctx->times = cbh_kernel_times{-1, -1, -1, 0};
+  if (A->nnz == 0 || B->nnz == 0) return empty_result(ctx, A->m, B->n, A->dtype, C);
+  return dispatch_sr(ctx, sr, A->dtype, [&](auto srv) -> int {
+    using SR = decltype(srv);
+    Scratch S(ctx);
+    Plan P;
+    ev_record(ctx, 0);
+    CBH_TRY(run_symbolic(ctx, S, A, B, P));
+    ev_record(ctx, 1);
+    cbh_mat* out;
+    const bool keep = (flags & CBH_KEEP_EMPTY_COLS) != 0;
+    int64_t nzcC = P.nzcB;
+    int64_t* pos = nullptr;
+    if (!keep) {
+      int64_t* flag;
+      CBH_TRY(S.get(&flag, P.nzcB + 1));
+      CBH_TRY(S.get(&pos, P.nzcB + 1));
+      hipLaunchKernelGGL(nz_flag_kernel, dim3(blocks_for(P.nzcB + 1, 256)), dim3(256), 0, ctx->stream, P.nnz,
+                         P.nzcB + 1, flag);
+      CBH_TRY(exclusive_scan_i64(ctx, S, flag, pos, P.nzcB + 1));
+      CBH_HIP(ctx, hipMemcpyAsync(&nzcC, pos + P.nzcB, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+      CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    CBH_TRY(new_mat(ctx, A->m, B->n, P.total_nnz, nzcC, A->dtype, &out));
+    int64_t launches = 0;
+    int rc = run_numeric<SR>(ctx, S, A, B, P, 0, P.nzcB, 0, out->ir, out->num, &launches);
+    if (rc == CBH_OK) {
+      if (keep) {
+        (void)hipMemcpyAsync(out->jc, B->jc, sizeof(int64_t) * P.nzcB, hipMemcpyDeviceToDevice, ctx->stream);
+        (void)hipMemcpyAsync(out->cp, P.Ccp, sizeof(int64_t) * (P.nzcB + 1), hipMemcpyDeviceToDevice, ctx->stream);
+      } else {
+        hipLaunchKernelGGL(compact_cols_kernel, dim3(blocks_for(P.nzcB, 256)), dim3(256), 0, ctx->stream, P.nnz, pos,
+                           B->jc, P.Ccp, P.nzcB, out->jc, out->cp);
+      }
+      ev_record(ctx, 2);
+      rc = check_err(ctx);
+    }
+    if (rc != CBH_OK) {
+      cbh_mat_free(ctx, out);
+      return rc;
+    }
+    if (ctx->timing) {
+      ctx->times.symbolic_ms = ev_ms(ctx, 0, 1);
+      ctx->times.numeric_ms = ev_ms(ctx, 1, 2);
+      ctx->times.total_ms = ev_ms(ctx, 0, 2);
+      ctx->times.numeric_launches = launches;
+    }
+    *C = out;
+    return CBH_OK;
+  });
+}
+
+int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh_mat* B, uint32_t flags,
+                      cbh_phase_stats* st) {
+  CBH_TRY(validate_pair(ctx, A, B));
+  if (!st) return fail(ctx, CBH_E_ARG, "null stats");
+  std::memset(st, 0, sizeof(*st));
+  ctx->times = cbh_kernel_times{-1, -1, -1, 0};
+  if (A->nnz == 0 || B->nnz == 0) return CBH_OK;
+  return dispatch_sr(ctx, sr, A->dtype, [&](auto srv) -> int {
+    using SR = decltype(srv);
+    using VT = typename SR::val_t;
+    Scratch S(ctx);
+    Plan P;
+    ev_record(ctx, 0);
+    CBH_TRY(run_symbolic(ctx, S, A, B, P));
+    ev_record(ctx, 1);
+    const size_t esz = sizeof(int32_t) + sizeof(VT);
+    int64_t budget_bytes = ctx->phase_budget;
+    if (budget_bytes <= 0) {
+      size_t freeb = 0, totb = 0;
+      CBH_HIP(ctx, hipMemGetInfo(&freeb, &totb));
+      budget_bytes = (int64_t)(freeb / 2);
+    }
+    int64_t budget = std::max<int64_t>(1, budget_bytes / (int64_t)esz);
+    // phase boundaries over B's column slots from the exact column offsets
+    std::vector<int64_t> hcp(P.nzcB + 1);
+    CBH_HIP(ctx, hipMemcpyAsync(hcp.data(), P.Ccp, sizeof(int64_t) * (P.nzcB + 1), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    std::vector<int64_t> cuts{0};
+    int64_t maxcol = 0;
+    for (int64_t c = 0; c < P.nzcB; ++c) maxcol = std::max(maxcol, hcp[c + 1] - hcp[c]);
+    budget = std::max(budget, maxcol);
+    while (cuts.back() < P.nzcB) {
+      const int64_t c0 = cuts.back();
+      const int64_t lim = hcp[c0] + budget;
+      int64_t c1 = (int64_t)(std::upper_bound(hcp.begin() + c0 + 1, hcp.end(), lim) - hcp.begin()) - 1;
+      if (c1 <= c0) c1 = c0 + 1;
+      cuts.push_back(c1);
+    }
+    const int64_t maxphase = [&] {
+      int64_t mx = 0;
+      for (size_t i = 1; i < cuts.size(); ++i) mx = std::max(mx, hcp[cuts[i]] - hcp[cuts[i - 1]]);
+      return mx;
+    }();
+    int32_t* ir;
+    VT* num;
+    CBH_TRY(S.get(&ir, maxphase));
+    CBH_TRY(S.get(&num, maxphase));
+    double* d_sum;
+    unsigned long long* d_dig;
+    CBH_TRY(S.get(&d_sum, 1));
+    CBH_TRY(S.get(&d_dig, 1));
+    CBH_HIP(ctx, hipMemsetAsync(d_sum, 0, sizeof(double), ctx->stream));
+    CBH_HIP(ctx, hipMemsetAsync(d_dig, 0, sizeof(unsigned long long), ctx->stream));
+    int64_t launches = 0;
+    for (size_t i = 1; i < cuts.size(); ++i) {
+      const int64_t c0 = cuts[i - 1], c1 = cuts[i];
+      CBH_TRY(run_numeric<SR>(ctx, S, A, B, P, c0, c1, hcp[c0], ir, num, &launches));
+      if (flags & CBH_PHASE_CHECKSUM) {
+        hipLaunchKernelGGL(checksum_kernel<VT>, dim3(blocks_for(c1 - c0, 4)), dim3(256), 0, ctx->stream, B->jc + c0,
+                           P.Ccp + c0, hcp[c0], c1 - c0, ir, num, hcp[c0], d_sum, d_dig);
+        CBH_HIP(ctx, hipGetLastError());
+      }
+    }
+    ev_record(ctx, 2);
+    CBH_TRY(check_err(ctx));
+    double hs = 0;
+    unsigned long long hd = 0;
+    CBH_HIP(ctx, hipMemcpyAsync(&hs, d_sum, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(&hd, d_dig, sizeof(hd), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    st->flops = P.total_flops;
+    st->nnz = P.total_nnz;
+    st->phases = (int64_t)cuts.size() - 1;
+    st->value_sum = hs;
+    st->digest = hd;
+    if (ctx->timing) {
+      ctx->times.symbolic_ms = ev_ms(ctx, 0, 1);
+      ctx->times.numeric_ms = ev_ms(ctx, 1, 2);
+      ctx->times.total_ms = ev_ms(ctx, 0, 2);
+      ctx->times.numeric_launches = launches;
+    }
+    return CBH_OK;
+  });
+}
+
+int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* parts, cbh_mat** C) {
+  if (!ctx || !C || nlists < 0 || (nlists > 0 && !parts)) return fail(ctx, CBH_E_ARG, "bad merge arguments");
+  if (nlists > kMaxLists) return fail(ctx, CBH_E_ARG, "at most 16 lists per merge; merge hierarchically");
+  *C = nullptr;
+  if (nlists == 0) return fail(ctx, CBH_E_ARG, "merge of zero lists has no dimensions");
+  const cbh_mat* P0 = parts[0];
+  for (int l = 0; l < nlists; ++l) {
+    if (!parts[l]) return fail(ctx, CBH_E_ARG, "null list");
+    if (parts[l]->m != P0->m || parts[l]->n != P0->n)
+      return fail(ctx, CBH_E_DIMMISMATCH, "Dimensions of SpTuples do not match on multiwayMerge()");
+    if (parts[l]->dtype != P0->dtype) return fail(ctx, CBH_E_ARG, "list dtypes differ");
+  }
+  const int dtype = P0->dtype;
+  const size_t vs = dtype_size(dtype);
+  if (nlists == 1) {  // MultiwayMerge.h:420-439: one list is copied
+    cbh_mat* out;
+    CBH_TRY(new_mat(ctx, P0->m, P0->n, P0->nnz, P0->nzc, dtype, &out));
+    CBH_HIP(ctx, hipMemcpyAsync(out->cp, P0->cp, sizeof(int64_t) * (P0->nzc + 1), hipMemcpyDeviceToDevice, ctx->stream));
+    if (P0->nzc) CBH_HIP(ctx, hipMemcpyAsync(out->jc, P0->jc, sizeof(int64_t) * P0->nzc, hipMemcpyDeviceToDevice, ctx->stream));
+    if (P0->nnz) {
+      CBH_HIP(ctx, hipMemcpyAsync(out->ir, P0->ir, sizeof(int32_t) * P0->nnz, hipMemcpyDeviceToDevice, ctx->stream));
+      CBH_HIP(ctx, hipMemcpyAsync(out->num, P0->num, vs * P0->nnz, hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *C = out;
+    return CBH_OK;
+  }
+  return dispatch_sr(ctx, sr, dtype, [&](auto srv) -> int {
+    using SR = decltype(srv);
+    Scratch S(ctx);
+    const int64_t n = P0->n;
+    int32_t* flag;
+    int64_t *idx, *flag64;
+    CBH_TRY(S.get(&flag, n + 1));
+    CBH_TRY(S.get(&flag64, n + 1));
+    CBH_TRY(S.get(&idx, n + 1));
+    CBH_HIP(ctx, hipMemsetAsync(flag, 0, sizeof(int32_t) * (n + 1), ctx->stream));
+    for (int l = 0; l < nlists; ++l)
+      if (parts[l]->nzc)
+        hipLaunchKernelGGL(mark_cols_kernel, dim3(blocks_for(parts[l]->nzc, 256)), dim3(256), 0, ctx->stream,
+                           parts[l]->jc, parts[l]->nzc, flag);
+    // widen flags for the int64 scan
+    hipLaunchKernelGGL(widen_i32_kernel, dim3(blocks_for(n + 1, 256)), dim3(256), 0, ctx->stream, flag, flag64, n + 1);
+    CBH_TRY(exclusive_scan_i64(ctx, S, flag64, idx, n + 1));
+    int64_t ncols = 0;
+    CBH_HIP(ctx, hipMemcpyAsync(&ncols, idx + n, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ncols == 0) return empty_result(ctx, P0->m, n, dtype, C);
+    int64_t *jcC, *seg_start, *seg_len, *work, *nnz, *Ccp;
+    int32_t *rmin, *rmax, *cols;
+    CBH_TRY(S.get(&jcC, ncols));
+    CBH_TRY(S.get(&seg_start, ncols * nlists));
+    CBH_TRY(S.get(&seg_len, ncols * nlists));
+    CBH_TRY(S.get(&work, ncols + 1));
+    CBH_TRY(S.get(&nnz, ncols + 1));
+    CBH_TRY(S.get(&Ccp, ncols + 1));
+    CBH_TRY(S.get(&rmin, ncols));
+    CBH_TRY(S.get(&rmax, ncols));
+    CBH_TRY(S.get(&cols, ncols));
+    hipLaunchKernelGGL(union_cols_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, flag, idx, n, jcC);
+    CBH_HIP(ctx, hipMemsetAsync(seg_len, 0, sizeof(int64_t) * ncols * nlists, ctx->stream));
+    CBH_HIP(ctx, hipMemsetAsync(seg_start, 0, sizeof(int64_t) * ncols * nlists, ctx->stream));
+    ListRows lr;
+    std::memset(&lr, 0, sizeof(lr));
+    TileArgs a;
+    std::memset(&a, 0, sizeof(a));
+    for (int l = 0; l < nlists; ++l) {
+      lr.ir[l] = parts[l]->ir;
+      a.lir[l] = parts[l]->ir;
+      a.lnum[l] = parts[l]->num;
+      if (parts[l]->nzc)
+        hipLaunchKernelGGL(merge_seg_kernel, dim3(blocks_for(parts[l]->nzc, 256)), dim3(256), 0, ctx->stream,
+                           parts[l]->jc, parts[l]->cp, parts[l]->nzc, idx, l, nlists, seg_start, seg_len);
+    }
+    hipLaunchKernelGGL(merge_work_kernel, dim3(blocks_for(ncols, 256)), dim3(256), 0, ctx->stream, seg_start, seg_len,
+                       nlists, lr, ncols, work, rmin, rmax);
+    CBH_HIP(ctx, hipGetLastError());
+    a.seg_start = seg_start;
+    a.seg_len = seg_len;
+    a.nlists = nlists;
+    a.cols = cols;
+    a.rmin = rmin;
+    a.rmax = rmax;
+    a.err = ctx->d_err;
+    // symbolic
+    CBH_HIP(ctx, hipMemsetAsync(nnz, 0, sizeof(int64_t) * (ncols + 1), ctx->stream));
+    BinLists bl;
+    CBH_TRY(make_bins(ctx, S, work, ncols, 0, cols, &bl));
+    a.work = work;
+    a.nnz_out = nnz;
+    CBH_TRY((launch_tile<SR, SymLarge, MODE_SYM_MRG>(ctx, a, bl.large_first, bl.large_count, CBH_K_MERGE_SYM)));
+    CBH_TRY((launch_tile<SR, SymSmall, MODE_SYM_MRG>(ctx, a, bl.small_first, bl.small_count, CBH_K_MERGE_SYM)));
+    CBH_TRY(exclusive_scan_i64(ctx, S, nnz, Ccp, ncols + 1));
+    int64_t total = 0;
+    CBH_HIP(ctx, hipMemcpyAsync(&total, Ccp + ncols, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    CBH_TRY(check_err(ctx));
+    cbh_mat* out;
+    CBH_TRY(new_mat(ctx, P0->m, n, total, ncols, dtype, &out));
+    int rc = make_bins(ctx, S, nnz, ncols, 0, cols, &bl);
+    if (rc == CBH_OK) {
+      a.work = nnz;
+      a.Ccp = Ccp;
+      a.cbase = 0;
+      a.Cir = out->ir;
+      a.Cnum = out->num;
+      rc = launch_tile<SR, NumLarge, MODE_NUM_MRG>(ctx, a, bl.large_first, bl.large_count, CBH_K_MERGE_NUM);
+      if (rc == CBH_OK)
+        rc = launch_tile<SR, NumSmall, MODE_NUM_MRG>(ctx, a, bl.small_first, bl.small_count, CBH_K_MERGE_NUM);
+    }
+    if (rc == CBH_OK) {
+      (void)hipMemcpyAsync(out->jc, jcC, sizeof(int64_t) * ncols, hipMemcpyDeviceToDevice, ctx->stream);
+      (void)hipMemcpyAsync(out->cp, Ccp, sizeof(int64_t) * (ncols + 1), hipMemcpyDeviceToDevice, ctx->stream);
+      rc = check_err(ctx);
+    }
+    if (rc != CBH_OK) {
+      cbh_mat_free(ctx, out);
+      return rc;
+    }
+    *C = out;
+    return CBH_OK;
+  });
+}
+
+}  // extern "C"

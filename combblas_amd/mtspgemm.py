@@ -1,0 +1,108 @@
+"""Host mirror of the reference's local SpGEMM interface (include/CombBLAS/mtSpGEMM.h,
+include/CombBLAS/MultiwayMerge.h). Same names, argument meaning and ownership rules; every call
+runs on the gfx950 kernels behind the C-ABI (no CPU path).
+
+Differences that follow from the device layout (documented in DESIGN.md §1):
+  * results are device DCSC blocks (SpDCCols) instead of SpTuples: the reference converts its
+    SpTuples to SpDCCols right after the call (ParFriends.h:1100-1102), here that is fused;
+  * LocalSpGEMMHash(sort=False) still returns rows ascending (a valid order of the unsorted
+    contract; the reference's slot order depends on a sequential insertion order);
+  * LocalSpGEMM (heap) and the hybrid share one numeric kernel: the result contract is identical.
+"""
+from __future__ import annotations
+
+import ctypes
+
+from . import _lib
+from ._lib import check, lib
+from .semirings import Semiring
+from .spdccols import SpDCCols
+
+
+def _spgemm(SR: Semiring, A: SpDCCols, B: SpDCCols, clearA, clearB, flags=0) -> SpDCCols:
+    if A.ctx is not B.ctx:
+        raise ValueError("A and B live in different contexts")
+    h = ctypes.c_void_p()
+    check(lib().cbh_spgemm(A.ctx.h, SR.code, A.h, B.h, flags, ctypes.byref(h)), A.ctx.h)
+    C = SpDCCols(A.ctx, h)
+    if clearA:
+        A.free()
+    if clearB:
+        B.free()
+    return C
+
+
+def LocalHybridSpGEMM(SR: Semiring, A: SpDCCols, B: SpDCCols, clearA=False, clearB=False, aux=None) -> SpDCCols:
+    """mtSpGEMM.h:213-460 -- C = A*B, rows ascending within each column."""
+    return _spgemm(SR, A, B, clearA, clearB)
+
+
+def LocalSpGEMMHash(SR: Semiring, A: SpDCCols, B: SpDCCols, clearA=False, clearB=False, sort=True) -> SpDCCols:
+    """mtSpGEMM.h:463-656 (sort=False is satisfied by the sorted result)."""
+    return _spgemm(SR, A, B, clearA, clearB)
+
+
+def LocalSpGEMM(SR: Semiring, A: SpDCCols, B: SpDCCols, clearA=False, clearB=False) -> SpDCCols:
+    """mtSpGEMM.h:74-202 (heap SpGEMM) -- same numeric contract as the hybrid."""
+    return _spgemm(SR, A, B, clearA, clearB)
+
+
+def estimateFLOPandNNZ(A: SpDCCols, B: SpDCCols, per_column=False):
+    """estimateFLOP (mtSpGEMM.h:1057-1134) + estimateNNZ_Hash (:806-933).
+    Returns (flops, nnzC) or, with per_column, (flops, nnzC, colflop, colnnz) as torch tensors."""
+    f, z = ctypes.c_int64(), ctypes.c_int64()
+    cf = cz = None
+    pf = pz = None
+    if per_column:
+        import torch
+        cf = torch.empty(B.nzc, dtype=torch.int64, device=A.ctx.tdevice)
+        cz = torch.empty(B.nzc, dtype=torch.int64, device=A.ctx.tdevice)
+        pf, pz = ctypes.c_void_p(cf.data_ptr()), ctypes.c_void_p(cz.data_ptr())
+    check(lib().cbh_spgemm_symbolic(A.ctx.h, A.h, B.h, ctypes.byref(f), ctypes.byref(z), pf, pz), A.ctx.h)
+    return (f.value, z.value, cf, cz) if per_column else (f.value, z.value)
+
+
+def EstimateLocalFLOP(SR: Semiring, A: SpDCCols, B: SpDCCols, clearA=False, clearB=False) -> int:
+    """mtSpGEMM.h:662-689"""
+    return estimateFLOPandNNZ(A, B)[0]
+
+
+def MultiwayMerge(SR: Semiring, lists, mdim=0, ndim=0, delarrs=False) -> SpDCCols:
+    """MultiwayMerge.h:411-526 -- merge column-sorted partials, SR::add on duplicates."""
+    if len(lists) == 0:
+        raise ValueError("MultiwayMerge of zero lists")
+    ctx = lists[0].ctx
+    for L in lists:
+        if (mdim or ndim) and (L.m != mdim or L.n != ndim):
+            raise _lib.CombBLASHipError(3002, "Dimensions of SpTuples do not match on multiwayMerge()")
+    cur = list(lists)
+    # the kernel merges up to 16 lists at once; larger fan-in is merged hierarchically
+    while len(cur) > 1 or cur is lists:
+        nxt = []
+        for i in range(0, len(cur), 16):
+            grp = cur[i:i + 16]
+            arr = (ctypes.c_void_p * len(grp))(*[g.h.value for g in grp])
+            h = ctypes.c_void_p()
+            check(lib().cbh_merge(ctx.h, SR.code, len(grp), arr, ctypes.byref(h)), ctx.h)
+            nxt.append(SpDCCols(ctx, h))
+        if cur is not lists:
+            for g in cur:
+                g.free()
+        cur = nxt
+    if delarrs:
+        for L in lists:
+            L.free()
+    return cur[0]
+
+
+def PhasedSpGEMM(SR: Semiring, A: SpDCCols, B: SpDCCols, checksum=False, budget_bytes=None):
+    """MemEfficientSpGEMM's phase loop (ParFriends.h:449-730) for one block: B's columns are
+    processed in phases sized from the exact symbolic pass; each phase's C block is materialised
+    in HBM then its buffer reused. Returns {flops, nnz, phases, value_sum, digest}."""
+    if budget_bytes is not None:
+        A.ctx.set_phase_budget(budget_bytes)
+    st = _lib.cbh_phase_stats()
+    flags = _lib.CBH_PHASE_CHECKSUM if checksum else 0
+    check(lib().cbh_spgemm_phased(A.ctx.h, SR.code, A.h, B.h, flags, ctypes.byref(st)), A.ctx.h)
+    return {"flops": st.flops, "nnz": st.nnz, "phases": st.phases, "value_sum": st.value_sum,
+            "digest": st.digest}

@@ -1,0 +1,183 @@
+/*
+ * combblas_hip.h — C-ABI of the MI355X (gfx950) semiring SpGEMM hot path.
+ *
+ * Plain pointers and sizes only (no torch / no C++ types). The C++ drop-in adaptor
+ * (include/combblas_hip/HipSpGEMM.h) and the Python host mirror (combblas_amd/) both
+ * sit on top of this interface. Every entry point names the reference interface it
+ * replaces:
+ *
+ *   cbh_spgemm            LocalHybridSpGEMM<SR,NTO>        include/CombBLAS/mtSpGEMM.h:213-460
+ *                         LocalSpGEMMHash<SR,NTO>(sort)     include/CombBLAS/mtSpGEMM.h:463-656
+ *                         LocalSpGEMM<SR,NTO> (heap)        include/CombBLAS/mtSpGEMM.h:74-202
+ *   cbh_spgemm_symbolic   estimateFLOP + estimateNNZ_Hash   include/CombBLAS/mtSpGEMM.h:1057-1134, 806-933
+ *                         (+ prefixsum, mtSpGEMM.h:23-70)
+ *   cbh_merge             MultiwayMerge<SR>                 include/CombBLAS/MultiwayMerge.h:411-526
+ *                         MultiwayMergeHash<SR>             include/CombBLAS/MultiwayMerge.h:536-684
+ *   cbh_mat_*             SpDCCols / Dcsc storage           include/CombBLAS/dcsc.h:124-130,
+ *                         (GetEssentials / Create)           SpDCCols.cpp:46,787-845
+ *   cbh_spgemm_phased     MemEfficientSpGEMM phase loop     include/CombBLAS/ParFriends.h:449-730
+ *                         (B split into column phases, SpDCCols::ColSplit SpDCCols.cpp:936-1090)
+ *   cbh_rmat_edges        RefGen21::make_graph (packed)     include/CombBLAS/RefGen21.h:246-301
+ *   cbh_edges_to_csc      SpParMat(DistEdgeList, removeloops) SpParMat.cpp:3140-3253, SpTuples.cpp:70-118
+ *
+ * Status codes mirror the reference's MPI_Abort codes (include/CombBLAS/SpDefs.h:72-78):
+ * 0 ok, 3001 GRIDMISMATCH, 3002 DIMMISMATCH, 3005 MATRIXALIAS, plus CBH_E_* below.
+ * Threading: one host thread per context (the reference calls the kernel from one thread
+ * per MPI rank). The library never calls MPI.
+ */
+#ifndef COMBBLAS_HIP_H
+#define COMBBLAS_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- status codes */
+#define CBH_OK 0
+#define CBH_E_GRIDMISMATCH 3001 /* SpDefs.h GRIDMISMATCH */
+#define CBH_E_DIMMISMATCH 3002  /* SpDefs.h DIMMISMATCH: A.getncol() != B.getnrow(), bad sizes */
+#define CBH_E_MATRIXALIAS 3005  /* SpDefs.h MATRIXALIAS */
+#define CBH_E_HIP 4001          /* a HIP runtime call failed (see cbh_last_error) */
+#define CBH_E_OOM 4002          /* device allocation failed */
+#define CBH_E_ARG 4003          /* invalid argument (null pointer, unknown semiring/dtype) */
+#define CBH_E_INTERNAL 4004     /* a device-side consistency check failed */
+#define CBH_E_NODEVICE 4005     /* no HIP device visible */
+
+/* ---------------------------------------------------------------- semirings / value types
+ * Built-in semirings (Semirings.h). The value type is both input and output type
+ * (T1 == T2 == T_promote), as in every hot-path call site listed in SURVEY.md §8(a).   */
+typedef enum cbh_semiring {
+  CBH_SR_PLUS_TIMES = 0, /* PlusTimesSRing<T,T>   Semirings.h:212-232 */
+  CBH_SR_SELECT_MAX = 1, /* SelectMaxSRing<T,T>   Semirings.h:165-187: add=max, multiply=a*b */
+  CBH_SR_MIN_PLUS = 2,   /* MinPlusSRing<T,T>     Semirings.h:235-255: add=min, multiply=inf_plus */
+  CBH_SR_OR_AND = 3,     /* boolean OR-AND (PlusTimesSRing<bool,bool>, KTipsSR) */
+  CBH_SR_SELECT_2ND = 4  /* Select2ndSRing<T,T,T> Semirings.h:143-163 (non-commutative add) */
+} cbh_semiring;
+
+typedef enum cbh_dtype {
+  CBH_F64 = 0,  /* double  */
+  CBH_I64 = 1,  /* int64_t */
+  CBH_BOOL = 2, /* bool, one byte per value */
+  CBH_F32 = 3,  /* float   */
+  CBH_I32 = 4   /* int32_t */
+} cbh_dtype;
+
+/* cbh_spgemm flags */
+#define CBH_SORTED_ROWS 0x1u   /* rows sorted within each column (LocalHybridSpGEMM, LocalSpGEMMHash sort=true) */
+#define CBH_KEEP_EMPTY_COLS 0x2u /* keep C columns of B's nzc even when empty (SpTuples view); default drops them (DCSC) */
+
+/* ---------------------------------------------------------------- matrices
+ * A local sparse block in DCSC form (combblas::Dcsc: cp[nzc+1], jc[nzc], ir[nnz], numx[nnz]).
+ * Row ids are local 32-bit (a local block has < 2^31 rows); column pointers and nnz are 64-bit. */
+typedef struct cbh_dcsc {
+  int64_t m, n;      /* SpDCCols::getnrow()/getncol() */
+  int64_t nnz, nzc;  /* SpDCCols::getnnz()/getnzc() */
+  const int64_t* cp; /* nzc+1 */
+  const int64_t* jc; /* nzc   */
+  const int32_t* ir; /* nnz   */
+  const void* num;   /* nnz values of dtype */
+} cbh_dcsc;
+
+typedef struct cbh_ctx cbh_ctx; /* one device + one stream + a stream-ordered memory pool */
+typedef struct cbh_mat cbh_mat; /* a device-resident DCSC block */
+
+int cbh_ctx_create(int device, cbh_ctx** ctx);
+int cbh_ctx_destroy(cbh_ctx* ctx);
+/* Use an existing hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = own stream. */
+int cbh_ctx_set_stream(cbh_ctx* ctx, void* hip_stream);
+void* cbh_ctx_stream(cbh_ctx* ctx);
+int cbh_ctx_synchronize(cbh_ctx* ctx);
+const char* cbh_last_error(cbh_ctx* ctx);
+/* Route every device allocation of this context through caller callbacks (e.g. the torch
+ * caching allocator), stream-ordered on `stream`. NULL alloc restores hipMallocAsync.        */
+typedef void* (*cbh_alloc_fn)(void* user, int64_t bytes, void* stream);
+typedef void (*cbh_free_fn)(void* user, void* ptr, void* stream);
+int cbh_ctx_set_allocator(cbh_ctx* ctx, cbh_alloc_fn alloc, cbh_free_fn release, void* user);
+/* Workspace budget for cbh_spgemm_phased (bytes of output buffer per phase); 0 = auto. */
+int cbh_ctx_set_phase_budget(cbh_ctx* ctx, int64_t bytes);
+
+/* Copy a host DCSC into a new device matrix (SpParHelper::BCastMatrix receive side / upload). */
+int cbh_mat_upload(cbh_ctx* ctx, const cbh_dcsc* host, cbh_dtype dtype, cbh_mat** out);
+/* Wrap device arrays without copying. The caller keeps them alive until cbh_mat_free. */
+int cbh_mat_wrap_device(cbh_ctx* ctx, const cbh_dcsc* dev, cbh_dtype dtype, cbh_mat** out);
+/* Sizes (host pointers, any may be NULL). */
+int cbh_mat_info(const cbh_mat* mat, int64_t* m, int64_t* n, int64_t* nnz, int64_t* nzc, int* dtype);
+/* Device pointers of the matrix arrays (valid until cbh_mat_free). */
+int cbh_mat_device_arrays(const cbh_mat* mat, const int64_t** cp, const int64_t** jc,
+                          const int32_t** ir, const void** num);
+/* Copy the matrix arrays to caller buffers; dst_on_device selects hipMemcpy direction. */
+int cbh_mat_copy_out(cbh_ctx* ctx, const cbh_mat* mat, int64_t* cp, int64_t* jc, int32_t* ir,
+                     void* num, int dst_on_device);
+int cbh_mat_free(cbh_ctx* ctx, cbh_mat* mat);
+
+/* ---------------------------------------------------------------- the hot path
+ * C = A * B over semiring sr. A, B, C share dtype. C is a new device matrix (caller frees).
+ * Output contract = LocalHybridSpGEMM's SpTuples converted to SpDCCols: columns in B's
+ * order, rows ascending within each column, explicit zeros kept, empty columns dropped
+ * unless CBH_KEEP_EMPTY_COLS.                                                            */
+int cbh_spgemm(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh_mat* B, uint32_t flags,
+               cbh_mat** C);
+/* Symbolic only: total flops (estimateFLOP) and exact nnz(C) (estimateNNZ_Hash).
+ * Optional per-column outputs (device pointers, length B.nzc) may be NULL.               */
+int cbh_spgemm_symbolic(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, int64_t* flops,
+                        int64_t* nnzC, int64_t* col_flops_dev, int64_t* col_nnz_dev);
+/* k-way merge of column-sorted partial products with SR::add on duplicates. */
+int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* parts, cbh_mat** C);
+
+/* Phased C = A * B for products larger than HBM: B's columns are processed in phases whose
+ * output fits the phase budget; each phase's C block is materialised in device memory and
+ * folded into the statistics below, then its buffer is reused. */
+typedef struct cbh_phase_stats {
+  int64_t flops;        /* number of SR::multiply calls (EstimateFLOP) */
+  int64_t nnz;          /* nnz(C) */
+  int64_t phases;       /* number of column phases used */
+  double value_sum;     /* sum of C's values as double (checksum) */
+  uint64_t digest;      /* order-sensitive digest of (col,row,value bits) in C order */
+} cbh_phase_stats;
+#define CBH_PHASE_CHECKSUM 0x100u /* also compute value_sum/digest (extra read of each phase) */
+int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh_mat* B,
+                      uint32_t flags, cbh_phase_stats* stats);
+
+/* Timing of the last cbh_spgemm/cbh_spgemm_phased call, per kernel class, measured with
+ * hipEvents on the context stream (milliseconds; -1 when not recorded).                  */
+typedef struct cbh_kernel_times {
+  double symbolic_ms, numeric_ms, total_ms;
+  int64_t numeric_launches;
+} cbh_kernel_times;
+int cbh_last_kernel_times(cbh_ctx* ctx, cbh_kernel_times* t);
+int cbh_ctx_enable_timing(cbh_ctx* ctx, int enable);
+
+/* Per-kernel-class totals accumulated while timing is enabled: HIP-event time of every launch,
+ * launch count, and the ALGORITHMIC bytes those launches processed (SURVEY.md §8(d):
+ * (s_i+s_v)*(nnz(B)+flops+nnz(C)) + column pointers; the symbolic pass counts row ids only).  */
+#define CBH_K_SYM_LARGE 0 /* tile_kernel<...,8192,512,512,MODE_SYM>  */
+#define CBH_K_SYM_SMALL 1 /* tile_kernel<...,512,128,256,MODE_SYM>   */
+#define CBH_K_NUM_LARGE 2 /* tile_kernel<SR,4096,512,512,MODE_NUM>   */
+#define CBH_K_NUM_SMALL 3 /* tile_kernel<SR,512,128,256,MODE_NUM>    */
+#define CBH_K_MERGE_SYM 4
+#define CBH_K_MERGE_NUM 5
+#define CBH_K_NKINDS 6
+typedef struct cbh_kernel_stat {
+  double ms;
+  int64_t launches;
+  double alg_bytes;
+} cbh_kernel_stat;
+int cbh_kernel_stats(cbh_ctx* ctx, int kind, cbh_kernel_stat* out);
+int cbh_kernel_stats_reset(cbh_ctx* ctx);
+
+/* ---------------------------------------------------------------- inputs (host side) */
+int cbh_rmat_edges(int scale, uint64_t userseed, int64_t start_edge, int64_t end_edge, int64_t* src,
+                   int64_t* dst);
+int cbh_edges_to_csc(int64_t m, int64_t n, int64_t nedges, const int64_t* rows, const int64_t* cols,
+                     int removeloops, int64_t* colptr, int32_t* rowidx, int64_t* count,
+                     int64_t* nnz_out);
+
+/* Library version / build tag (for logs). */
+const char* cbh_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* COMBBLAS_HIP_H */

@@ -1,0 +1,296 @@
+// TEST INFRASTRUCTURE ONLY. Built by oracle/Makefile against the reference sources
+// under $(COMBBLAS_REF) (default /root/reference) into oracle/_ref/ref_harness.
+// Nothing in the product library links or calls this.
+//
+// It drives the reference's own code so that the CPU restatement (oracle/spgemm_oracle.cpp)
+// and the HIP path can be pinned against it:
+//   gen   <scale> <ef> <out.cbm>                      DistEdgeList::GenGraph500Data(packed) +
+//                                                     SpParMat(DEL, removeloops=false)  (TC.cpp:139-148)
+//   mult  <sr> <kernel> <A.cbm> <B.cbm> <out.cbm>     LocalHybridSpGEMM / LocalSpGEMMHash / LocalSpGEMM
+//                                                     (mtSpGEMM.h:74,213,463)
+//   merge <sr> <out.cbm> <in1.cbm> ...                MultiwayMerge (MultiwayMerge.h:411)
+//   synch <sr> <A.cbm> <B.cbm> <out.cbm|-> [reps]     Mult_AnXBn_Synch on a 1x1 grid (ParFriends.h:1004),
+//                                                     prints wall time per call (MPI_Wtime)
+//   slice <scale> <ef> <col0> <col1> <reps> <sr>      CPU baseline: A (scale, ef) times the column block
+//                                                     A(:, col0:col1) with Mult_AnXBn_Synch; prints JSON
+// sr: pt_f64 | pt_i64 | max_i64 | min_i64 | bool ; kernel: hybrid | hash | hashu | heap
+#include <mpi.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "CombBLAS/CombBLAS.h"
+#include "cbm_io.h"
+
+using namespace combblas;
+
+// Globals some reference translation units expect to be defined by the application.
+double cblas_alltoalltime, cblas_allgathertime, cblas_mergeconttime, cblas_transvectime, cblas_localspmvtime;
+MTRand GlobalMT(123);
+
+// Boolean OR-AND semiring with the same contract as the test-defined KTipsSR
+// (ReleaseTests/KTipsTest.cpp:12-20).
+template <class T>
+struct OrAndSRing {
+  static T id() { return static_cast<T>(0); }
+  static bool returnedSAID() { return false; }
+  static MPI_Op mpi_op() { return MPI_LOR; }
+  static T add(const T& a, const T& b) { return (a || b); }
+  static T multiply(const T& a, const T& b) { return (a && b); }
+  static void axpy(T a, const T& x, T& y) { y = add(y, multiply(a, x)); }
+};
+
+template <class NT>
+static NT value_of(const cbm::Dcsc& d, int64_t i) {
+  return d.vtype == cbm::F64 ? static_cast<NT>(d.vf[i]) : static_cast<NT>(d.vi[i]);
+}
+
+template <class NT>
+static uint32_t vtype_of() {
+  if (std::is_same<NT, double>::value) return cbm::F64;
+  if (std::is_same<NT, bool>::value) return cbm::U8;
+  return cbm::I64;
+}
+
+template <class NT>
+static SpDCCols<int64_t, NT>* to_spdccols(const cbm::Dcsc& d) {
+  if (d.nnz() == 0) return new SpDCCols<int64_t, NT>(0, d.m, d.n, 0);
+  auto* s = new SpDCCols<int64_t, NT>(d.nnz(), d.m, d.n, d.nzc());
+  Dcsc<int64_t, NT>* dc = s->GetDCSC();
+  for (int64_t i = 0; i < d.nzc(); ++i) dc->jc[i] = d.jc[i];
+  for (int64_t i = 0; i <= d.nzc(); ++i) dc->cp[i] = d.cp[i];
+  for (int64_t i = 0; i < d.nnz(); ++i) {
+    dc->ir[i] = d.ir[i];
+    dc->numx[i] = value_of<NT>(d, i);
+  }
+  return s;
+}
+
+template <class NT>
+static cbm::Dcsc from_spdccols(const SpDCCols<int64_t, NT>& s) {
+  cbm::Dcsc d;
+  d.vtype = vtype_of<NT>();
+  d.m = s.getnrow();
+  d.n = s.getncol();
+  if (s.getnnz() == 0) {
+    d.cp.push_back(0);
+    return d;
+  }
+  Dcsc<int64_t, NT>* dc = s.GetDCSC();
+  d.jc.assign(dc->jc, dc->jc + dc->nzc);
+  d.cp.assign(dc->cp, dc->cp + dc->nzc + 1);
+  d.ir.resize(dc->nz);
+  for (int64_t i = 0; i < dc->nz; ++i) d.ir[i] = (int32_t)dc->ir[i];
+  if (d.vtype == cbm::F64) {
+    d.vf.resize(dc->nz);
+    for (int64_t i = 0; i < dc->nz; ++i) d.vf[i] = (double)dc->numx[i];
+  } else {
+    d.vi.resize(dc->nz);
+    for (int64_t i = 0; i < dc->nz; ++i) d.vi[i] = (int64_t)dc->numx[i];
+  }
+  return d;
+}
+
+template <class NT>
+static cbm::Dcsc from_sptuples(SpTuples<int64_t, NT>* t) {
+  // Column-sorted tuples -> DCSC in the tuples' own order (SpDCCols.cpp:109-183).
+  SpDCCols<int64_t, NT> s(*t, false);
+  return from_spdccols<NT>(s);
+}
+
+static double now() { return MPI_Wtime(); }
+
+template <class SR, class NT>
+static int do_mult(const std::string& kernel, const std::string& fa, const std::string& fb, const std::string& fo) {
+  cbm::Dcsc a = cbm::read(fa), b = cbm::read(fb);
+  SpDCCols<int64_t, NT>* A = to_spdccols<NT>(a);
+  SpDCCols<int64_t, NT>* B = to_spdccols<NT>(b);
+  SpTuples<int64_t, NT>* C = nullptr;
+  double t0 = now();
+  if (kernel == "hybrid")
+    C = LocalHybridSpGEMM<SR, NT>(*A, *B, false, false);
+  else if (kernel == "hash")
+    C = LocalSpGEMMHash<SR, NT>(*A, *B, false, false, true);
+  else if (kernel == "hashu")
+    C = LocalSpGEMMHash<SR, NT>(*A, *B, false, false, false);
+  else if (kernel == "heap")
+    C = LocalSpGEMM<SR, NT>(*A, *B, false, false);
+  else {
+    std::fprintf(stderr, "unknown kernel %s\n", kernel.c_str());
+    return 2;
+  }
+  double t1 = now();
+  std::fprintf(stderr, "kernel=%s nnzC=%lld time=%.6f\n", kernel.c_str(), (long long)C->getnnz(), t1 - t0);
+  cbm::write(fo, from_sptuples<NT>(C));
+  delete C;
+  delete A;
+  delete B;
+  return 0;
+}
+
+template <class SR, class NT>
+static int do_merge(const std::string& fo, const std::vector<std::string>& ins) {
+  std::vector<SpTuples<int64_t, NT>*> lists;
+  int64_t m = 0, n = 0;
+  for (auto& f : ins) {
+    cbm::Dcsc d = cbm::read(f);
+    m = d.m;
+    n = d.n;
+    SpDCCols<int64_t, NT>* s = to_spdccols<NT>(d);
+    lists.push_back(new SpTuples<int64_t, NT>(*s));
+    delete s;
+  }
+  SpTuples<int64_t, NT>* C = MultiwayMerge<SR>(lists, m, n, true);
+  cbm::write(fo, from_sptuples<NT>(C));
+  if (lists.size() != 1) delete C;
+  return 0;
+}
+
+template <class SR, class NT>
+static int do_synch(const std::string& fa, const std::string& fb, const std::string& fo, int reps) {
+  typedef SpDCCols<int64_t, NT> DER;
+  std::shared_ptr<CommGrid> grid(new CommGrid(MPI_COMM_WORLD, 0, 0));
+  cbm::Dcsc a = cbm::read(fa), b = cbm::read(fb);
+  SpParMat<int64_t, NT, DER> A(to_spdccols<NT>(a), grid);
+  SpParMat<int64_t, NT, DER> B(to_spdccols<NT>(b), grid);
+  SpParMat<int64_t, NT, DER> C = Mult_AnXBn_Synch<SR, NT, DER>(A, B);  // warm-up
+  for (int r = 0; r < reps; ++r) {
+    double t0 = now();
+    C = Mult_AnXBn_Synch<SR, NT, DER>(A, B);
+    double t1 = now();
+    std::printf("synch_time %.6f\n", t1 - t0);
+  }
+  if (fo != "-") cbm::write(fo, from_spdccols<NT>(C.seq()));
+  return 0;
+}
+
+static SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>>* gen_rmat(int scale, int ef) {
+  double init[4] = {.57, .19, .19, .05};
+  DistEdgeList<int64_t>* DEL = new DistEdgeList<int64_t>();
+  DEL->GenGraph500Data(init, scale, ef, true, true);
+  auto* A = new SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>>(*DEL, false);
+  delete DEL;
+  return A;
+}
+
+static int do_gen(int scale, int ef, const std::string& fo) {
+  auto* A = gen_rmat(scale, ef);
+  cbm::write(fo, from_spdccols<int64_t>(A->seq()));
+  delete A;
+  return 0;
+}
+
+// CPU baseline on a bounded column block of the north-star workload: C = A * A(:, c0:c1).
+template <class SR, class NT>
+static int do_slice(int scale, int ef, int64_t c0, int64_t c1, int reps) {
+  typedef SpDCCols<int64_t, NT> DER;
+  std::shared_ptr<CommGrid> grid(new CommGrid(MPI_COMM_WORLD, 0, 0));
+  double tg0 = now();
+  auto* G = gen_rmat(scale, ef);
+  double tg1 = now();
+  cbm::Dcsc a = from_spdccols<int64_t>(G->seq());
+  delete G;
+  // B = A(:, c0:c1) keeping all n columns (empty outside the block), as a ColSplit piece would.
+  cbm::Dcsc b;
+  b.vtype = a.vtype;
+  b.m = a.m;
+  b.n = a.n;
+  b.cp.push_back(0);
+  for (int64_t i = 0; i < a.nzc(); ++i) {
+    if (a.jc[i] < c0 || a.jc[i] >= c1) continue;
+    b.jc.push_back(a.jc[i]);
+    for (int64_t p = a.cp[i]; p < a.cp[i + 1]; ++p) {
+      b.ir.push_back(a.ir[p]);
+      b.vi.push_back(a.vi[p]);
+    }
+    b.cp.push_back((int64_t)b.ir.size());
+  }
+  SpParMat<int64_t, NT, DER> A(to_spdccols<NT>(a), grid);
+  SpParMat<int64_t, NT, DER> B(to_spdccols<NT>(b), grid);
+  int64_t flops = EstimateFLOP<SR>(A, B);
+  std::vector<double> ts;
+  int64_t nnzc = 0;
+  for (int r = 0; r < reps; ++r) {
+    double t0 = now();
+    SpParMat<int64_t, NT, DER> C = Mult_AnXBn_Synch<SR, NT, DER>(A, B);
+    double t1 = now();
+    ts.push_back(t1 - t0);
+    nnzc = C.getnnz();
+  }
+  std::sort(ts.begin(), ts.end());
+  double med = ts[ts.size() / 2];
+  int nthreads = 1;
+#ifdef THREADED
+#pragma omp parallel
+  {
+#pragma omp master
+    nthreads = omp_get_num_threads();
+  }
+#endif
+  std::printf("{\"flops\": %lld, \"nnzC\": %lld, \"median_s\": %.6f, \"min_s\": %.6f, \"reps\": %d, "
+              "\"gflops\": %.6f, \"threads\": %d, \"gen_s\": %.3f, \"col0\": %lld, \"col1\": %lld}\n",
+              (long long)flops, (long long)nnzc, med, ts[0], reps, 2.0 * flops / med / 1e9, nthreads, tg1 - tg0,
+              (long long)c0, (long long)c1);
+  return 0;
+}
+
+#define DISPATCH_SR(sr, CALL)                                                   \
+  if (sr == "pt_f64") {                                                         \
+    typedef PlusTimesSRing<double, double> SR;                                  \
+    typedef double NT;                                                          \
+    return CALL;                                                                \
+  } else if (sr == "pt_i64") {                                                  \
+    typedef PlusTimesSRing<int64_t, int64_t> SR;                                \
+    typedef int64_t NT;                                                         \
+    return CALL;                                                                \
+  } else if (sr == "max_i64") {                                                 \
+    typedef SelectMaxSRing<int64_t, int64_t> SR;                                \
+    typedef int64_t NT;                                                         \
+    return CALL;                                                                \
+  } else if (sr == "min_i64") {                                                 \
+    typedef MinPlusSRing<int64_t, int64_t> SR;                                  \
+    typedef int64_t NT;                                                         \
+    return CALL;                                                                \
+  } else if (sr == "bool") {                                                    \
+    typedef OrAndSRing<bool> SR;                                                \
+    typedef bool NT;                                                            \
+    return CALL;                                                                \
+  }
+
+static int run(int argc, char** argv) {
+  if (argc < 2) return 2;
+  std::string mode = argv[1];
+  if (mode == "gen" && argc == 5) return do_gen(std::atoi(argv[2]), std::atoi(argv[3]), argv[4]);
+  if (mode == "mult" && argc == 7) {
+    std::string sr = argv[2];
+    DISPATCH_SR(sr, (do_mult<SR, NT>(argv[3], argv[4], argv[5], argv[6])));
+  }
+  if (mode == "merge" && argc >= 5) {
+    std::string sr = argv[2];
+    std::vector<std::string> ins(argv + 4, argv + argc);
+    DISPATCH_SR(sr, (do_merge<SR, NT>(argv[3], ins)));
+  }
+  if (mode == "synch" && argc >= 6) {
+    std::string sr = argv[2];
+    int reps = argc > 6 ? std::atoi(argv[6]) : 1;
+    DISPATCH_SR(sr, (do_synch<SR, NT>(argv[3], argv[4], argv[5], reps)));
+  }
+  if (mode == "slice" && argc == 8) {
+    std::string sr = argv[7];
+    DISPATCH_SR(sr, (do_slice<SR, NT>(std::atoi(argv[2]), std::atoi(argv[3]), std::atoll(argv[4]),
+                                      std::atoll(argv[5]), std::atoi(argv[6]))));
+  }
+  std::fprintf(stderr, "bad arguments\n");
+  return 2;
+}
+
+int main(int argc, char** argv) {
+  MPI_Init(&argc, &argv);
+  int rc = run(argc, argv);
+  MPI_Finalize();
+  return rc;
+}
