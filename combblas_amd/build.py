@@ -29,7 +29,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB
     cmd = [HIPCC, "-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17", "-Wall",
-           "-Wno-unused-function", "-o", LIB + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES] + ["-lpthread"]
+           "-Wno-unused-function", "-Wl,-soname,libcombblas_hip.so", "-o", LIB + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES] + ["-lpthread"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd, cwd=CSRC)

@@ -1,0 +1,252 @@
+// HipSpGEMM.h -- C++ drop-in adaptor: CombBLAS's local SpGEMM entry points on the gfx950 path.
+//
+// Include AFTER "CombBLAS/CombBLAS.h". It provides
+//   combblas_hip::LocalHybridSpGEMM<SR,NTO>(A, B, clearA, clearB, aux)   (mtSpGEMM.h:213-217)
+//   combblas_hip::LocalSpGEMMHash<SR,NTO>(A, B, clearA, clearB, sort)    (mtSpGEMM.h:463-467)
+//   combblas_hip::LocalSpGEMM<SR,NTO>(A, B, clearA, clearB)              (mtSpGEMM.h:74-78)
+//   combblas_hip::MultiwayMerge<SR>(ArrSpTups, mdim, ndim, delarrs)      (MultiwayMerge.h:411-412)
+// with the reference signatures and ownership rules (heap SpTuples* the caller deletes, tuples
+// allocated with ::operator new and flagged isOperatorNew, clearA/clearB delete the inputs,
+// delarrs deletes the merged lists), and the macro
+//   COMBBLAS_HIP_INSTANTIATE(SR, IT, NT)
+// that declares explicit specializations of combblas::LocalHybridSpGEMM / LocalSpGEMMHash /
+// LocalSpGEMM / MultiwayMerge for that semiring and types, so that the UNCHANGED reference
+// drivers (PSpGEMM -> Mult_AnXBn_Synch, ParFriends.h:1004-1108; MemEfficientSpGEMM; the 3D
+// drivers) instantiate the HIP versions. Use it at namespace scope, after this header and before
+// the first call that instantiates a driver. Built-in semirings map to device functors through
+// combblas_hip::semiring_traits (specialize it for a user semiring whose device functor exists).
+//
+// All device work goes through the C-ABI in combblas_hip.h; link with libcombblas_hip.so.
+// Errors raise MPI_Abort with the library's code (3001/3002/3005 mirror SpDefs.h), as the
+// reference drivers do (ParFriends.h:160-181).
+#pragma once
+
+#include <mpi.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <tuple>
+#include <type_traits>
+#include <vector>
+
+#include "../combblas_hip.h"
+
+namespace combblas_hip {
+
+// ------------------------------------------------------------------ type/semiring mapping
+template <class NT>
+struct dtype_of;
+template <> struct dtype_of<double> { static constexpr cbh_dtype value = CBH_F64; };
+template <> struct dtype_of<int64_t> { static constexpr cbh_dtype value = CBH_I64; };
+template <> struct dtype_of<float> { static constexpr cbh_dtype value = CBH_F32; };
+template <> struct dtype_of<int32_t> { static constexpr cbh_dtype value = CBH_I32; };
+template <> struct dtype_of<bool> { static constexpr cbh_dtype value = CBH_BOOL; };
+
+template <class SR>
+struct semiring_traits;  // specialize: static constexpr cbh_semiring code
+template <class T1, class T2>
+struct semiring_traits<combblas::PlusTimesSRing<T1, T2>> { static constexpr cbh_semiring code = CBH_SR_PLUS_TIMES; };
+template <class T1, class T2>
+struct semiring_traits<combblas::SelectMaxSRing<T1, T2>> { static constexpr cbh_semiring code = CBH_SR_SELECT_MAX; };
+template <class T1, class T2>
+struct semiring_traits<combblas::MinPlusSRing<T1, T2>> { static constexpr cbh_semiring code = CBH_SR_MIN_PLUS; };
+
+inline void die(cbh_ctx* ctx, int rc, const char* what) {
+  std::fprintf(stderr, "combblas_hip: %s failed (%d): %s\n", what, rc, ctx ? cbh_last_error(ctx) : "");
+  MPI_Abort(MPI_COMM_WORLD, rc);
+}
+
+// One context per process (one rank drives one GPU, CommGrid semantics). Device = local rank
+// modulo visible devices unless COMBBLAS_HIP_DEVICE is set.
+inline cbh_ctx* context() {
+  static cbh_ctx* ctx = nullptr;
+  if (!ctx) {
+    int dev = 0;
+    if (const char* e = std::getenv("COMBBLAS_HIP_DEVICE")) dev = std::atoi(e);
+    else if (const char* l = std::getenv("LOCAL_RANK")) dev = std::atoi(l);
+    else if (const char* m = std::getenv("MPI_LOCALRANKID")) dev = std::atoi(m);
+    int rc = cbh_ctx_create(dev, &ctx);
+    if (rc != CBH_OK) rc = cbh_ctx_create(0, &ctx);
+    if (rc != CBH_OK) die(nullptr, rc, "cbh_ctx_create");
+  }
+  return ctx;
+}
+
+struct MatGuard {
+  cbh_mat* m = nullptr;
+  ~MatGuard() {
+    if (m) cbh_mat_free(context(), m);
+  }
+};
+
+// SpDCCols<IT,NT> (Dcsc arrays) -> device matrix. Row ids narrowed to the local int32 layout.
+template <class IT, class NT>
+cbh_mat* upload(const combblas::SpDCCols<IT, NT>& A) {
+  cbh_dcsc h{};
+  h.m = A.getnrow();
+  h.n = A.getncol();
+  h.nnz = A.getnnz();
+  h.nzc = A.getnzc();
+  std::vector<int64_t> cp(1, 0), jc;
+  std::vector<int32_t> ir;
+  std::vector<unsigned char> num;
+  if (h.nnz > 0) {
+    combblas::Dcsc<IT, NT>* d = A.GetDCSC();
+    cp.assign(d->cp, d->cp + d->nzc + 1);
+    jc.assign(d->jc, d->jc + d->nzc);
+    ir.resize(d->nz);
+    for (IT i = 0; i < d->nz; ++i) ir[i] = static_cast<int32_t>(d->ir[i]);
+    num.resize(sizeof(NT) * d->nz);
+    std::memcpy(num.data(), d->numx, sizeof(NT) * d->nz);
+  }
+  h.cp = cp.data();
+  h.jc = jc.data();
+  h.ir = ir.data();
+  h.num = num.data();
+  if (h.m > std::numeric_limits<int32_t>::max()) die(context(), CBH_E_DIMMISMATCH, "local rows exceed int32");
+  cbh_mat* out = nullptr;
+  int rc = cbh_mat_upload(context(), &h, dtype_of<NT>::value, &out);
+  if (rc != CBH_OK) die(context(), rc, "cbh_mat_upload");
+  return out;
+}
+
+// column-sorted SpTuples -> device DCSC
+template <class IT, class NT>
+cbh_mat* upload(const combblas::SpTuples<IT, NT>& T) {
+  cbh_dcsc h{};
+  h.m = T.getnrow();
+  h.n = T.getncol();
+  h.nnz = T.getnnz();
+  std::vector<int64_t> cp(1, 0), jc;
+  std::vector<int32_t> ir(h.nnz);
+  std::vector<NT> num(h.nnz);
+  for (int64_t i = 0; i < h.nnz; ++i) {
+    const IT c = T.colindex(i);
+    if (jc.empty() || jc.back() != c) {
+      if (!jc.empty()) cp.push_back(i);
+      jc.push_back(c);
+    }
+    ir[i] = static_cast<int32_t>(T.rowindex(i));
+    num[i] = T.numvalue(i);
+  }
+  if (!jc.empty()) cp.push_back(h.nnz);
+  h.nzc = (int64_t)jc.size();
+  h.cp = cp.data();
+  h.jc = jc.data();
+  h.ir = ir.data();
+  h.num = reinterpret_cast<const void*>(num.data());
+  cbh_mat* out = nullptr;
+  int rc = cbh_mat_upload(context(), &h, dtype_of<NT>::value, &out);
+  if (rc != CBH_OK) die(context(), rc, "cbh_mat_upload");
+  return out;
+}
+
+// device DCSC -> SpTuples<IT,NT>* (column-sorted; ::operator new tuples, mtSpGEMM.h:272,453)
+template <class IT, class NT>
+combblas::SpTuples<IT, NT>* download_tuples(cbh_mat* C) {
+  int64_t m, n, nnz, nzc;
+  cbh_mat_info(C, &m, &n, &nnz, &nzc, nullptr);
+  std::vector<int64_t> cp(nzc + 1), jc(nzc);
+  std::vector<int32_t> ir(nnz);
+  std::vector<NT> num(nnz);
+  int rc = cbh_mat_copy_out(context(), C, cp.data(), jc.data(), ir.data(), reinterpret_cast<void*>(num.data()), 0);
+  if (rc != CBH_OK) die(context(), rc, "cbh_mat_copy_out");
+  if (nnz == 0) return new combblas::SpTuples<IT, NT>(0, (IT)m, (IT)n);
+  auto* tuples = static_cast<std::tuple<IT, IT, NT>*>(::operator new(sizeof(std::tuple<IT, IT, NT>) * nnz));
+  for (int64_t c = 0; c < nzc; ++c)
+    for (int64_t p = cp[c]; p < cp[c + 1]; ++p) tuples[p] = std::make_tuple((IT)ir[p], (IT)jc[c], num[p]);
+  return new combblas::SpTuples<IT, NT>(nnz, (IT)m, (IT)n, tuples, true, true);
+}
+
+template <class SR, class NTO, class IT, class NT1, class NT2>
+combblas::SpTuples<IT, NTO>* LocalHybridSpGEMM(const combblas::SpDCCols<IT, NT1>& A,
+                                               const combblas::SpDCCols<IT, NT2>& B, bool clearA, bool clearB,
+                                               IT* aux = nullptr) {
+  static_assert(std::is_same<NT1, NTO>::value && std::is_same<NT2, NTO>::value,
+                "device path: input and output value types must match (T1 == T2 == T_promote)");
+  (void)aux;
+  const IT mdim = A.getnrow(), ndim = B.getncol();
+  combblas::SpTuples<IT, NTO>* out;
+  if (A.isZero() || B.isZero()) {
+    out = new combblas::SpTuples<IT, NTO>(0, mdim, ndim);  // mtSpGEMM.h:224-227
+  } else {
+    MatGuard a, b, c;
+    a.m = upload(A);
+    b.m = upload(B);
+    int rc = cbh_spgemm(context(), semiring_traits<SR>::code, a.m, b.m, CBH_SORTED_ROWS, &c.m);
+    if (rc != CBH_OK) die(context(), rc, "cbh_spgemm");
+    out = download_tuples<IT, NTO>(c.m);
+  }
+  if (clearA) delete const_cast<combblas::SpDCCols<IT, NT1>*>(&A);
+  if (clearB) delete const_cast<combblas::SpDCCols<IT, NT2>*>(&B);
+  return out;
+}
+
+template <class SR, class NTO, class IT, class NT1, class NT2>
+combblas::SpTuples<IT, NTO>* LocalSpGEMMHash(const combblas::SpDCCols<IT, NT1>& A,
+                                             const combblas::SpDCCols<IT, NT2>& B, bool clearA, bool clearB,
+                                             bool sort = true) {
+  (void)sort;  // ascending rows are a valid order for the unsorted contract
+  return combblas_hip::LocalHybridSpGEMM<SR, NTO>(A, B, clearA, clearB);
+}
+
+template <class SR, class NTO, class IT, class NT1, class NT2>
+combblas::SpTuples<IT, NTO>* LocalSpGEMM(const combblas::SpDCCols<IT, NT1>& A, const combblas::SpDCCols<IT, NT2>& B,
+                                         bool clearA, bool clearB) {
+  return combblas_hip::LocalHybridSpGEMM<SR, NTO>(A, B, clearA, clearB);
+}
+
+template <class SR, class IT, class NT>
+combblas::SpTuples<IT, NT>* MultiwayMerge(std::vector<combblas::SpTuples<IT, NT>*>& lists, IT mdim = 0, IT ndim = 0,
+                                          bool delarrs = false) {
+  const int nlists = (int)lists.size();
+  if (nlists == 0) return new combblas::SpTuples<IT, NT>(0, mdim, ndim);
+  if (nlists == 1 && delarrs) return lists[0];  // MultiwayMerge.h:422-425 steals the input
+  for (int i = 0; i < nlists; ++i)
+    if (mdim != lists[i]->getnrow() || ndim != lists[i]->getncol()) {
+      std::fprintf(stderr, "Dimensions of SpTuples do not match on multiwayMerge()\n");
+      return new combblas::SpTuples<IT, NT>(0, 0, 0);
+    }
+  std::vector<MatGuard> g(nlists);
+  std::vector<const cbh_mat*> parts(nlists);
+  for (int i = 0; i < nlists; ++i) parts[i] = g[i].m = upload(*lists[i]);
+  MatGuard c;
+  int rc = cbh_merge(context(), semiring_traits<SR>::code, nlists, parts.data(), &c.m);
+  if (rc != CBH_OK) die(context(), rc, "cbh_merge");
+  combblas::SpTuples<IT, NT>* out = download_tuples<IT, NT>(c.m);
+  if (delarrs)
+    for (auto* l : lists) delete l;
+  return out;
+}
+
+}  // namespace combblas_hip
+
+// Route the reference's own drivers to the device path for (SR, IT, NT): explicit
+// specializations of the combblas:: function templates, forwarding to combblas_hip::.
+#define COMBBLAS_HIP_INSTANTIATE(SR, IT, NT)                                                                  \
+  namespace combblas {                                                                                        \
+  template <>                                                                                                 \
+  inline SpTuples<IT, NT>* LocalHybridSpGEMM<SR, NT, IT, NT, NT>(const SpDCCols<IT, NT>& A,                  \
+                                                                 const SpDCCols<IT, NT>& B, bool clearA,      \
+                                                                 bool clearB, IT* aux) {                      \
+    return combblas_hip::LocalHybridSpGEMM<SR, NT>(A, B, clearA, clearB, aux);                               \
+  }                                                                                                           \
+  template <>                                                                                                 \
+  inline SpTuples<IT, NT>* LocalSpGEMMHash<SR, NT, IT, NT, NT>(const SpDCCols<IT, NT>& A,                    \
+                                                               const SpDCCols<IT, NT>& B, bool clearA,        \
+                                                               bool clearB, bool sort) {                      \
+    return combblas_hip::LocalSpGEMMHash<SR, NT>(A, B, clearA, clearB, sort);                                \
+  }                                                                                                           \
+  template <>                                                                                                 \
+  inline SpTuples<IT, NT>* LocalSpGEMM<SR, NT, IT, NT, NT>(const SpDCCols<IT, NT>& A, const SpDCCols<IT, NT>& B, \
+                                                           bool clearA, bool clearB) {                        \
+    return combblas_hip::LocalSpGEMM<SR, NT>(A, B, clearA, clearB);                                          \
+  }                                                                                                           \
+  template <>                                                                                                 \
+  inline SpTuples<IT, NT>* MultiwayMerge<SR, IT, NT>(std::vector<SpTuples<IT, NT>*> & L, IT mdim, IT ndim,    \
+                                                     bool delarrs) {                                          \
+    return combblas_hip::MultiwayMerge<SR, IT, NT>(L, mdim, ndim, delarrs);                                  \
+  }                                                                                                           \
+  }
