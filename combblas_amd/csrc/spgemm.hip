@@ -12,7 +12,9 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -176,53 +178,60 @@ __global__ __launch_bounds__(256) void flop_kernel(const int64_t* __restrict__ A
   }
 }
 
-// Bins: 0 = no work, 1 = small (work <= small_cap), 2 + (kSub-1-lg) = large, lg = floor(log2 work):
-// laid out in bin order so the large list runs from the heaviest columns down.
+// Bins: 0 = no work, 1 = small (work <= cap1), 2 = mid (work <= cap2), 3 + (kSub-1-lg) = large,
+// lg = floor(log2 work): laid out in bin order so the large list runs from the heaviest columns down.
 constexpr int kSub = 48;
-constexpr int kNB = 2 + kSub;
+constexpr int kNB = 3 + kSub;
+constexpr int kGroups = 3;  // small, mid, large
 
-__device__ __forceinline__ int bin_of(int64_t w, int64_t small_cap) {
+struct BinCaps {
+  int64_t cap1, cap2;
+};
+
+__device__ __forceinline__ int bin_of(int64_t w, BinCaps k) {
   if (w <= 0) return 0;
-  if (w <= small_cap) return 1;
+  if (w <= k.cap1) return 1;
+  if (w <= k.cap2) return 2;
   int lg = 63 - __clzll((unsigned long long)w);
   if (lg > kSub - 1) lg = kSub - 1;
-  return 2 + (kSub - 1 - lg);
+  return 3 + (kSub - 1 - lg);
 }
+__device__ __forceinline__ int group_of(int b) { return b <= 1 ? 0 : (b == 2 ? 1 : 2); }
 
-// Optional per-group unit sums for the roofline (group 0 = small bin, 1 = large bins):
+// Optional per-group unit sums for the roofline (groups small/mid/large):
 // sums[g*3 + 0] = sum of B column lengths, [1] = flops, [2] = nnz(C).
-__global__ __launch_bounds__(256) void bin_count_kernel(const int64_t* __restrict__ work, int64_t n, int64_t small_cap,
+__global__ __launch_bounds__(256) void bin_count_kernel(const int64_t* __restrict__ work, int64_t n, BinCaps caps,
                                                         unsigned long long* __restrict__ counts,
                                                         const int64_t* __restrict__ Bcp, const int64_t* __restrict__ flop,
                                                         const int64_t* __restrict__ nnz,
                                                         unsigned long long* __restrict__ sums) {
   __shared__ unsigned int h[kNB];
-  __shared__ unsigned long long ssum[6];
+  __shared__ unsigned long long ssum[3 * kGroups];
   for (int i = threadIdx.x; i < kNB; i += blockDim.x) h[i] = 0;
-  if (threadIdx.x < 6) ssum[threadIdx.x] = 0;
+  if (threadIdx.x < 3 * kGroups) ssum[threadIdx.x] = 0;
   __syncthreads();
-  unsigned long long loc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long loc[3 * kGroups] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x) {
-    const int b = bin_of(work[c], small_cap);
+    const int b = bin_of(work[c], caps);
     atomicAdd(&h[b], 1u);
     if (sums && b > 0) {
-      const int g = (b == 1) ? 0 : 1;
+      const int g = group_of(b);
       loc[g * 3 + 0] += (unsigned long long)(Bcp ? Bcp[c + 1] - Bcp[c] : 0);
       loc[g * 3 + 1] += (unsigned long long)(flop ? flop[c] : 0);
       loc[g * 3 + 2] += (unsigned long long)(nnz ? nnz[c] : 0);
     }
   }
   if (sums)
-    for (int i = 0; i < 6; ++i)
+    for (int i = 0; i < 3 * kGroups; ++i)
       if (loc[i]) atomicAdd(&ssum[i], loc[i]);
   __syncthreads();
   for (int i = threadIdx.x; i < kNB; i += blockDim.x)
     if (h[i]) atomicAdd(&counts[i], (unsigned long long)h[i]);
-  if (sums && threadIdx.x < 6 && ssum[threadIdx.x]) atomicAdd(&sums[threadIdx.x], ssum[threadIdx.x]);
+  if (sums && threadIdx.x < 3 * kGroups && ssum[threadIdx.x]) atomicAdd(&sums[threadIdx.x], ssum[threadIdx.x]);
 }
 
 __global__ __launch_bounds__(256) void bin_scatter_kernel(const int64_t* __restrict__ work, int64_t n, int64_t col0,
-                                                          int64_t small_cap, unsigned long long* __restrict__ cursor,
+                                                          BinCaps caps, unsigned long long* __restrict__ cursor,
                                                           int32_t* __restrict__ cols) {
   __shared__ unsigned int h[kNB];
   __shared__ unsigned long long base[kNB];
@@ -232,7 +241,7 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(const int64_t* __restr
   int b = -1;
   unsigned int r = 0;
   if (c < n) {
-    b = bin_of(work[c], small_cap);
+    b = bin_of(work[c], caps);
     r = atomicAdd(&h[b], 1u);
   }
   __syncthreads();
@@ -350,12 +359,15 @@ __global__ __launch_bounds__(256) void checksum_kernel(const int64_t* __restrict
 }
 
 // ============================================================================ kernel configurations
-// symbolic: small (flop <= 256) one 128-thread block per column, 512-slot table;
-//           large: 512 threads, 8192-slot key table, row tiles of <= 4096 flops.
-// numeric : small (nnz <= 256) 512(+64)-slot table; large: 4096(+64) slots, tiles of <= 2048 rows.
+// symbolic: small (flop <= 256): 128 threads, 512-key hash; mid (flop <= 4096): 256 threads,
+//           8192-key hash, one tile; large: 512 threads, LDS bitmap of 12288 words = 393,216 rows
+//           per tile (heavy columns: <= 11 tiles at scale 22, exact, no hashing).
+// numeric : small (nnz <= 256) 512(+64)-slot table; large: 4096(+64) slots, tiles of <= 2048 outputs.
 constexpr int64_t kSmallCap = 256;
+constexpr int64_t kSymMidCap = 4096;
 struct SymSmall { static constexpr int T = 512, BS = 128, EMAX = 256; };
-struct SymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512; };
+struct SymMid { static constexpr int T = 8192, BS = 256, EMAX = 512; };
+struct SymBmp { static constexpr int T = 12288, BS = 512, EMAX = 512; };
 struct NumSmall { static constexpr int T = 512, BS = 128, EMAX = 256; };
 struct NumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512; };
 
@@ -423,24 +435,26 @@ static int launch_tile(cbh_ctx* ctx, const TileArgs& args, int64_t first, int64_
 
 // Bins the column slots [0, n) by work. Returns list offsets of the small and large groups.
 struct BinLists {
-  int64_t small_first = 0, small_count = 0, large_first = 0, large_count = 0;
-  double units[6] = {0, 0, 0, 0, 0, 0};  // [small|large] x [sum b_j, sum flop_j, sum nnz_j] (timing only)
+  int64_t small_first = 0, small_count = 0, mid_first = 0, mid_count = 0, large_first = 0, large_count = 0;
+  int64_t sub_count[kSub] = {0};  // large sub-bins, index = floor(log2 work)
+  double units[3 * kGroups] = {0};  // [small|mid|large] x [sum b_j, sum flop_j, sum nnz_j] (timing only)
 };
 // Unit sums are gathered only when the context records timings (bench/roofline); Bcp/flop/nnz
 // are indexed like `work` (already offset by col0 by the caller).
 static int make_bins(cbh_ctx* ctx, Scratch& S, const int64_t* work, int64_t n, int64_t col0, int32_t* cols,
-                     BinLists* out, const int64_t* Bcp = nullptr, const int64_t* flop = nullptr,
+                     BinLists* out, BinCaps caps, const int64_t* Bcp = nullptr, const int64_t* flop = nullptr,
                      const int64_t* nnz = nullptr) {
+  constexpr int NS = 3 * kGroups;
   unsigned long long* counts;
-  CBH_TRY(S.get(&counts, 2 * kNB + 6));
+  CBH_TRY(S.get(&counts, 2 * kNB + NS));
   unsigned long long* sums = ctx->timing ? counts + 2 * kNB : nullptr;
-  CBH_HIP(ctx, hipMemsetAsync(counts, 0, sizeof(unsigned long long) * (2 * kNB + 6), ctx->stream));
+  CBH_HIP(ctx, hipMemsetAsync(counts, 0, sizeof(unsigned long long) * (2 * kNB + NS), ctx->stream));
   const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(bin_count_kernel, dim3(std::max(grid, 1)), dim3(256), 0, ctx->stream, work, n, kSmallCap, counts,
+  hipLaunchKernelGGL(bin_count_kernel, dim3(std::max(grid, 1)), dim3(256), 0, ctx->stream, work, n, caps, counts,
                      Bcp, flop, nnz, sums);
   CBH_HIP(ctx, hipGetLastError());
-  unsigned long long h[kNB + 2 * kNB + 6];
-  CBH_HIP(ctx, hipMemcpyAsync(h, counts, sizeof(unsigned long long) * (2 * kNB + 6), hipMemcpyDeviceToHost, ctx->stream));
+  unsigned long long h[2 * kNB + NS];
+  CBH_HIP(ctx, hipMemcpyAsync(h, counts, sizeof(unsigned long long) * (2 * kNB + NS), hipMemcpyDeviceToHost, ctx->stream));
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   unsigned long long off[kNB];
   unsigned long long run = 0;
@@ -452,16 +466,50 @@ static int make_bins(cbh_ctx* ctx, Scratch& S, const int64_t* work, int64_t n, i
   unsigned long long* cursor = counts + kNB;
   CBH_HIP(ctx, hipMemcpyAsync(cursor, off, sizeof(off), hipMemcpyHostToDevice, ctx->stream));
   hipLaunchKernelGGL(bin_scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, work, n, col0,
-                     kSmallCap, cursor, cols);
+                     caps, cursor, cols);
   CBH_HIP(ctx, hipGetLastError());
   // the host copy of `off` must outlive the async H2D copy
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (sums)
-    for (int i = 0; i < 6; ++i) out->units[i] = (double)h[2 * kNB + i];
+    for (int i = 0; i < NS; ++i) out->units[i] = (double)h[2 * kNB + i];
   out->small_first = 0;
   out->small_count = (int64_t)h[1];
-  out->large_first = (int64_t)h[1];
-  out->large_count = (int64_t)(run - h[1]);
+  out->mid_first = (int64_t)h[1];
+  out->mid_count = (int64_t)h[2];
+  out->large_first = (int64_t)(h[1] + h[2]);
+  out->large_count = (int64_t)(run - h[1] - h[2]);
+  for (int lg = 0; lg < kSub; ++lg) out->sub_count[lg] = (int64_t)h[3 + (kSub - 1 - lg)];
+  return CBH_OK;
+}
+
+// CBH_DIAG=1: launch every large sub-bin separately and print its time (profiling aid only).
+static bool diag_enabled() {
+  static int v = [] {
+    const char* e = std::getenv("CBH_DIAG");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v != 0;
+}
+template <class SR, class CFG, int MODE>
+static int launch_large_diag(cbh_ctx* ctx, const TileArgs& a, const BinLists& bl, const char* what) {
+  int64_t first = bl.large_first;
+  for (int lg = kSub - 1; lg >= 0; --lg) {
+    const int64_t n = bl.sub_count[lg];
+    if (!n) continue;
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, ctx->stream);
+    CBH_TRY((launch_tile<SR, CFG, MODE>(ctx, a, first, n)));
+    (void)hipEventRecord(e1, ctx->stream);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    std::fprintf(stderr, "[cbh diag] %s work 2^%d: %lld cols, %.3f ms\n", what, lg, (long long)n, ms);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    first += n;
+  }
   return CBH_OK;
 }
 
@@ -486,15 +534,19 @@ static int sum_i64(cbh_ctx* ctx, Scratch& S, const int64_t* in, int64_t n, int64
 static inline unsigned blocks_for(int64_t n, int bs) { return (unsigned)std::max<int64_t>(1, (n + bs - 1) / bs); }
 
 static int check_err(cbh_ctx* ctx) {
-  int h[4];
+  int h[16];
   CBH_HIP(ctx, hipMemcpyAsync(h, ctx->d_err, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (ctx->timing) flush_records(ctx);
-  if (h[0] || h[1]) {
+  if (h[0] || h[1] || h[2]) {
     CBH_HIP(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(h), ctx->stream));
     return fail(ctx, CBH_E_INTERNAL,
                 "device consistency check failed (count mismatch " + std::to_string(h[0]) + ", split failure " +
-                    std::to_string(h[1]) + ")");
+                    std::to_string(h[1]) + ", bounds guards " + std::to_string(h[2]) + " sites mask " +
+                    std::to_string(h[3]) + "; first: site " + std::to_string(h[4]) + " ctx " + std::to_string(h[5]) +
+                    " " + std::to_string(h[6]) + " " + std::to_string(h[7]) + " " + std::to_string(h[8]) + " " +
+                    std::to_string(h[9]) + " " + std::to_string(h[10]) + " block " + std::to_string(h[11]) +
+                    " thread " + std::to_string(h[12]) + ")");
   }
   return CBH_OK;
 }
@@ -509,6 +561,7 @@ struct Plan {  // device arrays describing C = A*B column by column (B's nonzero
   int64_t* nnz = nullptr;  // nzcB + 1
   int64_t* Ccp = nullptr;  // nzcB + 1
   int32_t* cols = nullptr; // nzcB
+  int32_t* gcur[2] = {nullptr, nullptr};  // per B entry cursors for columns with > EMAX entries
   int64_t total_flops = 0, total_nnz = 0;
 };
 
@@ -522,9 +575,16 @@ static TileArgs spgemm_args(const cbh_mat* A, const cbh_mat* B, const Plan& P, c
   a.Bir = B->ir;
   a.Bnum = B->num;
   a.cols = P.cols;
+  a.gcur[0] = P.gcur[0];
+  a.gcur[1] = P.gcur[1];
   a.rmin = P.rmin;
   a.rmax = P.rmax;
   a.err = ctx->d_err;
+  a.nnzA = A->nnz;
+  a.ncolA = A->n;
+  a.nnzB = B->nnz;
+  a.ccap = INT64_MAX;
+  a.nslots = P.nzcB;
   return a;
 }
 
@@ -537,6 +597,8 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   CBH_TRY(S.get(&P.nnz, P.nzcB + 1));
   CBH_TRY(S.get(&P.Ccp, P.nzcB + 1));
   CBH_TRY(S.get(&P.cols, P.nzcB));
+  CBH_TRY(S.get(&P.gcur[0], B->nnz));
+  CBH_TRY(S.get(&P.gcur[1], B->nnz));
   int64_t* d_tot;
   CBH_TRY(S.get(&d_tot, 2));
   hipLaunchKernelGGL(densify_cp_kernel, dim3(blocks_for(A->n + 1, 256)), dim3(256), 0, ctx->stream, A->jc, A->cp,
@@ -547,15 +609,18 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   CBH_TRY(sum_i64(ctx, S, P.flop, P.nzcB, d_tot));
   CBH_HIP(ctx, hipMemsetAsync(P.nnz, 0, sizeof(int64_t) * (P.nzcB + 1), ctx->stream));
   BinLists bl;
-  CBH_TRY(make_bins(ctx, S, P.flop, P.nzcB, 0, P.cols, &bl, B->cp, P.flop, nullptr));
+  CBH_TRY(make_bins(ctx, S, P.flop, P.nzcB, 0, P.cols, &bl, BinCaps{kSmallCap, kSymMidCap}, B->cp, P.flop, nullptr));
   TileArgs a = spgemm_args(A, B, P, ctx);
   a.work = P.flop;
   a.nnz_out = P.nnz;
   using Dummy = PlusTimesD<int64_t>;
   // algorithmic bytes of the symbolic pass: row ids of B and of every gathered A entry + pointers
-  const double sb_l = 4.0 * (bl.units[3] + bl.units[4]) + 16.0 * bl.large_count;
-  const double sb_s = 4.0 * (bl.units[0] + bl.units[1]) + 16.0 * bl.small_count;
-  CBH_TRY((launch_tile<Dummy, SymLarge, MODE_SYM>(ctx, a, bl.large_first, bl.large_count, CBH_K_SYM_LARGE, sb_l)));
+  const double sb_l = 4.0 * (bl.units[6] + bl.units[7]) + 16.0 * bl.large_count;
+  const double sb_s = 4.0 * (bl.units[0] + bl.units[1] + bl.units[3] + bl.units[4]) +
+                      16.0 * (bl.small_count + bl.mid_count);
+  if (diag_enabled()) CBH_TRY((launch_large_diag<Dummy, SymBmp, MODE_SYM_BMP>(ctx, a, bl, "symbolic-bitmap")));
+  else CBH_TRY((launch_tile<Dummy, SymBmp, MODE_SYM_BMP>(ctx, a, bl.large_first, bl.large_count, CBH_K_SYM_LARGE, sb_l)));
+  CBH_TRY((launch_tile<Dummy, SymMid, MODE_SYM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_SYM_SMALL, 0.0)));
   CBH_TRY((launch_tile<Dummy, SymSmall, MODE_SYM>(ctx, a, bl.small_first, bl.small_count, CBH_K_SYM_SMALL, sb_s)));
   CBH_TRY(exclusive_scan_i64(ctx, S, P.nnz, P.Ccp, P.nzcB + 1));
   CBH_HIP(ctx, hipMemcpyAsync(d_tot + 1, P.Ccp + P.nzcB, sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
@@ -570,20 +635,23 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
 // numeric over column slots [c0, c1) writing C entries at Ccp[c]-cbase
 template <class SR>
 static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat* B, Plan& P, int64_t c0, int64_t c1,
-                       int64_t cbase, int32_t* Cir, void* Cnum, int64_t* launches) {
+                       int64_t cbase, int32_t* Cir, void* Cnum, int64_t* launches, int64_t ccap) {
   BinLists bl;
-  CBH_TRY(make_bins(ctx, S, P.nnz + c0, c1 - c0, c0, P.cols, &bl, B->cp + c0, P.flop + c0, P.nnz + c0));
+  CBH_TRY(make_bins(ctx, S, P.nnz + c0, c1 - c0, c0, P.cols, &bl, BinCaps{kSmallCap, kSmallCap}, B->cp + c0,
+                    P.flop + c0, P.nnz + c0));
   TileArgs a = spgemm_args(A, B, P, ctx);
   a.work = P.nnz;
   a.Ccp = P.Ccp;
   a.cbase = cbase;
   a.Cir = Cir;
   a.Cnum = Cnum;
+  a.ccap = ccap;
   // algorithmic bytes: (s_i+s_v) * (nnz(B) + flops + nnz(C)) + pointers
   constexpr double eb = 4.0 + sizeof(typename SR::val_t);
-  const double nb_l = eb * (bl.units[3] + bl.units[4] + bl.units[5]) + 16.0 * bl.large_count;
+  const double nb_l = eb * (bl.units[6] + bl.units[7] + bl.units[8]) + 16.0 * bl.large_count;
   const double nb_s = eb * (bl.units[0] + bl.units[1] + bl.units[2]) + 16.0 * bl.small_count;
-  CBH_TRY((launch_tile<SR, NumLarge, MODE_NUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
+  if (diag_enabled()) CBH_TRY((launch_large_diag<SR, NumLarge, MODE_NUM>(ctx, a, bl, "numeric")));
+  else CBH_TRY((launch_tile<SR, NumLarge, MODE_NUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
   CBH_TRY((launch_tile<SR, NumSmall, MODE_NUM>(ctx, a, bl.small_first, bl.small_count, CBH_K_NUM_SMALL, nb_s)));
   if (launches) *launches += (bl.large_count > 0) + (bl.small_count > 0);
   return CBH_OK;
@@ -683,7 +751,15 @@ int cbh_ctx_create(int device, cbh_ctx** out) {
       delete c;
       return CBH_E_HIP;
     }
-  if (hipMalloc(&c->d_err, 4 * sizeof(int)) != hipSuccess || hipMemset(c->d_err, 0, 4 * sizeof(int)) != hipSuccess) {
+  {  // keep memory freed by hipFreeAsync mapped in the device pool: phase buffers of ~100 GB
+     // are re-requested every product and re-mapping them costs seconds.
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+      uint64_t thr = UINT64_MAX;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    }
+  }
+  if (hipMalloc(&c->d_err, 16 * sizeof(int)) != hipSuccess || hipMemset(c->d_err, 0, 16 * sizeof(int)) != hipSuccess) {
     delete c;
     return CBH_E_HIP;
   }
@@ -907,7 +983,7 @@ int cbh_spgemm(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh_mat* B
     }
     CBH_TRY(new_mat(ctx, A->m, B->n, P.total_nnz, nzcC, A->dtype, &out));
     int64_t launches = 0;
-    int rc = run_numeric<SR>(ctx, S, A, B, P, 0, P.nzcB, 0, out->ir, out->num, &launches);
+    int rc = run_numeric<SR>(ctx, S, A, B, P, 0, P.nzcB, 0, out->ir, out->num, &launches, P.total_nnz);
     if (rc == CBH_OK) {
       if (keep) {
         (void)hipMemcpyAsync(out->jc, B->jc, sizeof(int64_t) * P.nzcB, hipMemcpyDeviceToDevice, ctx->stream);
@@ -979,8 +1055,15 @@ int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh
     }();
     int32_t* ir;
     VT* num;
+    auto hnow = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double ta = hnow();
     CBH_TRY(S.get(&ir, maxphase));
     CBH_TRY(S.get(&num, maxphase));
+    if (diag_enabled()) {
+      CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      std::fprintf(stderr, "[cbh diag] phased: %zu phases, budget %lld entries, alloc %.1f ms\n", cuts.size() - 1,
+                   (long long)budget, hnow() - ta);
+    }
     double* d_sum;
     unsigned long long* d_dig;
     CBH_TRY(S.get(&d_sum, 1));
@@ -990,7 +1073,13 @@ int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh
     int64_t launches = 0;
     for (size_t i = 1; i < cuts.size(); ++i) {
       const int64_t c0 = cuts[i - 1], c1 = cuts[i];
-      CBH_TRY(run_numeric<SR>(ctx, S, A, B, P, c0, c1, hcp[c0], ir, num, &launches));
+      const double tp = hnow();
+      CBH_TRY(run_numeric<SR>(ctx, S, A, B, P, c0, c1, hcp[c0], ir, num, &launches, maxphase));
+      if (diag_enabled()) {
+        CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        std::fprintf(stderr, "[cbh diag] phase %zu: cols [%lld,%lld) %.1f ms host wall\n", i, (long long)c0,
+                     (long long)c1, hnow() - tp);
+      }
       if (flags & CBH_PHASE_CHECKSUM) {
         hipLaunchKernelGGL(checksum_kernel<VT>, dim3(blocks_for(c1 - c0, 4)), dim3(256), 0, ctx->stream, B->jc + c0,
                            P.Ccp + c0, hcp[c0], c1 - c0, ir, num, hcp[c0], d_sum, d_dig);
@@ -1099,6 +1188,11 @@ int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* p
     a.seg_start = seg_start;
     a.seg_len = seg_len;
     a.nlists = nlists;
+    a.nnzA = INT64_MAX;
+    a.ncolA = INT64_MAX;
+    a.nnzB = INT64_MAX;
+    a.ccap = INT64_MAX;
+    a.nslots = ncols;
     a.cols = cols;
     a.rmin = rmin;
     a.rmax = rmax;
@@ -1106,10 +1200,11 @@ int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* p
     // symbolic
     CBH_HIP(ctx, hipMemsetAsync(nnz, 0, sizeof(int64_t) * (ncols + 1), ctx->stream));
     BinLists bl;
-    CBH_TRY(make_bins(ctx, S, work, ncols, 0, cols, &bl));
+    CBH_TRY(make_bins(ctx, S, work, ncols, 0, cols, &bl, BinCaps{kSmallCap, kSymMidCap}));
     a.work = work;
     a.nnz_out = nnz;
-    CBH_TRY((launch_tile<SR, SymLarge, MODE_SYM_MRG>(ctx, a, bl.large_first, bl.large_count, CBH_K_MERGE_SYM)));
+    CBH_TRY((launch_tile<SR, SymBmp, MODE_SYM_BMP_MRG>(ctx, a, bl.large_first, bl.large_count, CBH_K_MERGE_SYM)));
+    CBH_TRY((launch_tile<SR, SymMid, MODE_SYM_MRG>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_MERGE_SYM)));
     CBH_TRY((launch_tile<SR, SymSmall, MODE_SYM_MRG>(ctx, a, bl.small_first, bl.small_count, CBH_K_MERGE_SYM)));
     CBH_TRY(exclusive_scan_i64(ctx, S, nnz, Ccp, ncols + 1));
     int64_t total = 0;
@@ -1118,7 +1213,7 @@ int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* p
     CBH_TRY(check_err(ctx));
     cbh_mat* out;
     CBH_TRY(new_mat(ctx, P0->m, n, total, ncols, dtype, &out));
-    int rc = make_bins(ctx, S, nnz, ncols, 0, cols, &bl);
+    int rc = make_bins(ctx, S, nnz, ncols, 0, cols, &bl, BinCaps{kSmallCap, kSmallCap});
     if (rc == CBH_OK) {
       a.work = nnz;
       a.Ccp = Ccp;

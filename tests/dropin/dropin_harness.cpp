@@ -79,14 +79,16 @@ static int run_case(const char* name, SpParMat<int64_t, int64_t, SpDCCols<int64_
 int main(int argc, char** argv) {
   MPI_Init(&argc, &argv);
   int scale = argc > 1 ? std::atoi(argv[1]) : 12;
-  double init[4] = {.57, .19, .19, .05};
-  DistEdgeList<int64_t>* DEL = new DistEdgeList<int64_t>();
-  DEL->GenGraph500Data(init, scale, 16, true, true);
-  SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>> G(*DEL, false);
-  delete DEL;
   int bad = 0;
-  bad += run_case<double, PlusTimesSRing<double, double>, CpuPlusTimes<double>>("PSpGEMM<PlusTimes<double>>", G);
-  bad += run_case<int64_t, SelectMaxSRing<int64_t, int64_t>, CpuSelectMax<int64_t>>("PSpGEMM<SelectMax<int64>>", G);
+  {  // every CombBLAS object must be destroyed before MPI_Finalize
+    double init[4] = {.57, .19, .19, .05};
+    DistEdgeList<int64_t>* DEL = new DistEdgeList<int64_t>();
+    DEL->GenGraph500Data(init, scale, 16, true, true);
+    SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>> G(*DEL, false);
+    delete DEL;
+    bad += run_case<double, PlusTimesSRing<double, double>, CpuPlusTimes<double>>("PSpGEMM<PlusTimes<double>>", G);
+    bad += run_case<int64_t, SelectMaxSRing<int64_t, int64_t>, CpuSelectMax<int64_t>>("PSpGEMM<SelectMax<int64>>", G);
+  }
   MPI_Finalize();
   return bad ? 1 : 0;
 }
