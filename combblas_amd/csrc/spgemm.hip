@@ -36,6 +36,8 @@ struct cbh_ctx {
   cbh_kernel_times times{-1, -1, -1, 0};
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   int* d_err = nullptr;  // 4 ints of device-side error flags
+  void* ws = nullptr;  // persistent phase workspace (hipMalloc'd once, grow-only): a ~150 GB
+  int64_t ws_bytes = 0;  // buffer must not be re-mapped on every product
   cbh_alloc_fn alloc = nullptr;
   cbh_free_fn release = nullptr;
   void* alloc_user = nullptr;
@@ -774,6 +776,7 @@ int cbh_ctx_destroy(cbh_ctx* ctx) {
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->evpool) (void)hipEventDestroy(e);
+  if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return CBH_OK;
@@ -1028,11 +1031,15 @@ int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh
     const size_t esz = sizeof(int32_t) + sizeof(VT);
     int64_t budget_bytes = ctx->phase_budget;
     if (budget_bytes <= 0) {
-      size_t freeb = 0, totb = 0;
-      CBH_HIP(ctx, hipMemGetInfo(&freeb, &totb));
-      budget_bytes = (int64_t)(freeb / 2);
+      if (ctx->ws_bytes > 0) {
+        budget_bytes = ctx->ws_bytes - 512;
+      } else {
+        size_t freeb = 0, totb = 0;
+        CBH_HIP(ctx, hipMemGetInfo(&freeb, &totb));
+        budget_bytes = (int64_t)(freeb / 2);
+      }
     }
-    int64_t budget = std::max<int64_t>(1, budget_bytes / (int64_t)esz);
+    int64_t budget = std::max<int64_t>(1, std::min<int64_t>(budget_bytes / (int64_t)esz, P.total_nnz));
     // phase boundaries over B's column slots from the exact column offsets
     std::vector<int64_t> hcp(P.nzcB + 1);
     CBH_HIP(ctx, hipMemcpyAsync(hcp.data(), P.Ccp, sizeof(int64_t) * (P.nzcB + 1), hipMemcpyDeviceToHost, ctx->stream));
@@ -1057,8 +1064,18 @@ int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh
     VT* num;
     auto hnow = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double ta = hnow();
-    CBH_TRY(S.get(&ir, maxphase));
-    CBH_TRY(S.get(&num, maxphase));
+    const int64_t ir_bytes = ((maxphase * (int64_t)sizeof(int32_t)) + 255) & ~int64_t(255);
+    const int64_t need = ir_bytes + maxphase * (int64_t)sizeof(VT) + 256;
+    if (ctx->ws_bytes < need) {
+      CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      if (ctx->ws) (void)hipFree(ctx->ws);
+      ctx->ws = nullptr;
+      ctx->ws_bytes = 0;
+      CBH_HIP(ctx, hipMalloc(&ctx->ws, (size_t)need));
+      ctx->ws_bytes = need;
+    }
+    ir = reinterpret_cast<int32_t*>(ctx->ws);
+    num = reinterpret_cast<VT*>(reinterpret_cast<char*>(ctx->ws) + ir_bytes);
     if (diag_enabled()) {
       CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
       std::fprintf(stderr, "[cbh diag] phased: %zu phases, budget %lld entries, alloc %.1f ms\n", cuts.size() - 1,
