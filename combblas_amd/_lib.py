@@ -9,7 +9,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcombblas_hip.so")
+# CBH_LIB=stamps selects the diagnostic build (combblas_amd/build.py --stamps); default is the product
+LIB_PATH = os.path.join(_HERE, "libcombblas_hip_stamps.so" if os.environ.get("CBH_LIB") == "stamps"
+                        else "libcombblas_hip.so")
 
 c_int64_p = ctypes.POINTER(ctypes.c_int64)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)

@@ -12,30 +12,36 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcombblas_hip.so")
 SOURCES = ["spgemm.hip", "rmat.cpp"]
-HEADERS = ["semiring.h", "tile_kernel.h", "host_util.h", os.path.join("..", "..", "include", "combblas_hip.h")]
+HEADERS = ["semiring.h", "tile_kernel.h", "task_kernel.h", "host_util.h", os.path.join("..", "..", "include", "combblas_hip.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("CBH_OFFLOAD_ARCH", "gfx950")
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
+def _stale(lib: str = LIB) -> bool:
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
-        return LIB
+def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
+    """stamps=True builds the diagnostic variant libcombblas_hip_stamps.so (-DCBH_STAMPS: per-phase
+    s_memtime cycle counts, printed with CBH_DIAG=1; load it with CBH_LIB=stamps). Never the product."""
+    lib = LIB.replace(".so", "_stamps.so") if stamps else LIB
+    if not force and not _stale(lib):
+        return lib
     cmd = [HIPCC, "-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17", "-Wall",
-           "-Wno-unused-function", "-Wl,-soname,libcombblas_hip.so", "-o", LIB + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES] + ["-lpthread"]
+           "-Wno-unused-function", "-Wl,-soname," + os.path.basename(lib), "-o", lib + ".tmp"] + \
+        (["-DCBH_STAMPS"] if stamps else []) + [os.path.join(CSRC, s) for s in SOURCES] + ["-lpthread"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd, cwd=CSRC)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force=True, verbose=True))
+    import sys
+
+    print(build(force=True, verbose=True, stamps="--stamps" in sys.argv))

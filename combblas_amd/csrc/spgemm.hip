@@ -21,7 +21,7 @@
 
 #include "../../include/combblas_hip.h"
 #include "semiring.h"
-#include "tile_kernel.h"
+#include "task_kernel.h"
 
 using namespace cbh;
 
@@ -200,36 +200,30 @@ __device__ __forceinline__ int bin_of(int64_t w, BinCaps k) {
 }
 __device__ __forceinline__ int group_of(int b) { return b <= 1 ? 0 : (b == 2 ? 1 : 2); }
 
-// Optional per-group unit sums for the roofline (groups small/mid/large):
-// sums[g*3 + 0] = sum of B column lengths, [1] = flops, [2] = nnz(C).
+// Optional per-group unit sums for the roofline (groups small/mid/large): sums[g] = sum of
+// units[item] (algorithmic entries an item moves).
 __global__ __launch_bounds__(256) void bin_count_kernel(const int64_t* __restrict__ work, int64_t n, BinCaps caps,
                                                         unsigned long long* __restrict__ counts,
-                                                        const int64_t* __restrict__ Bcp, const int64_t* __restrict__ flop,
-                                                        const int64_t* __restrict__ nnz,
+                                                        const int64_t* __restrict__ units,
                                                         unsigned long long* __restrict__ sums) {
   __shared__ unsigned int h[kNB];
-  __shared__ unsigned long long ssum[3 * kGroups];
+  __shared__ unsigned long long ssum[kGroups];
   for (int i = threadIdx.x; i < kNB; i += blockDim.x) h[i] = 0;
-  if (threadIdx.x < 3 * kGroups) ssum[threadIdx.x] = 0;
+  if (threadIdx.x < kGroups) ssum[threadIdx.x] = 0;
   __syncthreads();
-  unsigned long long loc[3 * kGroups] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long loc[kGroups] = {0, 0, 0};
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x) {
     const int b = bin_of(work[c], caps);
     atomicAdd(&h[b], 1u);
-    if (sums && b > 0) {
-      const int g = group_of(b);
-      loc[g * 3 + 0] += (unsigned long long)(Bcp ? Bcp[c + 1] - Bcp[c] : 0);
-      loc[g * 3 + 1] += (unsigned long long)(flop ? flop[c] : 0);
-      loc[g * 3 + 2] += (unsigned long long)(nnz ? nnz[c] : 0);
-    }
+    if (sums && units && b > 0) loc[group_of(b)] += (unsigned long long)units[c];
   }
   if (sums)
-    for (int i = 0; i < 3 * kGroups; ++i)
+    for (int i = 0; i < kGroups; ++i)
       if (loc[i]) atomicAdd(&ssum[i], loc[i]);
   __syncthreads();
   for (int i = threadIdx.x; i < kNB; i += blockDim.x)
     if (h[i]) atomicAdd(&counts[i], (unsigned long long)h[i]);
-  if (sums && threadIdx.x < 3 * kGroups && ssum[threadIdx.x]) atomicAdd(&sums[threadIdx.x], ssum[threadIdx.x]);
+  if (sums && threadIdx.x < kGroups && ssum[threadIdx.x]) atomicAdd(&sums[threadIdx.x], ssum[threadIdx.x]);
 }
 
 __global__ __launch_bounds__(256) void bin_scatter_kernel(const int64_t* __restrict__ work, int64_t n, int64_t col0,
@@ -435,25 +429,24 @@ static int launch_tile(cbh_ctx* ctx, const TileArgs& args, int64_t first, int64_
   return CBH_OK;
 }
 
-// Bins the column slots [0, n) by work. Returns list offsets of the small and large groups.
+// Bins the items [0, n) (column slots or tasks) by work; writes item ids + col0 into `ids`.
 struct BinLists {
   int64_t small_first = 0, small_count = 0, mid_first = 0, mid_count = 0, large_first = 0, large_count = 0;
   int64_t sub_count[kSub] = {0};  // large sub-bins, index = floor(log2 work)
-  double units[3 * kGroups] = {0};  // [small|mid|large] x [sum b_j, sum flop_j, sum nnz_j] (timing only)
+  double units[kGroups] = {0};    // [small|mid|large] sum of units (timing only)
 };
-// Unit sums are gathered only when the context records timings (bench/roofline); Bcp/flop/nnz
-// are indexed like `work` (already offset by col0 by the caller).
-static int make_bins(cbh_ctx* ctx, Scratch& S, const int64_t* work, int64_t n, int64_t col0, int32_t* cols,
-                     BinLists* out, BinCaps caps, const int64_t* Bcp = nullptr, const int64_t* flop = nullptr,
-                     const int64_t* nnz = nullptr) {
-  constexpr int NS = 3 * kGroups;
+// Unit sums are gathered only when the context records timings (bench/roofline); `units` is
+// indexed like `work`.
+static int make_bins(cbh_ctx* ctx, Scratch& S, const int64_t* work, int64_t n, int64_t col0, int32_t* ids,
+                     BinLists* out, BinCaps caps, const int64_t* units = nullptr) {
+  constexpr int NS = kGroups;
   unsigned long long* counts;
   CBH_TRY(S.get(&counts, 2 * kNB + NS));
   unsigned long long* sums = ctx->timing ? counts + 2 * kNB : nullptr;
   CBH_HIP(ctx, hipMemsetAsync(counts, 0, sizeof(unsigned long long) * (2 * kNB + NS), ctx->stream));
   const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(bin_count_kernel, dim3(std::max(grid, 1)), dim3(256), 0, ctx->stream, work, n, caps, counts,
-                     Bcp, flop, nnz, sums);
+                     units, sums);
   CBH_HIP(ctx, hipGetLastError());
   unsigned long long h[2 * kNB + NS];
   CBH_HIP(ctx, hipMemcpyAsync(h, counts, sizeof(unsigned long long) * (2 * kNB + NS), hipMemcpyDeviceToHost, ctx->stream));
@@ -468,7 +461,7 @@ static int make_bins(cbh_ctx* ctx, Scratch& S, const int64_t* work, int64_t n, i
   unsigned long long* cursor = counts + kNB;
   CBH_HIP(ctx, hipMemcpyAsync(cursor, off, sizeof(off), hipMemcpyHostToDevice, ctx->stream));
   hipLaunchKernelGGL(bin_scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, work, n, col0,
-                     caps, cursor, cols);
+                     caps, cursor, ids);
   CBH_HIP(ctx, hipGetLastError());
   // the host copy of `off` must outlive the async H2D copy
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -553,22 +546,179 @@ static int check_err(cbh_ctx* ctx) {
   return CBH_OK;
 }
 
-// ============================================================================ symbolic (shared by spgemm)
-struct Plan {  // device arrays describing C = A*B column by column (B's nonzero columns)
-  int64_t nzcB = 0;
+// ============================================================================ task plan (spgemm)
+// Every nonzero column j of B becomes S_j tasks: equal-width row ranges of [rmin_j, rmax_j]
+// with about kTaskFlops products each (S_j = 1 for light columns). Tasks of a column are
+// consecutive and in row order, so the exclusive scan of the per-task counts gives every task
+// its output offset and C's column pointers are the offsets of each column's first task.
+constexpr int64_t kTaskFlopsDefault = 65536;
+static int64_t task_flops() {
+  static int64_t v = [] {
+    const char* e = std::getenv("CBH_TASK_FLOPS");
+    const long long x = e ? std::atoll(e) : 0;
+    return x > 0 ? (int64_t)x : kTaskFlopsDefault;
+  }();
+  return v;
+}
+
+__global__ void task_count_kernel(const int64_t* __restrict__ flop, const int32_t* __restrict__ rmin,
+                                  const int32_t* __restrict__ rmax, int64_t n, int64_t ft, int64_t* __restrict__ S) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t f = flop[i];
+  int64_t s = 0;
+  if (f > 0) {
+    const int64_t span = (int64_t)rmax[i] - rmin[i] + 1;
+    s = (f + ft - 1) / ft;
+    if (s > span) s = span;
+    if (s < 1) s = 1;
+  }
+  S[i] = s;
+}
+
+// one wave per column: balanced split lo_s = rmin + span*s/S; per-task work and roofline units
+// split so that they sum exactly to the column's totals
+__global__ __launch_bounds__(256) void task_fill_kernel(const int64_t* __restrict__ tstart, const int64_t* __restrict__ flop,
+                                                        const int32_t* __restrict__ rmin, const int32_t* __restrict__ rmax,
+                                                        const int64_t* __restrict__ Bcp, int64_t n,
+                                                        int32_t* __restrict__ tcol, int32_t* __restrict__ tlo,
+                                                        int32_t* __restrict__ thi, uint8_t* __restrict__ tfull,
+                                                        int64_t* __restrict__ twork, int64_t* __restrict__ tunits) {
+  const int lane = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= n) return;
+  const int64_t t0 = tstart[c], S = tstart[c + 1] - t0;
+  if (S <= 0) return;
+  const int64_t span = (int64_t)rmax[c] - rmin[c] + 1, f = flop[c], b = Bcp[c + 1] - Bcp[c];
+  for (int64_t s = lane; s < S; s += 64) {
+    const int64_t t = t0 + s;
+    tcol[t] = (int32_t)c;
+    tlo[t] = (int32_t)(rmin[c] + span * s / S);
+    thi[t] = (int32_t)(rmin[c] + span * (s + 1) / S);
+    tfull[t] = (uint8_t)((s == 0 ? 1 : 0) | (s == S - 1 ? 2 : 0));
+    twork[t] = f * (s + 1) / S - f * s / S;
+    tunits[t] = (b + f) * (s + 1) / S - (b + f) * s / S;
+  }
+}
+
+__global__ void gather_i64_kernel(const int64_t* __restrict__ src, const int64_t* __restrict__ idx, int64_t n,
+                                  int64_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[idx[i]];
+}
+__global__ void diff_i64_kernel(const int64_t* __restrict__ x, int64_t n, int64_t* __restrict__ d) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) d[i] = x[i + 1] - x[i];
+}
+__global__ void add_i64_kernel(const int64_t* __restrict__ x, const int64_t* __restrict__ y, int64_t n,
+                               int64_t* __restrict__ o) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) o[i] = x[i] + y[i];
+}
+
+// task-kernel configurations: T slots, BS threads, EMAX entries per chunk, U products per thread
+struct TSymSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
+struct TSymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512, U = 4; };
+struct TNumSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
+struct TNumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512, U = 4; };
+
+template <class SR, class CFG, int MODE>
+static int launch_task(cbh_ctx* ctx, const TaskArgs& args, int64_t first, int64_t count, int kind = -1,
+                       double bytes = 0) {
+  if (count <= 0) return CBH_OK;
+  size_t e0 = (size_t)-1;
+  if (ctx->timing && kind >= 0) {
+    e0 = next_event(ctx);
+    if (e0 != (size_t)-1) (void)hipEventRecord(ctx->evpool[e0], ctx->stream);
+  }
+  using C = TaskCfg<SR, CFG::T, CFG::BS, CFG::EMAX, CFG::U, MODE>;
+  auto kern = task_kernel<SR, CFG::T, CFG::BS, CFG::EMAX, CFG::U, MODE>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    CBH_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)C::bytes));
+    attr_set = true;
+  }
+  const int64_t kMaxGrid = 1ll << 30;
+  for (int64_t off = 0; off < count; off += kMaxGrid) {
+    const int64_t n = std::min(kMaxGrid, count - off);
+    TaskArgs b = args;
+    b.order = args.order + first + off;
+    b.norder = n;
+    hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(CFG::BS), C::bytes, ctx->stream, b);
+    CBH_HIP(ctx, hipGetLastError());
+  }
+  if (e0 != (size_t)-1) {
+    const size_t e1 = next_event(ctx);
+    if (e1 != (size_t)-1) {
+      (void)hipEventRecord(ctx->evpool[e1], ctx->stream);
+      ctx->recs.push_back({kind, e0, e1, bytes});
+    }
+  }
+  return CBH_OK;
+}
+
+// CBH_DIAG=1: every large sub-bin launched separately with its time printed (profiling aid only)
+template <class SR, class CFG, int MODE>
+static int launch_task_diag(cbh_ctx* ctx, const TaskArgs& a, const BinLists& bl, const char* what) {
+  int64_t first = bl.large_first;
+  for (int lg = kSub - 1; lg >= 0; --lg) {
+    const int64_t n = bl.sub_count[lg];
+    if (!n) continue;
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, ctx->stream);
+    CBH_TRY((launch_task<SR, CFG, MODE>(ctx, a, first, n)));
+    (void)hipEventRecord(e1, ctx->stream);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    std::fprintf(stderr, "[cbh diag] %s work 2^%d: %lld tasks, %.3f ms\n", what, lg, (long long)n, ms);
+#ifdef CBH_STAMPS
+    {
+      unsigned long long hs[16];
+      (void)hipMemcpyFromSymbol(hs, HIP_SYMBOL(g_stamps), sizeof(hs));
+      const unsigned long long z[16] = {0};
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
+      double tot = 0;
+      for (int k = 0; k < 12; ++k) tot += (double)hs[k];
+      std::fprintf(stderr, "[cbh stamps]   wg=%llu cyc/wg=%.0f  setup %.1f%% clear %.1f%% entries %.1f%% scan %.1f%% own %.1f%% products %.1f%% | ovf-check %.1f%% cursor+count %.1f%% place %.1f%% end-sync %.1f%% | tail %.1f%%\n",
+                   hs[12], tot / std::max(1ull, hs[12]), 100 * hs[0] / tot, 100 * hs[1] / tot, 100 * hs[2] / tot,
+                   100 * hs[3] / tot, 100 * hs[4] / tot, 100 * hs[5] / tot, 100 * hs[8] / tot, 100 * hs[9] / tot,
+                   100 * hs[10] / tot, 100 * hs[6] / tot, 100 * hs[7] / tot);
+    }
+#endif
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    first += n;
+  }
+  return CBH_OK;
+}
+
+struct Plan {  // device arrays describing C = A*B (B's nonzero column slots, tasks)
+  int64_t nzcB = 0, ntasks = 0;
   int64_t* Adense = nullptr;  // A.n + 1
-  int64_t* flop = nullptr;    // nzcB
+  int64_t* flop = nullptr;    // nzcB + 1
   int32_t* rmin = nullptr;
   int32_t* rmax = nullptr;
-  int64_t* nnz = nullptr;  // nzcB + 1
-  int64_t* Ccp = nullptr;  // nzcB + 1
-  int32_t* cols = nullptr; // nzcB
-  int32_t* gcur[2] = {nullptr, nullptr};  // per B entry cursors for columns with > EMAX entries
+  int64_t* tstart = nullptr;  // nzcB + 1: first task of each column
+  int32_t* tcol = nullptr;    // per task
+  int32_t* tlo = nullptr;
+  int32_t* thi = nullptr;
+  uint8_t* tfull = nullptr;
+  int64_t* twork = nullptr;   // flops estimate
+  int64_t* tunits = nullptr;  // roofline units (B entries + products), later + outputs
+  int64_t* tcnt = nullptr;    // ntasks + 1: outputs per task
+  int64_t* toff = nullptr;    // ntasks + 1: output offset per task
+  int32_t* order = nullptr;   // ntasks: launch order
+  int64_t* nnz = nullptr;     // nzcB + 1
+  int64_t* Ccp = nullptr;     // nzcB + 1
   int64_t total_flops = 0, total_nnz = 0;
 };
 
-static TileArgs spgemm_args(const cbh_mat* A, const cbh_mat* B, const Plan& P, cbh_ctx* ctx) {
-  TileArgs a;
+static TaskArgs task_args(const cbh_mat* A, const cbh_mat* B, const Plan& P, cbh_ctx* ctx) {
+  TaskArgs a;
   std::memset(&a, 0, sizeof(a));
   a.Acp = P.Adense;
   a.Air = A->ir;
@@ -576,86 +726,116 @@ static TileArgs spgemm_args(const cbh_mat* A, const cbh_mat* B, const Plan& P, c
   a.Bcp = B->cp;
   a.Bir = B->ir;
   a.Bnum = B->num;
-  a.cols = P.cols;
-  a.gcur[0] = P.gcur[0];
-  a.gcur[1] = P.gcur[1];
-  a.rmin = P.rmin;
-  a.rmax = P.rmax;
+  a.order = P.order;
+  a.tcol = P.tcol;
+  a.tlo = P.tlo;
+  a.thi = P.thi;
+  a.tfull = P.tfull;
   a.err = ctx->d_err;
   a.nnzA = A->nnz;
   a.ncolA = A->n;
-  a.nnzB = B->nnz;
+  a.ntasks = P.ntasks;
   a.ccap = INT64_MAX;
-  a.nslots = P.nzcB;
   return a;
 }
 
 static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat* B, Plan& P) {
   P.nzcB = B->nzc;
+  const int64_t n = P.nzcB;
   CBH_TRY(S.get(&P.Adense, A->n + 1));
-  CBH_TRY(S.get(&P.flop, P.nzcB + 1));
-  CBH_TRY(S.get(&P.rmin, P.nzcB));
-  CBH_TRY(S.get(&P.rmax, P.nzcB));
-  CBH_TRY(S.get(&P.nnz, P.nzcB + 1));
-  CBH_TRY(S.get(&P.Ccp, P.nzcB + 1));
-  CBH_TRY(S.get(&P.cols, P.nzcB));
-  CBH_TRY(S.get(&P.gcur[0], B->nnz));
-  CBH_TRY(S.get(&P.gcur[1], B->nnz));
+  CBH_TRY(S.get(&P.flop, n + 1));
+  CBH_TRY(S.get(&P.rmin, n));
+  CBH_TRY(S.get(&P.rmax, n));
+  CBH_TRY(S.get(&P.tstart, n + 1));
+  CBH_TRY(S.get(&P.nnz, n + 1));
+  CBH_TRY(S.get(&P.Ccp, n + 1));
+  int64_t* scnt;
+  CBH_TRY(S.get(&scnt, n + 1));
   int64_t* d_tot;
-  CBH_TRY(S.get(&d_tot, 2));
+  CBH_TRY(S.get(&d_tot, 3));
   hipLaunchKernelGGL(densify_cp_kernel, dim3(blocks_for(A->n + 1, 256)), dim3(256), 0, ctx->stream, A->jc, A->cp,
                      A->nzc, A->n, A->nnz, P.Adense);
-  hipLaunchKernelGGL(flop_kernel, dim3(blocks_for(P.nzcB, 4)), dim3(256), 0, ctx->stream, P.Adense, A->ir, B->cp, B->ir,
-                     P.nzcB, P.flop, P.rmin, P.rmax);
+  hipLaunchKernelGGL(flop_kernel, dim3(blocks_for(n, 4)), dim3(256), 0, ctx->stream, P.Adense, A->ir, B->cp, B->ir, n,
+                     P.flop, P.rmin, P.rmax);
   CBH_HIP(ctx, hipGetLastError());
-  CBH_TRY(sum_i64(ctx, S, P.flop, P.nzcB, d_tot));
-  CBH_HIP(ctx, hipMemsetAsync(P.nnz, 0, sizeof(int64_t) * (P.nzcB + 1), ctx->stream));
-  BinLists bl;
-  CBH_TRY(make_bins(ctx, S, P.flop, P.nzcB, 0, P.cols, &bl, BinCaps{kSmallCap, kSymMidCap}, B->cp, P.flop, nullptr));
-  TileArgs a = spgemm_args(A, B, P, ctx);
-  a.work = P.flop;
-  a.nnz_out = P.nnz;
-  using Dummy = PlusTimesD<int64_t>;
-  // algorithmic bytes of the symbolic pass: row ids of B and of every gathered A entry + pointers
-  const double sb_l = 4.0 * (bl.units[6] + bl.units[7]) + 16.0 * bl.large_count;
-  const double sb_s = 4.0 * (bl.units[0] + bl.units[1] + bl.units[3] + bl.units[4]) +
-                      16.0 * (bl.small_count + bl.mid_count);
-  if (diag_enabled()) CBH_TRY((launch_large_diag<Dummy, SymBmp, MODE_SYM_BMP>(ctx, a, bl, "symbolic-bitmap")));
-  else CBH_TRY((launch_tile<Dummy, SymBmp, MODE_SYM_BMP>(ctx, a, bl.large_first, bl.large_count, CBH_K_SYM_LARGE, sb_l)));
-  CBH_TRY((launch_tile<Dummy, SymMid, MODE_SYM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_SYM_SMALL, 0.0)));
-  CBH_TRY((launch_tile<Dummy, SymSmall, MODE_SYM>(ctx, a, bl.small_first, bl.small_count, CBH_K_SYM_SMALL, sb_s)));
-  CBH_TRY(exclusive_scan_i64(ctx, S, P.nnz, P.Ccp, P.nzcB + 1));
-  CBH_HIP(ctx, hipMemcpyAsync(d_tot + 1, P.Ccp + P.nzcB, sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
+  CBH_TRY(sum_i64(ctx, S, P.flop, n, d_tot));
+  hipLaunchKernelGGL(task_count_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, P.flop, P.rmin, P.rmax, n,
+                     task_flops(), scnt);
+  CBH_HIP(ctx, hipMemsetAsync(scnt + n, 0, sizeof(int64_t), ctx->stream));
+  CBH_TRY(exclusive_scan_i64(ctx, S, scnt, P.tstart, n + 1));
   int64_t h[2];
-  CBH_HIP(ctx, hipMemcpyAsync(h, d_tot, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipMemcpyAsync(&h[1], P.tstart + n, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipMemcpyAsync(&h[0], d_tot, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   P.total_flops = h[0];
+  P.ntasks = h[1];
+  if (P.ntasks > INT32_MAX) return fail(ctx, CBH_E_INTERNAL, "more than 2^31 tasks");
+  const int64_t nt = std::max<int64_t>(P.ntasks, 1);
+  CBH_TRY(S.get(&P.tcol, nt));
+  CBH_TRY(S.get(&P.tlo, nt));
+  CBH_TRY(S.get(&P.thi, nt));
+  CBH_TRY(S.get(&P.tfull, nt));
+  CBH_TRY(S.get(&P.twork, nt));
+  CBH_TRY(S.get(&P.tunits, nt));
+  CBH_TRY(S.get(&P.tcnt, nt + 1));
+  CBH_TRY(S.get(&P.toff, nt + 1));
+  CBH_TRY(S.get(&P.order, nt));
+  hipLaunchKernelGGL(task_fill_kernel, dim3(blocks_for(n, 4)), dim3(256), 0, ctx->stream, P.tstart, P.flop, P.rmin,
+                     P.rmax, B->cp, n, P.tcol, P.tlo, P.thi, P.tfull, P.twork, P.tunits);
+  CBH_HIP(ctx, hipGetLastError());
+  CBH_HIP(ctx, hipMemsetAsync(P.tcnt, 0, sizeof(int64_t) * (nt + 1), ctx->stream));
+  BinLists bl;
+  CBH_TRY(make_bins(ctx, S, P.twork, P.ntasks, 0, P.order, &bl, BinCaps{kSmallCap, kSmallCap}, P.tunits));
+  TaskArgs a = task_args(A, B, P, ctx);
+  a.twork = P.twork;
+  a.cnt = P.tcnt;
+  using Dummy = PlusTimesD<int64_t>;
+  // algorithmic bytes of the symbolic pass: row ids of B and of every gathered A entry + pointers
+  const double sb_l = 4.0 * bl.units[2] + 16.0 * bl.large_count;
+  const double sb_s = 4.0 * (bl.units[0] + bl.units[1]) + 16.0 * (bl.small_count + bl.mid_count);
+  if (diag_enabled()) CBH_TRY((launch_task_diag<Dummy, TSymLarge, MODE_TSYM>(ctx, a, bl, "symbolic")));
+  else CBH_TRY((launch_task<Dummy, TSymLarge, MODE_TSYM>(ctx, a, bl.large_first, bl.large_count, CBH_K_SYM_LARGE, sb_l)));
+  CBH_TRY((launch_task<Dummy, TSymSmall, MODE_TSYM>(ctx, a, bl.small_first, bl.small_count + bl.mid_count,
+                                                     CBH_K_SYM_SMALL, sb_s)));
+  // task offsets -> column pointers of C
+  CBH_TRY(exclusive_scan_i64(ctx, S, P.tcnt, P.toff, P.ntasks + 1));
+  hipLaunchKernelGGL(gather_i64_kernel, dim3(blocks_for(n + 1, 256)), dim3(256), 0, ctx->stream, P.toff, P.tstart,
+                     n + 1, P.Ccp);
+  hipLaunchKernelGGL(diff_i64_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, P.Ccp, n, P.nnz);
+  CBH_HIP(ctx, hipMemsetAsync(P.nnz + n, 0, sizeof(int64_t), ctx->stream));
+  // roofline units of the numeric pass: + outputs
+  hipLaunchKernelGGL(add_i64_kernel, dim3(blocks_for(P.ntasks, 256)), dim3(256), 0, ctx->stream, P.tunits, P.tcnt,
+                     P.ntasks, P.tunits);
+  CBH_HIP(ctx, hipGetLastError());
+  CBH_HIP(ctx, hipMemcpyAsync(&h[1], P.Ccp + n, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   P.total_nnz = h[1];
   return check_err(ctx);
 }
 
-// numeric over column slots [c0, c1) writing C entries at Ccp[c]-cbase
+// numeric over the tasks of column slots [c0, c1) (task ids [t0, t1)) writing C entries at toff-cbase
 template <class SR>
-static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat* B, Plan& P, int64_t c0, int64_t c1,
+static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat* B, Plan& P, int64_t t0, int64_t t1,
                        int64_t cbase, int32_t* Cir, void* Cnum, int64_t* launches, int64_t ccap) {
+  if (t1 <= t0) return CBH_OK;
   BinLists bl;
-  CBH_TRY(make_bins(ctx, S, P.nnz + c0, c1 - c0, c0, P.cols, &bl, BinCaps{kSmallCap, kSmallCap}, B->cp + c0,
-                    P.flop + c0, P.nnz + c0));
-  TileArgs a = spgemm_args(A, B, P, ctx);
-  a.work = P.nnz;
-  a.Ccp = P.Ccp;
+  CBH_TRY(make_bins(ctx, S, P.tcnt + t0, t1 - t0, t0, P.order, &bl, BinCaps{kSmallCap, kSmallCap}, P.tunits + t0));
+  TaskArgs a = task_args(A, B, P, ctx);
+  a.twork = P.tcnt;
+  a.toff = P.toff;
   a.cbase = cbase;
   a.Cir = Cir;
   a.Cnum = Cnum;
   a.ccap = ccap;
   // algorithmic bytes: (s_i+s_v) * (nnz(B) + flops + nnz(C)) + pointers
   constexpr double eb = 4.0 + sizeof(typename SR::val_t);
-  const double nb_l = eb * (bl.units[6] + bl.units[7] + bl.units[8]) + 16.0 * bl.large_count;
-  const double nb_s = eb * (bl.units[0] + bl.units[1] + bl.units[2]) + 16.0 * bl.small_count;
-  if (diag_enabled()) CBH_TRY((launch_large_diag<SR, NumLarge, MODE_NUM>(ctx, a, bl, "numeric")));
-  else CBH_TRY((launch_tile<SR, NumLarge, MODE_NUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
-  CBH_TRY((launch_tile<SR, NumSmall, MODE_NUM>(ctx, a, bl.small_first, bl.small_count, CBH_K_NUM_SMALL, nb_s)));
-  if (launches) *launches += (bl.large_count > 0) + (bl.small_count > 0);
+  const double nb_l = eb * bl.units[2] + 16.0 * bl.large_count;
+  const double nb_s = eb * (bl.units[0] + bl.units[1]) + 16.0 * (bl.small_count + bl.mid_count);
+  if (diag_enabled()) CBH_TRY((launch_task_diag<SR, TNumLarge, MODE_TNUM>(ctx, a, bl, "numeric")));
+  else CBH_TRY((launch_task<SR, TNumLarge, MODE_TNUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
+  CBH_TRY((launch_task<SR, TNumSmall, MODE_TNUM>(ctx, a, bl.small_first, bl.small_count + bl.mid_count,
+                                                  CBH_K_NUM_SMALL, nb_s)));
+  if (launches) *launches += (bl.large_count > 0) + (bl.small_count + bl.mid_count > 0);
   return CBH_OK;
 }
 
@@ -986,7 +1166,7 @@ int cbh_spgemm(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh_mat* B
     }
     CBH_TRY(new_mat(ctx, A->m, B->n, P.total_nnz, nzcC, A->dtype, &out));
     int64_t launches = 0;
-    int rc = run_numeric<SR>(ctx, S, A, B, P, 0, P.nzcB, 0, out->ir, out->num, &launches, P.total_nnz);
+    int rc = run_numeric<SR>(ctx, S, A, B, P, 0, P.ntasks, 0, out->ir, out->num, &launches, P.total_nnz);
     if (rc == CBH_OK) {
       if (keep) {
         (void)hipMemcpyAsync(out->jc, B->jc, sizeof(int64_t) * P.nzcB, hipMemcpyDeviceToDevice, ctx->stream);
@@ -1041,8 +1221,9 @@ int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh
     }
     int64_t budget = std::max<int64_t>(1, std::min<int64_t>(budget_bytes / (int64_t)esz, P.total_nnz));
     // phase boundaries over B's column slots from the exact column offsets
-    std::vector<int64_t> hcp(P.nzcB + 1);
+    std::vector<int64_t> hcp(P.nzcB + 1), hts(P.nzcB + 1);
     CBH_HIP(ctx, hipMemcpyAsync(hcp.data(), P.Ccp, sizeof(int64_t) * (P.nzcB + 1), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(hts.data(), P.tstart, sizeof(int64_t) * (P.nzcB + 1), hipMemcpyDeviceToHost, ctx->stream));
     CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
     std::vector<int64_t> cuts{0};
     int64_t maxcol = 0;
@@ -1091,7 +1272,7 @@ int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh
     for (size_t i = 1; i < cuts.size(); ++i) {
       const int64_t c0 = cuts[i - 1], c1 = cuts[i];
       const double tp = hnow();
-      CBH_TRY(run_numeric<SR>(ctx, S, A, B, P, c0, c1, hcp[c0], ir, num, &launches, maxphase));
+      CBH_TRY(run_numeric<SR>(ctx, S, A, B, P, hts[c0], hts[c1], hcp[c0], ir, num, &launches, maxphase));
       if (diag_enabled()) {
         CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
         std::fprintf(stderr, "[cbh diag] phase %zu: cols [%lld,%lld) %.1f ms host wall\n", i, (long long)c0,

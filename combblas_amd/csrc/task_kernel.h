@@ -1,0 +1,475 @@
+// gfx950 SpGEMM kernels, TASK-PARALLEL form (the SpGEMM hot path; merges still use tile_kernel.h).
+//
+// A task is one row range [lo, hi) of one output column j (one nonzero column of B). Heavy
+// columns are cut into tasks of about kTaskFlops products, so the heaviest column of R-MAT
+// scale 22 (15.7 M products, 752 K outputs) spreads over hundreds of workgroups instead of one
+// (the per-column row-tile loop of tile_kernel.h was tail-bound). R-MAT rows are scrambled
+// (uniform), so equal-width row ranges carry equal work.
+//
+// Inside a task the range is processed in SUB-TILES that fit one LDS table, one after another.
+// Every B entry k of the column keeps, in LDS, a cursor into its row-sorted A column and the row
+// at that cursor: an entry with no product in the current sub-tile costs one LDS read (no global
+// traffic), an active one gallops forward from its cursor. Products of a sub-tile are flattened
+// (LDS scan of segment lengths), each thread gathers U of them before any table update
+// (memory-level parallelism), and an owner map (segment starts + block max-scan) names the entry.
+//
+//   symbolic (MODE_TSYM): distinct rows of the task -> cnt[task]        [estimateNNZ_Hash, mtSpGEMM.h:806-933]
+//            sub-tile = an LDS bitmap over 32*T rows (exact, no hashing) or, for sparse ranges,
+//            an LDS key hash of <= T/2 products -- whichever needs fewer sub-tiles.
+//   offsets : exclusive scan of cnt over tasks (a column's tasks are consecutive, in row order),
+//             so every task knows where its outputs go and C's column pointers fall out.
+//   numeric (MODE_TNUM): SR::add(SR::multiply(a,b)) into an order-preserving LDS hash (slot =
+//            (row-lo)*T/(hi-lo), forward probing), sub-tiles of <= T/2 outputs, written at
+//            toff[task] with rows ascending                              [LocalHybridSpGEMM, mtSpGEMM.h:289-441]
+//            Commit without sorting: keys in different runs of occupied slots are already in
+//            order, so slot s goes to (occupied slots before its run) + (rank of
+//            its key inside the run) -- replaces the per-column std::sort (mtSpGEMM.h:434).
+// Columns with more than EMAX entries are processed in entry chunks whose cursors are re-derived
+// by binary search every sub-tile (slower path; rare on R-MAT: 16 % of scale-22 flops).
+#pragma once
+#include "tile_kernel.h"
+
+namespace cbh {
+
+enum : int { MODE_TSYM = 0, MODE_TNUM = 1 };
+constexpr int32_t kNoRow = 0x7fffffff;
+
+// Diagnostic build only (-DCBH_STAMPS, libcombblas_hip_stamps.so): thread 0 of every workgroup
+// adds the s_memtime cycles of each kernel phase (delimited by block barriers) into g_stamps.
+#ifdef CBH_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define CBH_STAMP(k)                                    \
+  do {                                                  \
+    if (threadIdx.x == 0) {                             \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+      st_[k] += t_ - t_prev_;                           \
+      t_prev_ = t_;                                     \
+    }                                                   \
+  } while (0)
+#else
+#define CBH_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
+struct TaskArgs {
+  const int64_t* Acp;  // A dense column pointers (A.n + 1)
+  const int32_t* Air;
+  const void* Anum;
+  const int64_t* Bcp;  // B DCSC column pointers (per nonzero column slot)
+  const int32_t* Bir;
+  const void* Bnum;
+  const int32_t* order;  // task ids in launch order
+  int64_t norder;
+  const int32_t* tcol;   // per task: column slot j
+  const int32_t* tlo;    // per task: row range [lo, hi)
+  const int32_t* thi;
+  const uint8_t* tfull;  // per task: bit0 = lo is the column's first row, bit1 = hi past its last row
+  const int64_t* twork;  // symbolic: flops of the task (estimate); numeric: exact output count
+  int64_t* cnt;          // symbolic output
+  const int64_t* toff;   // numeric: output offset of every task
+  int64_t cbase;
+  int32_t* Cir;
+  void* Cnum;
+  int64_t ccap;
+  int* err;
+  int64_t nnzA, ncolA, ntasks;
+};
+
+// first q in [lo, hi) with rows[q] >= key (rows sorted); global memory, 64-bit positions
+__device__ __forceinline__ int64_t lb_rows64(const int32_t* __restrict__ rows, int64_t lo, int64_t hi, int32_t key) {
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (rows[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+// galloping lower bound from lo (rows[lo-1] < key is known): lo, lo+1, lo+3, lo+7, ...
+__device__ __forceinline__ int64_t gallop64(const int32_t* __restrict__ rows, int64_t lo, int64_t hi, int32_t key) {
+  int64_t step = 1, prev = lo;
+  int64_t nx = lo;
+  while (nx < hi) {
+    if (rows[nx] >= key) return lb_rows64(rows, prev, nx, key);
+    prev = nx + 1;
+    nx = lo + step;
+    step <<= 1;
+  }
+  return lb_rows64(rows, prev, hi, key);
+}
+
+template <class SR, int T, int BS, int EMAX, int U, int MODE>
+struct TaskCfg {
+  static constexpr bool NUM = MODE == MODE_TNUM;
+  using val_t = typename SR::val_t;
+  using acc_t = typename SR::acc_t;
+  static constexpr int TA = NUM ? T + kGuard : T;  // slots (symbolic: 32-bit words, keys or bitmap)
+  static constexpr int NW = BS / 64;
+  static constexpr int WIN = U * BS;
+  static constexpr size_t al(size_t x) { return (x + 15) & ~size_t(15); }
+  static constexpr size_t o_keys = 0;
+  static constexpr size_t o_vals = al(o_keys + sizeof(int32_t) * TA);
+  static constexpr size_t o_pos = al(o_vals + (NUM ? sizeof(acc_t) * TA : 0));
+  static constexpr size_t o_end = al(o_pos + sizeof(int64_t) * EMAX);
+  static constexpr size_t o_qoff = al(o_end + sizeof(int64_t) * EMAX);
+  static constexpr size_t o_scale = al(o_qoff + sizeof(int64_t) * EMAX);
+  static constexpr size_t o_next = al(o_scale + (NUM ? sizeof(val_t) * EMAX : 0));
+  static constexpr size_t o_next2 = al(o_next + sizeof(int32_t) * EMAX);
+  static constexpr size_t o_off = al(o_next2 + sizeof(int32_t) * EMAX);
+  static constexpr size_t o_own = al(o_off + sizeof(int32_t) * (EMAX + 1));
+  static constexpr size_t o_red = al(o_own + sizeof(int32_t) * WIN);
+  static constexpr size_t bytes = al(o_red + sizeof(int32_t) * (2 * NW + 4));
+};
+
+template <class SR, int T, int BS, int EMAX, int U, int MODE>
+__global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
+  using C = TaskCfg<SR, T, BS, EMAX, U, MODE>;
+  using val_t = typename C::val_t;
+  using acc_t = typename C::acc_t;
+  constexpr bool NUM = C::NUM;
+  constexpr int TA = C::TA, NW = C::NW, WIN = C::WIN;
+  static_assert((T & (T - 1)) == 0, "table size must be a power of two");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int32_t* keys = reinterpret_cast<int32_t*>(smem + C::o_keys);
+  uint32_t* words = reinterpret_cast<uint32_t*>(smem + C::o_keys);
+  acc_t* vals = reinterpret_cast<acc_t*>(smem + C::o_vals);
+  int64_t* epos = reinterpret_cast<int64_t*>(smem + C::o_pos);    // cursor (absolute index into A)
+  int64_t* eend = reinterpret_cast<int64_t*>(smem + C::o_end);    // end of the A column
+  int64_t* qoff = reinterpret_cast<int64_t*>(smem + C::o_qoff);   // epos - exclusive offset
+  val_t* escale = reinterpret_cast<val_t*>(smem + C::o_scale);    // B value
+  int32_t* enext = reinterpret_cast<int32_t*>(smem + C::o_next);  // row at the cursor (kNoRow: done)
+  int32_t* enext2 = reinterpret_cast<int32_t*>(smem + C::o_next2);  // row at the sub-tile's stop
+  int32_t* eoff = reinterpret_cast<int32_t*>(smem + C::o_off);
+  int32_t* own = reinterpret_cast<int32_t*>(smem + C::o_own);
+  int32_t* red = reinterpret_cast<int32_t*>(smem + C::o_red);
+  __shared__ int32_t s_ovf;  // overflow flag of the current sub-tile (LDS; read after barriers)
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#ifdef CBH_STAMPS
+  uint64_t st_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t t_prev_ = __builtin_amdgcn_s_memtime();
+#endif
+  if ((int64_t)blockIdx.x >= a.norder) return;
+  const int32_t task = a.order[blockIdx.x];
+  if (task < 0 || task >= a.ntasks) {
+    if (tid == 0) guard_fail(a.err, 9, task);
+    return;
+  }
+  const int32_t c = a.tcol[task];
+  const int64_t e0 = a.Bcp[c];
+  const int64_t ne = a.Bcp[c + 1] - e0;
+  const int64_t work = a.twork[task];
+  const int32_t tlo = a.tlo[task], thi = a.thi[task];
+  const uint8_t full = a.tfull[task];
+  if (work <= 0 || thi <= tlo) {
+    if (!NUM && tid == 0) a.cnt[task] = 0;
+    return;
+  }
+  const int64_t span = (int64_t)thi - tlo;
+  // sub-tile plan (uniform in rows)
+  bool bitmap = false;
+  int64_t R;
+  {
+    constexpr int64_t cap = T / 2;
+    R = (work + cap - 1) / cap;
+    if (!NUM) {
+      const int64_t Rb = (span + 32ll * T - 1) / (32ll * T);
+      if (Rb <= R) {
+        bitmap = true;
+        R = Rb;
+      }
+    }
+    if (R > span) R = span;
+    if (R < 1) R = 1;
+  }
+  const int64_t wnom = (span + R - 1) / R;
+  const bool chunked = ne > EMAX;
+  const int nchunks = chunked ? (int)((ne + EMAX - 1) / EMAX) : 1;
+
+  // violated bounds guards are recorded in a register and reported once at the end: a guard_fail
+  // (global atomics with return values) inside a hot loop makes the compiler drain vmcnt there
+  int bad = 0;  // bit k: guard site k violated
+  // entry state of entries [first, first+cnt): cursor at the first row >= lo
+  auto load_entries = [&](int64_t first, int cnt, int32_t lo, bool lo_is_start) {
+    for (int i = tid; i < cnt; i += BS) {
+      const int64_t p = e0 + first + i;
+      const int32_t k = a.Bir[p];
+      int64_t base = 0, end = 0;
+      if (k < 0 || k >= a.ncolA) {
+        bad |= 1 << 1;
+      } else {
+        base = a.Acp[k];
+        end = a.Acp[k + 1];
+        if (base < 0 || end < base || end > a.nnzA) {
+          bad |= 1 << 2;
+          base = end = 0;
+        }
+      }
+      if constexpr (NUM) escale[i] = reinterpret_cast<const val_t*>(a.Bnum)[p];
+      const int64_t pos = (lo_is_start || base == end) ? base : lb_rows64(a.Air, base, end, lo);
+      epos[i] = pos;
+      eend[i] = end;
+      enext[i] = pos < end ? a.Air[pos] : kNoRow;
+    }
+  };
+
+  if (!chunked) {
+    load_entries(0, (int)ne, tlo, (full & 1) != 0);
+    __syncthreads();
+  }
+  CBH_STAMP(0);
+
+  int64_t out_pos = 0, out_end = 0;
+  if constexpr (NUM) {
+    out_pos = a.toff[task] - a.cbase;
+    out_end = a.toff[task + 1] - a.cbase;
+  }
+  int my_count = 0;  // symbolic hash: keys this thread inserted first
+
+  int32_t lo = tlo;
+  int64_t w = wnom;
+  while (lo < thi) {
+    const int32_t hi = (int32_t)(((int64_t)lo + w < thi) ? lo + w : thi);
+    const bool hi_is_end = hi == thi && (full & 2);
+    const uint32_t tw = (uint32_t)(hi - lo);
+    const uint64_t scale = ((uint64_t)T << 32) / (uint64_t)tw;  // numeric order-preserving slot map
+    if (bitmap) {
+      const int nwords = (int)((tw + 31) >> 5);
+      for (int s = tid; s < nwords; s += BS) words[s] = 0u;
+    } else {
+      for (int s = tid; s < TA; s += BS) {
+        keys[s] = kEmpty;
+        if constexpr (NUM) vals[s] = SR::identity();
+      }
+    }
+    if (tid == 0) __hip_atomic_store(&s_ovf, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int count_before = my_count;
+    __syncthreads();
+    CBH_STAMP(1);
+
+    for (int ch = 0; ch < nchunks; ++ch) {
+      int nec = (int)ne;
+      if (chunked) {
+        const int64_t first = (int64_t)ch * EMAX;
+        nec = (int)((ne - first) < EMAX ? (ne - first) : EMAX);
+        load_entries(first, nec, lo, lo == tlo && (full & 1));
+        __syncthreads();
+      }
+      // segment of every entry inside [lo, hi): idle entries (next row >= hi) cost one LDS read
+      for (int i = tid; i < nec; i += BS) {
+        const int32_t nx = enext[i];
+        const int64_t p = epos[i];
+        int64_t stop = p;
+        int32_t nx2 = nx;
+        if (nx < hi) {
+          const int64_t end = eend[i];
+          if (hi_is_end) {
+            stop = end;
+            nx2 = kNoRow;
+          } else {
+            stop = gallop64(a.Air, p + 1, end, hi);
+            nx2 = stop < end ? a.Air[stop] : kNoRow;
+          }
+        }
+        eoff[i] = (int32_t)(stop - p);
+        enext2[i] = nx2;
+      }
+      __syncthreads();
+      CBH_STAMP(2);
+      block_scan_excl<BS>(eoff, nec, red);
+      for (int i = tid; i < nec; i += BS) qoff[i] = epos[i] - eoff[i];
+      const int P = eoff[nec];
+      CBH_STAMP(3);
+      int carry = -1;  // owner of the product just before the window
+      for (int w0 = 0; w0 < P; w0 += WIN) {
+        const int wn = (P - w0) < WIN ? (P - w0) : WIN;
+        for (int x = tid; x < WIN; x += BS) own[x] = (x == 0) ? carry : -1;
+        __syncthreads();
+        for (int i = tid; i < nec; i += BS) {
+          const int s0 = eoff[i];
+          if (s0 >= w0 && s0 < w0 + wn && eoff[i + 1] > s0) own[s0 - w0] = i;
+        }
+        __syncthreads();
+        block_max_scan<BS, WIN>(own, red);
+        carry = own[wn - 1];
+        CBH_STAMP(4);
+        if (!bitmap && __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+        // gather U products per thread first (all loads in flight), then update the table
+        // (branch-free: lanes past the window re-read product 0 and are masked afterwards)
+        int32_t r[U];
+        int ow[U];
+        val_t av[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int x0 = tid + u * BS;
+          const int x = x0 < wn ? x0 : 0;
+          const int i = own[x];
+          const int64_t q = qoff[i] + w0 + x;
+          ow[u] = i;
+          r[u] = a.Air[q];
+          if constexpr (NUM) av[u] = reinterpret_cast<const val_t*>(a.Anum)[q];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (tid + u * BS >= wn) continue;
+          val_t vv{};
+          if constexpr (NUM) vv = SR::multiply(av[u], escale[ow[u]]);
+          const uint32_t d = (uint32_t)(r[u] - lo);
+          if (d >= tw) {
+            bad |= 1 << 8;
+            continue;
+          }
+          if (bitmap) {
+            atomicOr(&words[d >> 5], 1u << (d & 31));
+          } else if constexpr (NUM) {
+            uint32_t s = (uint32_t)(((uint64_t)d * scale) >> 32);
+            bool ok = false;
+            for (int probe = 0; probe < kPmax && s < (uint32_t)TA; ++probe, ++s) {
+              const int32_t k = atomicCAS(&keys[s], kEmpty, r[u]);
+              if (k == kEmpty || k == r[u]) {
+                SR::lds_acc(&vals[s], vv);
+                ok = true;
+                break;
+              }
+            }
+            if (!ok) __hip_atomic_store(&s_ovf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          } else {
+            constexpr int LG = __builtin_ctz(T);
+            uint32_t s = ((uint32_t)r[u] * 0x9E3779B1u) >> (32 - LG);
+            bool ok = false;
+            for (int probe = 0; probe < 2 * kPmax; ++probe, s = (s + 1) & (T - 1)) {
+              const int32_t k = atomicCAS(&keys[s], kEmpty, r[u]);
+              if (k == kEmpty) ++my_count;
+              if (k == kEmpty || k == r[u]) {
+                ok = true;
+                break;
+              }
+            }
+            if (!ok) __hip_atomic_store(&s_ovf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
+        __syncthreads();
+        CBH_STAMP(5);
+      }
+      if (!bitmap && __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+      if (chunked) __syncthreads();  // entry state is reloaded by the next chunk
+    }
+    if (!bitmap && __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {  // table could not hold the sub-tile: halve the row range, redo
+      __syncthreads();
+      my_count = count_before;
+      if (tw == 1) {
+        if (tid == 0) atomicOr(&a.err[1], 1);
+        return;
+      }
+      w = (tw + 1) / 2;
+      continue;
+    }
+    CBH_STAMP(8);
+    if (!chunked)  // advance the cursors past the committed sub-tile
+      for (int i = tid; i < (int)ne; i += BS) {
+        epos[i] = qoff[i] + eoff[i + 1];
+        enext[i] = enext2[i];
+      }
+    if (bitmap) {
+      const int nwords = (int)((tw + 31) >> 5);
+      for (int s = tid; s < nwords; s += BS) my_count += __popc(words[s]);
+    } else if constexpr (NUM) {
+      // rank commit: wave w owns 64-aligned slot blocks; pass 1 counts, one barrier, pass 2 places
+      // every occupied slot at (occupied slots before its run) + (rank of its key in the run).
+      // Run bounds come from the occupancy ballot, ranks from shuffles; runs crossing a 64-slot
+      // group boundary (rare at load <= 1/2) take an LDS walk.
+      constexpr int SPW = ((TA + NW - 1) / NW + 63) / 64 * 64;
+      const int sb = wid * SPW, se = (sb + SPW < TA) ? sb + SPW : TA;
+      int wc = 0;
+      for (int s0 = sb; s0 < se; s0 += 64) {
+        const int s = s0 + lane;
+        wc += __popcll(__ballot(s < se && keys[s] != kEmpty));
+      }
+      if (lane == 0) red[NW + wid] = wc;
+      __syncthreads();
+      CBH_STAMP(9);
+      int64_t o = out_pos;
+      int tot = 0;
+#pragma unroll
+      for (int x = 0; x < NW; ++x) {
+        const int rr = red[NW + x];
+        o += (x < wid) ? rr : 0;
+        tot += rr;
+      }
+      const uint64_t lt = (1ull << lane) - 1ull;
+      for (int s0 = sb; s0 < se; s0 += 64) {
+        const int s = s0 + lane;
+        const int32_t key = (s < se) ? keys[s] : kEmpty;
+        const bool occ = key != kEmpty;
+        const uint64_t mask = __ballot(occ);
+        if (mask == 0) continue;
+        const bool prev_occ = s0 > 0 && keys[s0 - 1] != kEmpty;
+        const bool next_occ = s0 + 64 < TA && keys[s0 + 64] != kEmpty;
+        const uint64_t below = ~mask & lt;
+        const uint64_t above = ~mask & ~(lt | (1ull << lane));
+        const int rs = below ? 64 - __clzll(below) : 0;  // first lane of the run
+        const int re = above ? __ffsll((long long)above) - 1 : 64;  // one past its last lane
+        const bool cross = occ && ((rs == 0 && prev_occ) || (re == 64 && next_occ));
+        const bool inr = occ && !cross;
+        const int len = re - rs;
+        // rank inside the run: compare with the keys d lanes to the left and right, d = 1, 2, ...
+        // (DPP whole-wave shifts: VALU only, no LDS round trip)
+        int rank = 0;
+        {
+          int32_t kl = key, kr = key;
+          for (int d = 1; __ballot(inr && d < len) != 0; ++d) {
+            kl = __builtin_amdgcn_update_dpp(kEmpty, kl, 0x138, 0xf, 0xf, false);  // wave_shr:1
+            kr = __builtin_amdgcn_update_dpp(kEmpty, kr, 0x130, 0xf, 0xf, false);  // wave_shl:1
+            rank += (inr && lane - d >= rs && kl < key) ? 1 : 0;
+            rank += (inr && lane + d < re && kr < key) ? 1 : 0;
+          }
+        }
+        int lead = lane - rs;  // run slots before this one
+        if (occ && cross) {
+          int a0 = s;
+          while (a0 > 0 && keys[a0 - 1] != kEmpty) --a0;
+          rank = 0;
+          for (int x = a0; x < TA; ++x) {
+            const int32_t kx = keys[x];
+            if (kx == kEmpty) break;
+            rank += kx < key;
+          }
+          lead = s - a0;
+        }
+        if (occ) {
+          const int64_t pos = o + __popcll(mask & lt) - lead + rank;
+          if (pos >= out_end || pos >= a.ccap || pos < 0) {
+            bad |= 1 << 5;
+          } else {
+            a.Cir[pos] = key;
+            reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(vals[s]);
+          }
+        }
+        o += __popcll(mask);
+      }
+      CBH_STAMP(10);
+      out_pos += tot;
+    }
+    lo = hi;
+    w = wnom;
+    __syncthreads();
+    CBH_STAMP(6);
+  }
+  if constexpr (!NUM) {
+    const int total = block_sum_int<NW>(my_count, red);
+    if (tid == 0) a.cnt[task] = total;
+  } else {
+    if (tid == 0 && out_pos != out_end) atomicAdd(&a.err[0], 1);
+  }
+  if (bad) guard_fail(a.err, 31 - __clz(bad), c, bad, lo);
+#ifdef CBH_STAMPS
+  CBH_STAMP(7);
+  if (tid == 0) {
+    for (int k = 0; k < 12; ++k) atomicAdd(&g_stamps[k], (unsigned long long)st_[k]);
+    atomicAdd(&g_stamps[12], 1ull);
+  }
+#endif
+}
+
+}  // namespace cbh
