@@ -375,12 +375,27 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
       const int nwords = (int)((tw + 31) >> 5);
       for (int s = tid; s < nwords; s += BS) my_count += __popc(words[s]);
     } else if constexpr (NUM) {
-      // rank commit: wave w owns 64-aligned slot blocks; pass 1 counts, one barrier, pass 2 places
-      // every occupied slot at (occupied slots before its run) + (rank of its key in the run).
-      // Run bounds come from the occupancy ballot, ranks from shuffles; runs crossing a 64-slot
-      // group boundary (rare at load <= 1/2) take an LDS walk.
+      // rank commit. Slot s goes to (occupied slots before its run) + (rank of its key in the
+      // run). Wave regions and 64-slot chunks start at run boundaries (a wave's region begins at
+      // an empty slot; a chunk whose last run continues stops before that run), so every run
+      // lies inside one chunk: run bounds come from the occupancy ballot, ranks from DPP shifts.
       constexpr int SPW = ((TA + NW - 1) / NW + 63) / 64 * 64;
-      const int sb = wid * SPW, se = (sb + SPW < TA) ? sb + SPW : TA;
+      int sb = wid * SPW;
+      if (wid > 0) {
+        int found = TA;
+        for (int s0 = sb; s0 < TA; s0 += 64) {
+          const int s = s0 + lane;
+          const uint64_t em = __ballot(s < TA && keys[s] == kEmpty);
+          if (em) {
+            found = s0 + __ffsll((long long)em) - 1;
+            break;
+          }
+        }
+        sb = found < TA ? found : TA;
+      }
+      if (lane == 0) red[wid] = sb;
+      __syncthreads();
+      const int se = (wid + 1 < NW) ? red[wid + 1] : TA;
       int wc = 0;
       for (int s0 = sb; s0 < se; s0 += 64) {
         const int s = s0 + lane;
@@ -388,7 +403,6 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
       }
       if (lane == 0) red[NW + wid] = wc;
       __syncthreads();
-      CBH_STAMP(9);
       int64_t o = out_pos;
       int tot = 0;
 #pragma unroll
@@ -398,38 +412,46 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         tot += rr;
       }
       const uint64_t lt = (1ull << lane) - 1ull;
-      for (int s0 = sb; s0 < se; s0 += 64) {
+      int s0 = sb;
+      while (s0 < se) {
         const int s = s0 + lane;
         const int32_t key = (s < se) ? keys[s] : kEmpty;
+        const acc_t val = (s < se) ? vals[s] : SR::identity();
         const bool occ = key != kEmpty;
-        const uint64_t mask = __ballot(occ);
-        if (mask == 0) continue;
-        const bool prev_occ = s0 > 0 && keys[s0 - 1] != kEmpty;
-        const bool next_occ = s0 + 64 < TA && keys[s0 + 64] != kEmpty;
+        uint64_t mask = __ballot(occ);
+        // the chunk's last run continues past the chunk: stop the chunk before that run
+        int cut = 64;
+        bool walk = false;
+        if ((mask >> 63) && s0 + 64 < se && keys[s0 + 64] != kEmpty) {
+          const uint64_t em = ~mask;
+          if (em) cut = 64 - __clzll(em);  // one past the last empty lane
+          else walk = true;                // a run of >= 64 slots (clustered rows): LDS walk
+        }
+        const uint64_t keep = cut == 64 ? ~0ull : ((1ull << cut) - 1ull);
+        mask &= keep;
+        const bool mine = occ && lane < cut;
         const uint64_t below = ~mask & lt;
-        const uint64_t above = ~mask & ~(lt | (1ull << lane));
-        const int rs = below ? 64 - __clzll(below) : 0;  // first lane of the run
-        const int re = above ? __ffsll((long long)above) - 1 : 64;  // one past its last lane
-        const bool cross = occ && ((rs == 0 && prev_occ) || (re == 64 && next_occ));
-        const bool inr = occ && !cross;
+        const uint64_t above = ~mask & ~(lt | (1ull << lane)) & keep;
+        const int rs = below ? 64 - __clzll(below) : 0;
+        const int re = above ? __ffsll((long long)above) - 1 : cut;
         const int len = re - rs;
-        // rank inside the run: compare with the keys d lanes to the left and right, d = 1, 2, ...
-        // (DPP whole-wave shifts: VALU only, no LDS round trip)
-        int rank = 0;
+        // the chunk's first run may be the tail of a >= 64-slot run begun in a walked chunk
+        const bool prev_occ = s0 > sb && keys[s0 - 1] != kEmpty;
+        const bool lw = mine && (walk || (prev_occ && rs == 0));
+        const bool dp = mine && !lw;
+        int rank = 0, lead = lane - rs;
         {
           int32_t kl = key, kr = key;
-          for (int d = 1; __ballot(inr && d < len) != 0; ++d) {
+          for (int d = 1; __ballot(dp && d < len) != 0; ++d) {
             kl = __builtin_amdgcn_update_dpp(kEmpty, kl, 0x138, 0xf, 0xf, false);  // wave_shr:1
             kr = __builtin_amdgcn_update_dpp(kEmpty, kr, 0x130, 0xf, 0xf, false);  // wave_shl:1
-            rank += (inr && lane - d >= rs && kl < key) ? 1 : 0;
-            rank += (inr && lane + d < re && kr < key) ? 1 : 0;
+            rank += (dp && lane - d >= rs && kl < key) ? 1 : 0;
+            rank += (dp && lane + d < re && kr < key) ? 1 : 0;
           }
         }
-        int lead = lane - rs;  // run slots before this one
-        if (occ && cross) {
+        if (lw) {
           int a0 = s;
           while (a0 > 0 && keys[a0 - 1] != kEmpty) --a0;
-          rank = 0;
           for (int x = a0; x < TA; ++x) {
             const int32_t kx = keys[x];
             if (kx == kEmpty) break;
@@ -437,18 +459,18 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
           }
           lead = s - a0;
         }
-        if (occ) {
+        if (mine) {
           const int64_t pos = o + __popcll(mask & lt) - lead + rank;
           if (pos >= out_end || pos >= a.ccap || pos < 0) {
             bad |= 1 << 5;
           } else {
             a.Cir[pos] = key;
-            reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(vals[s]);
+            reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(val);
           }
         }
         o += __popcll(mask);
+        s0 += cut;
       }
-      CBH_STAMP(10);
       out_pos += tot;
     }
     lo = hi;
