@@ -9,10 +9,11 @@ whole product: symbolic pass (estimateFLOP + exact nnz) and every numeric column
 materialised in HBM one after another (MemEfficientSpGEMM's phase loop, ParFriends.h:449-730).
 Inputs are resident in HBM before the timed region.
 
-N>1 (launched by torch.distributed.run): the same fixed product is split into N column stripes
-of B with equal flops; every rank holds A (generated locally, no data-path collective) and
-computes its stripe -> "scaling": "strong". Timing: barrier + synchronize around exactly K steps,
-max over ranks.
+N>1 (launched by torch.distributed.run): the same fixed product on a process grid, as the
+reference distributes it (north_star): 2D SUMMA with RCCL row/column broadcasts of the DCSC
+blocks on a square world (4 GPUs = 2x2), 3D SUMMA otherwise (2 GPUs = 1x1x2, 8 GPUs = 2x2x2:
+per-layer SUMMA + the fiber reduce-scatter as an RCCL alltoall), every phase of C materialised in
+HBM -> "scaling": "strong". Timing: barrier + synchronize around exactly K steps, max over ranks.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scale 22]
 """
@@ -33,7 +34,7 @@ sys.path.insert(0, HERE)
 METRIC = "semiring GFLOP/s for R-MAT A² SpGEMM at 1/2/4/8 GPUs; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
 DOMINANT = "num_large"
-DOMINANT_KERNEL = "cbh::tile_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 1>"
+DOMINANT_KERNEL = "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 4, 1>"
 
 
 def parse():
@@ -47,28 +48,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-cols-frac", type=float, default=1.0 / 64, help="column sample of the CPU baseline")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on a node; gloo only for rehearsals")
+    p.add_argument("--share-gpu", action="store_true", help="rehearsal: every rank on cuda:0 (needs gloo)")
     return p.parse_args()
-
-
-def column_stripe(A, world, rank):
-    """B's nonzero columns split into `world` contiguous stripes of equal flops."""
-    if world == 1:
-        return 0, A.nzc
-    dense = np.zeros(A.n + 1, np.int64)
-    dense[A.jc + 1] = np.diff(A.cp)
-    lenA = dense[1:]
-    flop = np.add.reduceat(lenA[A.ir].astype(np.int64), A.cp[:-1]) if A.nnz else np.zeros(0, np.int64)
-    cum = np.concatenate([[0], np.cumsum(flop)])
-    cuts = [int(np.searchsorted(cum, cum[-1] * r / world)) for r in range(world + 1)]
-    cuts[0], cuts[-1] = 0, A.nzc
-    return cuts[rank], cuts[rank + 1]
-
-
-def slice_cols(A, i0, i1):
-    import combblas_amd as cb
-
-    s, e = A.cp[i0], A.cp[i1]
-    return cb.HostDcsc(A.m, A.n, A.jc[i0:i1], A.cp[i0:i1 + 1] - s, A.ir[s:e], A.num[s:e])
 
 
 def cpu_baseline(scale, ef, frac):
@@ -109,6 +91,25 @@ def cpu_baseline(scale, ef, frac):
             "sample": sample + f": {flops} flops in {dt:.3f} s (oracle restatement), nnzC {C.nnz}"}
 
 
+def grid_shape(world):
+    """2D SUMMA on a square world (1, 4, 9, ...); otherwise 3D with the fewest layers that leave a
+    square layer grid (2 -> 1x1x2, 8 -> 2x2x2), as BASELINE.json's north_star lays out."""
+    import math
+
+    for layers in range(1, world + 1):
+        if world % layers == 0 and math.isqrt(world // layers) ** 2 == world // layers:
+            return layers
+    return world
+
+
+def host_flops(A):
+    """flops(A*A) = sum_k nnz(A(:,k)) * nnz(A(k,:)) (EstimateFLOP, ParFriends.h:355-441)"""
+    colnnz = np.zeros(A.n, np.int64)
+    colnnz[A.jc] = np.diff(A.cp)
+    rownnz = np.bincount(A.ir, minlength=A.m).astype(np.int64)
+    return int(np.dot(colnnz, rownnz))
+
+
 def main():
     args = parse()
     import torch
@@ -118,10 +119,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.share_gpu:  # rehearsal of the N-rank path on a one-GPU box (gloo, ranks share cuda:0)
+        local = 0
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -133,24 +139,79 @@ def main():
     def allreduce(x, op):
         t = torch.tensor([x], dtype=torch.float64, device=dev)
         if world > 1:
+            if args.dist_backend == "gloo":
+                t = t.cpu()
             dist.all_reduce(t, op=op)
         return t.item()
 
-    # ---------------------------------------------------------------- inputs (resident in HBM)
-    A = cb.rmat(args.scale, args.edgefactor, dtype=np.float64)
-    i0, i1 = column_stripe(A, world, rank)
-    Bs = slice_cols(A, i0, i1)
-    ctx = cb.Context(local, torch_allocator=False)
-    if args.phase_budget_gb > 0:
-        ctx.set_phase_budget(int(args.phase_budget_gb * 2**30))
-    dA = cb.SpDCCols.from_host(ctx, A)
-    dB = cb.SpDCCols.from_host(ctx, Bs)  # separate copy (aliasing is rejected, ParFriends.h:172)
-    nnzA = A.nnz
-    del A, Bs
     SR = cb.PlusTimesSRing
+    A = cb.rmat(args.scale, args.edgefactor, dtype=np.float64)
+    nnzA = A.nnz
+    if world == 1:
+        # ------------------------------------------------------------ 1 GPU: device phase loop
+        ctx = cb.Context(local, torch_allocator=False)
+        if args.phase_budget_gb > 0:
+            ctx.set_phase_budget(int(args.phase_budget_gb * 2**30))
+        dA = cb.SpDCCols.from_host(ctx, A)
+        dB = cb.SpDCCols.from_host(ctx, A)  # separate copy (aliasing is rejected, ParFriends.h:172)
+        del A
+
+        def step():
+            return cb.PhasedSpGEMM(SR, dA, dB)
+
+        def verify():
+            sv = cb.PhasedSpGEMM(SR, dA, dB, checksum=True)
+            return sv["nnz"], sv["value_sum"]
+        parallelism = "1 GPU"
+    else:
+        # ------------------------------------------------------------ N GPUs: SUMMA over RCCL
+        from combblas_amd import parfriends as pf
+        from combblas_amd.backend import HipBackend
+        from combblas_amd.commgrid import CommGrid, CommGrid3D
+        from combblas_amd.spparmat import SpParMat, SpParMat3D
+
+        ctx = cb.Context(local)
+        be = HipBackend(ctx)
+        layers = grid_shape(world)
+        flops_total = host_flops(A)
+        budget = int(args.phase_budget_gb * 2**30) if args.phase_budget_gb > 0 else 0
+        if layers == 1:
+            grid = CommGrid()
+            dA, dB = SpParMat.distribute(A, grid, be), SpParMat.distribute(A, grid, be)
+            parallelism = f"2D SUMMA {grid.grrows}x{grid.grcols} (RCCL broadcasts)"
+        else:
+            g3 = CommGrid3D(layers)
+            dA = SpParMat3D.distribute(A, g3, be, colsplit=True)
+            dB = SpParMat3D.distribute(A, g3, be, colsplit=False)
+            parallelism = f"3D SUMMA {g3.gridRows}x{g3.gridCols}x{layers} (RCCL broadcasts + fiber alltoall)"
+        del A
+        acc = {}
+
+        def consume(C, c0, c1):
+            acc["nnz"] = acc.get("nnz", 0) + be.dims(C)[2]
+            if acc.get("sum") is not None:
+                acc["sum"] += float(be.arrays(C)[3].sum().item()) if be.dims(C)[2] else 0.0
+
+        def run():
+            if layers == 1:
+                ph = pf.MemEfficientSpGEMM(SR, dA, dB, phases=0, perProcessMemory=budget, on_phase=consume)
+            else:
+                ph = pf.Mult_AnXBn_SUMMA3D(SR, dA, dB, phases=0, perProcessMemory=budget, on_phase=consume)
+            return ph
+
+        def step():
+            acc.clear()
+            ph = run()
+            return {"flops": flops_total, "nnz": acc["nnz"], "phases": ph}
+
+        def verify():
+            acc.clear()
+            acc["sum"] = 0.0
+            run()
+            return acc["nnz"], acc["sum"]
 
     for _ in range(args.warmup):
-        st = cb.PhasedSpGEMM(SR, dA, dB)
+        st = step()
     ctx.synchronize()
     ctx.enable_timing(True)
     ctx.reset_kernel_stats()
@@ -158,7 +219,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        st = cb.PhasedSpGEMM(SR, dA, dB)
+        st = step()
     ctx.synchronize()
     torch.cuda.synchronize()
     barrier()
@@ -168,7 +229,7 @@ def main():
 
     my_s = (t1 - t0) / max(args.steps, 1)
     step_s = allreduce(my_s, dist.ReduceOp.MAX if world > 1 else None)
-    flops = allreduce(float(st["flops"]), dist.ReduceOp.SUM if world > 1 else None)
+    flops = float(st["flops"])  # the whole product's multiplies (every rank knows the total)
     nnzC = allreduce(float(st["nnz"]), dist.ReduceOp.SUM if world > 1 else None)
     value = 2.0 * flops / step_s / 1e9
 
@@ -188,14 +249,13 @@ def main():
 
     check = None
     if not args.no_verify:
-        sv = cb.PhasedSpGEMM(SR, dA, dB, checksum=True)
-        nnz_all = allreduce(float(sv["nnz"]), dist.ReduceOp.SUM if world > 1 else None)
-        vsum = allreduce(sv["value_sum"], dist.ReduceOp.SUM if world > 1 else None)
+        nz, vs = verify()
+        nnz_all = allreduce(float(nz), dist.ReduceOp.SUM if world > 1 else None)
+        vsum = allreduce(vs, dist.ReduceOp.SUM if world > 1 else None)
         known = {22: 24766243778, 20: 3284757756, 18: 425342972, 16: 53638834, 14: 6471508}.get(args.scale)
         check = {"nnzC": int(nnz_all), "value_sum": vsum, "expected_nnzC": known,
                  "ok": (known is None or int(nnz_all) == known)}
 
-    out = None
     if rank == 0:
         base = None
         if world == 1 and not args.no_cpu_baseline:
@@ -207,13 +267,12 @@ def main():
             "data": "synthetic: packed Graph500 R-MAT (seed 0xDECAFBAD), bit-identical to the reference generator",
             "config": {"workload": f"rmat{args.scale}_ef{args.edgefactor}_AxA_PlusTimes_f64", "scale": args.scale,
                        "edgefactor": args.edgefactor, "nnzA": nnzA, "flops": int(flops), "nnzC": int(nnzC),
-                       "phases": st["phases"], "parallelism": f"B column stripes x{world}" if world > 1 else "1 GPU",
+                       "phases": st["phases"], "parallelism": parallelism,
                        "kernel_ms": {n: round(v["ms"] / max(args.steps, 1), 3) for n, v in ks.items()}},
             "roofline": roofline, "cpu_baseline": base, "check": check,
         }
         print(json.dumps(out), flush=True)
     barrier()
-    del dA, dB
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

@@ -151,8 +151,8 @@ __global__ void densify_cp_kernel(const int64_t* __restrict__ jc, const int64_t*
 // (A's columns are row-sorted, so first/last entries bound them).
 __global__ __launch_bounds__(256) void flop_kernel(const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
                                                    const int64_t* __restrict__ Bcp, const int32_t* __restrict__ Bir,
-                                                   int64_t nzc, int64_t* __restrict__ flop, int32_t* __restrict__ rmin,
-                                                   int32_t* __restrict__ rmax) {
+                                                   int64_t nzc, int64_t ncolA, int64_t* __restrict__ flop,
+                                                   int32_t* __restrict__ rmin, int32_t* __restrict__ rmax, int* err) {
   const int lane = threadIdx.x & 63;
   const int64_t col = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (col >= nzc) return;
@@ -160,6 +160,10 @@ __global__ __launch_bounds__(256) void flop_kernel(const int64_t* __restrict__ A
   int32_t mn = INT32_MAX, mx = -1;
   for (int64_t p = Bcp[col] + lane; p < Bcp[col + 1]; p += 64) {
     const int32_t k = Bir[p];
+    if (k < 0 || k >= ncolA) {  // B row id outside A's columns: report, do not index
+      guard_fail(err, 11, col, k, ncolA);
+      continue;
+    }
     const int64_t s = Acp[k], e = Acp[k + 1];
     if (e > s) {
       f += e - s;
@@ -274,9 +278,13 @@ __global__ void widen_i32_kernel(const int32_t* __restrict__ f, int64_t* __restr
 }
 
 // merge: mark union of column ids
-__global__ void mark_cols_kernel(const int64_t* __restrict__ jc, int64_t nzc, int32_t* __restrict__ flag) {
+__global__ void mark_cols_kernel(const int64_t* __restrict__ jc, int64_t nzc, int64_t n, int32_t* __restrict__ flag,
+                                 int* err) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nzc) flag[jc[i]] = 1;
+  if (i >= nzc) return;
+  const int64_t c = jc[i];
+  if (c < 0 || c >= n) guard_fail(err, 10, i, c, n);
+  else flag[c] = 1;
 }
 __global__ void union_cols_kernel(const int32_t* __restrict__ flag, const int64_t* __restrict__ idx, int64_t n,
                                   int64_t* __restrict__ jcC) {
@@ -756,7 +764,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   hipLaunchKernelGGL(densify_cp_kernel, dim3(blocks_for(A->n + 1, 256)), dim3(256), 0, ctx->stream, A->jc, A->cp,
                      A->nzc, A->n, A->nnz, P.Adense);
   hipLaunchKernelGGL(flop_kernel, dim3(blocks_for(n, 4)), dim3(256), 0, ctx->stream, P.Adense, A->ir, B->cp, B->ir, n,
-                     P.flop, P.rmin, P.rmax);
+                     A->n, P.flop, P.rmin, P.rmax, ctx->d_err);
   CBH_HIP(ctx, hipGetLastError());
   CBH_TRY(sum_i64(ctx, S, P.flop, n, d_tot));
   hipLaunchKernelGGL(task_count_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, P.flop, P.rmin, P.rmax, n,
@@ -1346,13 +1354,14 @@ int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* p
     for (int l = 0; l < nlists; ++l)
       if (parts[l]->nzc)
         hipLaunchKernelGGL(mark_cols_kernel, dim3(blocks_for(parts[l]->nzc, 256)), dim3(256), 0, ctx->stream,
-                           parts[l]->jc, parts[l]->nzc, flag);
+                           parts[l]->jc, parts[l]->nzc, n, flag, ctx->d_err);
     // widen flags for the int64 scan
     hipLaunchKernelGGL(widen_i32_kernel, dim3(blocks_for(n + 1, 256)), dim3(256), 0, ctx->stream, flag, flag64, n + 1);
     CBH_TRY(exclusive_scan_i64(ctx, S, flag64, idx, n + 1));
     int64_t ncols = 0;
     CBH_HIP(ctx, hipMemcpyAsync(&ncols, idx + n, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
     CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    CBH_TRY(check_err(ctx));  // column ids outside [0, n): stop before they index anything
     if (ncols == 0) return empty_result(ctx, P0->m, n, dtype, C);
     int64_t *jcC, *seg_start, *seg_len, *work, *nnz, *Ccp;
     int32_t *rmin, *rmax, *cols;

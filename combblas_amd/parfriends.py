@@ -1,0 +1,285 @@
+"""Distributed SpGEMM drivers over RCCL (reference: include/CombBLAS/ParFriends.h).
+
+  Mult_AnXBn_Synch     ParFriends.h:1004-1108  2D SUMMA: per stage i, A's block (r,i) is broadcast
+                                               on the row world and B's block (i,c) on the column
+                                               world, multiplied locally, and the stage partials
+                                               are merged (MultiwayMerge).
+  MemEfficientSpGEMM   ParFriends.h:449-730    the same product with B's columns cut into phases so
+                                               that the partials of one phase fit the memory budget
+                                               (the prune/select/recover steps of HipMCL are not on
+                                               this path).
+  Mult_AnXBn_SUMMA3D   ParFriends.h:2917-3190  per-layer SUMMA, then the fiber reduce-scatter: the
+                                               layer partial is cut into nlayers column ranges
+                                               (divisions3d), exchanged with an alltoallv and the
+                                               received pieces merged.
+  PSpGEMM              SpParMat.h:454-467      dispatch on the operand type.
+
+MI355X design: every block is device-resident and every collective moves HBM tensors
+(torch.distributed "nccl" = RCCL over xGMI), the local multiply / merge / symbolic pass are the
+gfx950 kernels (backend.HipBackend). In the phased drivers all stage blocks are broadcast once
+up front and kept in HBM (a scale-22 R-MAT A is 0.8 GB; HBM is 288 GB), so the phase loop of
+the 2D driver runs without any communication and phases are planned from the exact per-column
+nnz of the partials (estimateNNZ_Hash), not from a sampled estimate.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ._lib import CombBLASHipError
+from .comm import allgather_i64, allreduce_, alltoallv, bcast
+from .commgrid import ProductGrid
+from .spparmat import SpParMat, SpParMat3D, block_range
+
+DIMMISMATCH = 3002
+
+
+# ---------------------------------------------------------------------------------- block utils
+def _empty(be, m, n, vdtype):
+    dev = be.device
+    return be.wrap(m, n, torch.zeros(1, dtype=torch.int64, device=dev), torch.zeros(0, dtype=torch.int64, device=dev),
+                   torch.zeros(0, dtype=torch.int32, device=dev), torch.zeros(0, dtype=vdtype, device=dev))
+
+
+def _colslice(be, blk, c0, c1):
+    """columns [c0, c1) of a block, same column space (ir/num are views, cp is rebased)"""
+    m, n, nnz, nzc = be.dims(blk)
+    if c0 <= 0 and c1 >= n:
+        return blk
+    cp, jc, ir, num = be.arrays(blk)
+    s, e = (int(x) for x in torch.searchsorted(jc, torch.tensor([c0, c1], dtype=torch.int64, device=jc.device)).cpu())
+    p0, p1 = (int(x) for x in cp[[s, e]].cpu()) if nzc else (0, 0)
+    return be.wrap(m, n, (cp[s:e + 1] - p0).contiguous(), jc[s:e], ir[p0:p1], num[p0:p1])
+
+
+def _concat_cols(be, blocks, m, n, vdtype):
+    """ColConcatenate of blocks over increasing, disjoint column ranges of one column space"""
+    blocks = [b for b in blocks if be.dims(b)[3] > 0]
+    if not blocks:
+        return _empty(be, m, n, vdtype)
+    if len(blocks) == 1:
+        return blocks[0]
+    arrs = [be.arrays(b) for b in blocks]
+    off, cps = 0, []
+    for i, (cp, jc, ir, num) in enumerate(arrs):
+        cps.append((cp[:-1] if i + 1 < len(arrs) else cp) + off)
+        off += ir.numel()
+    return be.wrap(m, n, torch.cat(cps), torch.cat([a[1] for a in arrs]), torch.cat([a[2] for a in arrs]),
+                   torch.cat([a[3] for a in arrs]))
+
+
+def _merge(be, SR, parts, m, n, vdtype):
+    parts = [p for p in parts if be.dims(p)[2] > 0]  # `if(!C_cont->isZero()) tomerge.push_back`
+    if not parts:
+        return _empty(be, m, n, vdtype)
+    if len(parts) == 1:
+        return parts[0]
+    return be.merge(SR, parts, m, n)
+
+
+def _essentials(be, blk, group):
+    """SpParHelper::GetSetSizes: (m, n, nnz, nzc) of every rank of the group"""
+    return allgather_i64(be.dims(blk), group, be.device).tolist()
+
+
+def _bcast_block(be, blk, ess, root, group, vdtype):
+    """SpParHelper::BCastMatrix: rank `root` of `group` sends its block's cp, jc, ir, num"""
+    m, n, nnz, nzc = ess[root]
+    if group.rank == root:
+        cp, jc, ir, num = be.arrays(blk)
+    else:
+        dev = be.device
+        cp = torch.empty(nzc + 1, dtype=torch.int64, device=dev)
+        jc = torch.empty(nzc, dtype=torch.int64, device=dev)
+        ir = torch.empty(nnz, dtype=torch.int32, device=dev)
+        num = torch.empty(nnz, dtype=vdtype, device=dev)
+    for t in (cp, jc, ir, num):
+        bcast(t, root, group)
+    return blk if group.rank == root else be.wrap(m, n, cp, jc, ir, num)
+
+
+def _check_dims(A, B):
+    if A.getncol() != B.getnrow():
+        raise CombBLASHipError(DIMMISMATCH, f"Can not multiply, dimensions does not match {A.getncol()} != {B.getnrow()}")
+    if A.seq is B.seq:
+        raise CombBLASHipError(3005, "A and B must not alias (ParFriends.h:172-179)")
+
+
+def _stage_blocks(A, B, grid, stages):
+    be = A.backend
+    vdtype = be.value_dtype(A.seq)
+    Aess = _essentials(be, A.seq, grid.rowWorld)
+    Bess = _essentials(be, B.seq, grid.colWorld)
+    Ab = [_bcast_block(be, A.seq, Aess, i, grid.rowWorld, vdtype) for i in range(stages)]
+    Bb = [_bcast_block(be, B.seq, Bess, i, grid.colWorld, vdtype) for i in range(stages)]
+    return Ab, Bb, vdtype
+
+
+def _phase_cuts(be, Ab, Bb, ncols, phases, budget_entries, group=None):
+    """Column ranges [c0, c1) of the local output block. With phases <= 0 they are planned from
+    the exact per-column nnz of the stage partials (summed over `group`, so that every rank of
+    a fiber cuts identically), each phase's partials staying within budget_entries."""
+    if phases and phases > 0:
+        return [block_range(ncols, phases, p) for p in range(phases)]
+    if group is not None:  # every rank of the fiber must cut identically
+        t = torch.tensor([budget_entries], dtype=torch.int64, device=be.device)
+        budget_entries = int(allreduce_(t, group, torch.distributed.ReduceOp.MIN).item())
+    col = torch.zeros(ncols + 1, dtype=torch.int64, device=be.device)
+    for a, b in zip(Ab, Bb):
+        if be.dims(b)[3]:
+            col.index_add_(0, be.arrays(b)[1], be.col_nnz(a, b))
+    if group is not None:
+        allreduce_(col, group)
+    cum = np.concatenate([[0], np.cumsum(col[:ncols].cpu().numpy())])
+    cuts, c0 = [], 0
+    while c0 < ncols:
+        c1 = int(np.searchsorted(cum, cum[c0] + budget_entries, side="right")) - 1
+        c1 = min(max(c1, c0 + 1), ncols)
+        cuts.append((c0, c1))
+        c0 = c1
+    return cuts or [(0, ncols)]
+
+
+def _budget_entries(be, vdtype, perProcessMemory, copies):
+    if perProcessMemory and perProcessMemory > 0:
+        budget = perProcessMemory
+    else:
+        free, _ = torch.cuda.mem_get_info(be.device) if be.device.type == "cuda" else (1 << 34, 0)
+        budget = int(free * 0.4)
+    esz = 4 + torch.empty(0, dtype=vdtype).element_size()
+    return max(1, budget // (esz * copies))
+
+
+# ---------------------------------------------------------------------------------- 2D
+def Mult_AnXBn_Synch(SR, A: SpParMat, B: SpParMat, clearA=False, clearB=False) -> SpParMat:
+    """C = A*B by 2D SUMMA (ParFriends.h:1004-1108); received blocks are dropped after their stage."""
+    _check_dims(A, B)
+    grid, stages = ProductGrid(A.commGrid, B.commGrid)
+    be = A.backend
+    vdtype = be.value_dtype(A.seq)
+    Aess = _essentials(be, A.seq, grid.rowWorld)
+    Bess = _essentials(be, B.seq, grid.colWorld)
+    Aself, Bself = grid.GetRankInProcRow(), grid.GetRankInProcCol()
+    m, n = be.dims(A.seq)[0], be.dims(B.seq)[1]
+    tomerge = []
+    for i in range(stages):
+        Ai = _bcast_block(be, A.seq, Aess, i, grid.rowWorld, vdtype)
+        Bi = _bcast_block(be, B.seq, Bess, i, grid.colWorld, vdtype)
+        tomerge.append(be.multiply(SR, Ai, Bi))
+        if i != Aself:
+            be.free(Ai)
+        if i != Bself:
+            be.free(Bi)
+    C = _merge(be, SR, tomerge, m, n, vdtype)
+    if clearA:
+        be.free(A.seq)
+    if clearB:
+        be.free(B.seq)
+    return SpParMat(C, grid, be, A.m, B.n, A.row_off, B.col_off)
+
+
+def MemEfficientSpGEMM(SR, A: SpParMat, B: SpParMat, phases=0, perProcessMemory=0, on_phase=None):
+    """Phased 2D SUMMA (ParFriends.h:449-730 without the MCL prune). phases=0 plans the phases
+    from the exact symbolic pass and `perProcessMemory` bytes (default 40 % of free HBM).
+    on_phase(C_block, c0, c1) consumes each phase's block of C (local columns [c0, c1)); without
+    it the phases are concatenated and the SpParMat C is returned."""
+    _check_dims(A, B)
+    grid, stages = ProductGrid(A.commGrid, B.commGrid)
+    be = A.backend
+    Ab, Bb, vdtype = _stage_blocks(A, B, grid, stages)
+    m, n = be.dims(A.seq)[0], be.dims(B.seq)[1]
+    cuts = _phase_cuts(be, Ab, Bb, n, phases, _budget_entries(be, vdtype, perProcessMemory, 2))
+    out = []
+    for c0, c1 in cuts:
+        parts = [be.multiply(SR, a, _colslice(be, b, c0, c1)) for a, b in zip(Ab, Bb)]
+        C = _merge(be, SR, parts, m, n, vdtype)
+        if on_phase is not None:
+            on_phase(C, c0, c1)
+        else:
+            out.append(C)
+    if on_phase is not None:
+        return len(cuts)
+    return SpParMat(_concat_cols(be, out, m, n, vdtype), grid, be, A.m, B.n, A.row_off, B.col_off)
+
+
+# ---------------------------------------------------------------------------------- 3D
+def _divisions3d(ncols, nlayers):
+    """SpParMat3D::CalculateColSplitDistributionOfLayer (non-special), SpParMat3D.cpp:592-605"""
+    y = ncols // nlayers
+    return [y] * (nlayers - 1) + [ncols - (nlayers - 1) * y]
+
+
+def _fiber_reduce_scatter(be, SR, P, grid3, m, ncols, vdtype):
+    """ParFriends.h:3097-3183: column chunk j of the layer partial P goes to fiber rank j; the
+    received pieces of this rank's chunk are merged. Returns (block, chunk start)."""
+    L, me = grid3.gridLayers, grid3.rankInFiber
+    fib = grid3.fiberWorld
+    div = _divisions3d(ncols, L)
+    starts = np.concatenate([[0], np.cumsum(div)]).astype(np.int64)
+    cp, jc, ir, num = be.arrays(P)
+    dev = be.device
+    bounds = torch.searchsorted(jc, torch.tensor(starts, dtype=torch.int64, device=dev))
+    cpb = cp[bounds]
+    slot_b, ent_b = bounds.cpu().tolist(), cpb.cpu().tolist()
+    s_nzc = [slot_b[j + 1] - slot_b[j] for j in range(L)]
+    s_nnz = [ent_b[j + 1] - ent_b[j] for j in range(L)]
+    lo = ent_b[0]
+    prof = torch.tensor([v for j in range(L) for v in (s_nzc[j], s_nnz[j])], dtype=torch.int64, device=dev)
+    rprof = alltoallv(prof, [2] * L, [2] * L, fib).cpu().tolist()
+    r_nzc, r_nnz = rprof[0::2], rprof[1::2]
+    s0, s1 = slot_b[0], slot_b[L]
+    collen = (cp[s0 + 1:s1 + 1] - cp[s0:s1]).contiguous()
+    rjc = alltoallv(jc[s0:s1], s_nzc, r_nzc, fib)
+    rlen = alltoallv(collen, s_nzc, r_nzc, fib)
+    rir = alltoallv(ir[lo:ent_b[L]], s_nnz, r_nnz, fib)
+    rnum = alltoallv(num[lo:ent_b[L]], s_nnz, r_nnz, fib)
+    c0, w = int(starts[me]), int(div[me])
+    pieces, a, b = [], 0, 0
+    for j in range(L):
+        if r_nzc[j]:
+            cpj = torch.zeros(r_nzc[j] + 1, dtype=torch.int64, device=dev)
+            torch.cumsum(rlen[a:a + r_nzc[j]], 0, out=cpj[1:])
+            pieces.append(be.wrap(m, w, cpj, rjc[a:a + r_nzc[j]] - c0, rir[b:b + r_nnz[j]], rnum[b:b + r_nnz[j]]))
+        a += r_nzc[j]
+        b += r_nnz[j]
+    return _merge(be, SR, pieces, m, w, vdtype), c0
+
+
+def Mult_AnXBn_SUMMA3D(SR, A: SpParMat3D, B: SpParMat3D, phases=1, perProcessMemory=0, on_phase=None):
+    """C = A*B on a 3D grid (A column-split, B row-split). Returns the column-split SpParMat3D C,
+    or, with on_phase, feeds every phase's piece of this rank's C chunk to on_phase(C, c0, c1)
+    (local columns of the chunk) and returns the number of phases. phases=0 plans them from the
+    exact symbolic pass (the reference's MemEfficientSpGEMM3D phase loop, ParFriends.h:3200-3520)."""
+    _check_dims(A, B)
+    if not A.colsplit or B.colsplit:
+        raise CombBLASHipError(DIMMISMATCH, "Mult_AnXBn_SUMMA3D needs a column-split A and a row-split B")
+    g3 = A.commGrid3D
+    grid, stages = ProductGrid(g3.commGridLayer, B.commGrid3D.commGridLayer)
+    be = A.backend
+    Ab, Bb, vdtype = _stage_blocks(A, B, grid, stages)
+    m, n = be.dims(A.seq)[0], be.dims(B.seq)[1]
+    cuts = _phase_cuts(be, Ab, Bb, n, phases, _budget_entries(be, vdtype, perProcessMemory, 3), group=g3.fiberWorld)
+    div = _divisions3d(n, g3.gridLayers)
+    out, mine0 = [], 0
+    for c0, c1 in cuts:
+        parts = [be.multiply(SR, a, _colslice(be, b, c0, c1)) for a, b in zip(Ab, Bb)]
+        P = _merge(be, SR, parts, m, n, vdtype)
+        C, mine0 = _fiber_reduce_scatter(be, SR, P, g3, m, n, vdtype)
+        w = div[g3.rankInFiber]
+        p0, p1 = min(max(c0 - mine0, 0), w), min(max(c1 - mine0, 0), w)
+        if on_phase is not None:
+            on_phase(C, p0, p1)
+        else:
+            out.append(C)
+    if on_phase is not None:
+        return len(cuts)
+    w = div[g3.rankInFiber]
+    Cb = _concat_cols(be, out, m, w, vdtype)
+    return SpParMat3D(Cb, g3, be, A.m, B.n, True, A.row_off, B.col_off + mine0)
+
+
+def PSpGEMM(SR, A, B, **kw):
+    """SpParMat.h:454-467 -- the product of two distributed matrices on their grid."""
+    if isinstance(A, SpParMat3D):
+        return Mult_AnXBn_SUMMA3D(SR, A, B, **kw)
+    return Mult_AnXBn_Synch(SR, A, B, **kw)

@@ -69,10 +69,18 @@ class Context:
         self.device = device
         self._live = {}
         self._alloc_cb = self._free_cb = None
+        self.tdevice = None
         if torch_allocator or stream is not None:
             torch = _torch()
             self.tdevice = torch.device("cuda", device)
-            s = stream if stream is not None else torch.cuda.current_stream(self.tdevice)
+            s = stream
+            if s is None or s.cuda_stream == 0:
+                # torch's default stream is the legacy NULL stream, which the C-ABI cannot name
+                # (NULL = "own stream"): give library and torch one explicit stream instead, and
+                # make it this thread's current stream so torch ops on library outputs (and the
+                # collectives that sync with the current stream) are ordered with the kernels.
+                s = torch.cuda.Stream(self.tdevice)
+                torch.cuda.set_stream(s)
             self.tstream = s
             check(L.cbh_ctx_set_stream(self.h, ctypes.c_void_p(s.cuda_stream)), self.h)
         if torch_allocator:

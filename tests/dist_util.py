@@ -1,0 +1,156 @@
+"""Multi-process harness for the distributed drivers (test infrastructure only).
+
+`OracleBackend` supplies the local-block operations of combblas_amd.backend.HipBackend from the
+CPU oracle, on host torch tensors, so that the grid logic of parfriends.py (stage broadcasts,
+phase planning, 3D reduce-scatter, merges) runs under `gloo` in CPU processes. The product path
+never uses it: HipBackend has no CPU fallback.
+
+`run_world(fn, world, *args)` spawns `world` processes with a gloo process group on 127.0.0.1
+and returns what rank 0's fn returned.
+"""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+import tempfile
+import traceback
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(HERE))
+
+import helpers as H  # noqa: E402
+
+ORACLE_SR = {"PlusTimesSRing": "plus_times", "SelectMaxSRing": "select_max", "MinPlusSRing": "min_plus",
+             "OrAndSRing": "or_and"}
+T_OF_NP = {np.dtype(np.float64): torch.float64, np.dtype(np.int64): torch.int64, np.dtype(np.uint8): torch.uint8,
+           np.dtype(np.int32): torch.int32, np.dtype(np.float32): torch.float32}
+
+
+class OBlock:
+    def __init__(self, m, n, cp, jc, ir, num):
+        self.m, self.n = int(m), int(n)
+        self.cp, self.jc, self.ir, self.num = cp, jc, ir, num
+
+    def dcsc(self):
+        return H.Dcsc(self.m, self.n, self.jc.numpy(), self.cp.numpy(), self.ir.numpy(), self.num.numpy())
+
+
+class OracleBackend:
+    device = torch.device("cpu")
+
+    def __init__(self):
+        self.o = H.Oracle()
+
+    @staticmethod
+    def _from_dcsc(d):
+        num = np.ascontiguousarray(d.num.astype(np.uint8) if d.num.dtype == np.bool_ else d.num)
+        return OBlock(d.m, d.n, torch.from_numpy(np.ascontiguousarray(d.cp, np.int64)),
+                      torch.from_numpy(np.ascontiguousarray(d.jc, np.int64)),
+                      torch.from_numpy(np.ascontiguousarray(d.ir, np.int32)), torch.from_numpy(num))
+
+    def from_host(self, h):
+        return self._from_dcsc(h)
+
+    @staticmethod
+    def wrap(m, n, cp, jc, ir, num):
+        return OBlock(m, n, cp.contiguous(), jc.contiguous(), ir.contiguous(), num.contiguous())
+
+    @staticmethod
+    def dims(b):
+        return b.m, b.n, int(b.ir.numel()), int(b.jc.numel())
+
+    @staticmethod
+    def arrays(b):
+        return b.cp, b.jc, b.ir, b.num
+
+    @staticmethod
+    def value_dtype(b):
+        return b.num.dtype
+
+    @staticmethod
+    def to_host(b):
+        import combblas_amd as cb
+        return cb.HostDcsc(b.m, b.n, b.jc.numpy(), b.cp.numpy(), b.ir.numpy(), b.num.numpy())
+
+    @staticmethod
+    def free(b):
+        pass
+
+    def multiply(self, SR, A, B):
+        if A.ir.numel() == 0 or B.ir.numel() == 0:
+            return OBlock(A.m, B.n, torch.zeros(1, dtype=torch.int64), torch.zeros(0, dtype=torch.int64),
+                          torch.zeros(0, dtype=torch.int32), torch.zeros(0, dtype=A.num.dtype))
+        return self._from_dcsc(self.o.spgemm(A.dcsc(), B.dcsc(), ORACLE_SR[SR.name], "hybrid"))
+
+    def merge(self, SR, blocks, m, n):
+        return self._from_dcsc(self.o.merge([b.dcsc() for b in blocks], ORACLE_SR[SR.name]))
+
+    def col_nnz(self, A, B):
+        if A.ir.numel() == 0 or B.ir.numel() == 0:
+            return torch.zeros(B.jc.numel(), dtype=torch.int64)
+        return torch.from_numpy(self.o.symbolic(A.dcsc(), B.dcsc())[3])
+
+    def synchronize(self):
+        pass
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn, args, outdir):
+    import pickle
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    res = None
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        res = ("ok", fn(rank, world, *args))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException:  # noqa: BLE001
+        res = ("err", traceback.format_exc())
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump(res, f)
+
+
+def run_world(fn, world, *args, timeout=240):
+    """Runs fn(rank, world, *args) on `world` gloo processes; returns rank 0's result."""
+    import pickle
+
+    import torch.multiprocessing as mp
+
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        port = _free_port()
+        procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, d)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout)
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                raise TimeoutError("distributed test timed out")
+        results = []
+        for r in range(world):
+            path = os.path.join(d, f"r{r}.pkl")
+            if not os.path.exists(path):
+                raise RuntimeError(f"rank {r} died (exit {procs[r].exitcode})")
+            with open(path, "rb") as f:
+                results.append(pickle.load(f))
+        for r, (st, v) in enumerate(results):
+            if st != "ok":
+                raise AssertionError(f"rank {r} failed:\n{v}")
+        return results[0][1]
