@@ -241,9 +241,13 @@ def main():
                 "avg_launch_ms": round(k["ms"] / max(k["launches"], 1), 4),
                 "alg_bytes_per_launch": round(k["alg_bytes"] / max(k["launches"], 1))}
     pmc = os.path.join(HERE, "profiles", "pmc_num_large.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc):  # PMC passes of the same kernel (tools/pmc_traffic.py); stale files are ignored
         try:
-            roofline["traffic"] = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            p = json.load(open(pmc))
+            if p.get("kernel") == DOMINANT_KERNEL:
+                roofline["traffic"] = p.get("hbm_bytes_per_launch")
+                roofline["traffic_note"] = (f"HBM bytes per launch from rocprofv3 PMC (2xFETCH_SIZE+WRITE_SIZE, gfx950 "
+                                            f"correction; raw {p.get('hbm_bytes_per_launch_raw')}), {p.get('source')}")
         except Exception:  # noqa: BLE001
             pass
 
