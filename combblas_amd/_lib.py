@@ -9,8 +9,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# CBH_LIB=stamps selects the diagnostic build (combblas_amd/build.py --stamps); default is the product
-LIB_PATH = os.path.join(_HERE, "libcombblas_hip_stamps.so" if os.environ.get("CBH_LIB") == "stamps"
+# CBH_LIB=<variant> selects a diagnostic build libcombblas_hip_<variant>.so (combblas_amd/build.py
+# --stamps / --variant); default is the product
+LIB_PATH = os.path.join(_HERE, f"libcombblas_hip_{os.environ['CBH_LIB']}.so" if os.environ.get("CBH_LIB")
                         else "libcombblas_hip.so")
 
 c_int64_p = ctypes.POINTER(ctypes.c_int64)

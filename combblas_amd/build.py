@@ -25,15 +25,20 @@ def _stale(lib: str = LIB) -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, stamps: bool = False, variant: str = "",
+          defines: tuple = ()) -> str:
     """stamps=True builds the diagnostic variant libcombblas_hip_stamps.so (-DCBH_STAMPS: per-phase
-    s_memtime cycle counts, printed with CBH_DIAG=1; load it with CBH_LIB=stamps). Never the product."""
-    lib = LIB.replace(".so", "_stamps.so") if stamps else LIB
+    s_memtime cycle counts, printed with CBH_DIAG=1; load it with CBH_LIB=stamps). variant/defines
+    build other diagnostic variants (e.g. variant="abl1", defines=("CBH_ABL=1",): kernel-phase
+    ablations) as libcombblas_hip_<variant>.so, loaded with CBH_LIB=<variant>. Never the product."""
+    if stamps:
+        variant, defines = "stamps", tuple(defines) + ("CBH_STAMPS",)
+    lib = LIB.replace(".so", f"_{variant}.so") if variant else LIB
     if not force and not _stale(lib):
         return lib
     cmd = [HIPCC, "-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17", "-Wall",
            "-Wno-unused-function", "-Wl,-soname," + os.path.basename(lib), "-o", lib + ".tmp"] + \
-        (["-DCBH_STAMPS"] if stamps else []) + [os.path.join(CSRC, s) for s in SOURCES] + ["-lpthread"]
+        [f"-D{d}" for d in defines] + [os.path.join(CSRC, s) for s in SOURCES] + ["-lpthread"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd, cwd=CSRC)
@@ -44,4 +49,9 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
 if __name__ == "__main__":
     import sys
 
-    print(build(force=True, verbose=True, stamps="--stamps" in sys.argv))
+    args = sys.argv[1:]
+    if "--variant" in args:  # --variant NAME DEF [DEF ...]
+        k = args.index("--variant")
+        print(build(force=True, verbose=True, variant=args[k + 1], defines=tuple(args[k + 2:])))
+    else:
+        print(build(force=True, verbose=True, stamps="--stamps" in args))

@@ -569,26 +569,33 @@ static int64_t task_flops() {
   return v;
 }
 
+// Row blocks: C's rows are cut into blocks of RB rows (kRowBlocks blocks); interior task
+// boundaries of a split column sit on block boundaries, where the row-block table of A gives
+// every entry's position directly (ablk_kernel).
+constexpr int64_t kRowBlocks = 128;
+
 __global__ void task_count_kernel(const int64_t* __restrict__ flop, const int32_t* __restrict__ rmin,
-                                  const int32_t* __restrict__ rmax, int64_t n, int64_t ft, int64_t* __restrict__ S) {
+                                  const int32_t* __restrict__ rmax, int64_t n, int64_t ft, int32_t RB,
+                                  int64_t* __restrict__ S) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t f = flop[i];
   int64_t s = 0;
   if (f > 0) {
-    const int64_t span = (int64_t)rmax[i] - rmin[i] + 1;
+    const int64_t nb = (int64_t)(rmax[i] / RB) - rmin[i] / RB + 1;  // row blocks the column touches
     s = (f + ft - 1) / ft;
-    if (s > span) s = span;
+    if (s > nb) s = nb;
     if (s < 1) s = 1;
   }
   S[i] = s;
 }
 
-// one wave per column: balanced split lo_s = rmin + span*s/S; per-task work and roofline units
-// split so that they sum exactly to the column's totals
+// one wave per column: task s takes row blocks [b0 + nb*s/S, b0 + nb*(s+1)/S) (clipped to
+// [rmin, rmax] at the column's ends); per-task work and roofline units are split in proportion
+// to the blocks so that they sum exactly to the column's totals
 __global__ __launch_bounds__(256) void task_fill_kernel(const int64_t* __restrict__ tstart, const int64_t* __restrict__ flop,
                                                         const int32_t* __restrict__ rmin, const int32_t* __restrict__ rmax,
-                                                        const int64_t* __restrict__ Bcp, int64_t n,
+                                                        const int64_t* __restrict__ Bcp, int64_t n, int32_t RB,
                                                         int32_t* __restrict__ tcol, int32_t* __restrict__ tlo,
                                                         int32_t* __restrict__ thi, uint8_t* __restrict__ tfull,
                                                         int64_t* __restrict__ twork, int64_t* __restrict__ tunits) {
@@ -597,16 +604,36 @@ __global__ __launch_bounds__(256) void task_fill_kernel(const int64_t* __restric
   if (c >= n) return;
   const int64_t t0 = tstart[c], S = tstart[c + 1] - t0;
   if (S <= 0) return;
-  const int64_t span = (int64_t)rmax[c] - rmin[c] + 1, f = flop[c], b = Bcp[c + 1] - Bcp[c];
+  const int64_t f = flop[c], b = Bcp[c + 1] - Bcp[c];
+  const int64_t b0 = rmin[c] / RB, nb = (int64_t)(rmax[c] / RB) - b0 + 1;
   for (int64_t s = lane; s < S; s += 64) {
     const int64_t t = t0 + s;
+    const int64_t c0 = nb * s / S, c1 = nb * (s + 1) / S;
     tcol[t] = (int32_t)c;
-    tlo[t] = (int32_t)(rmin[c] + span * s / S);
-    thi[t] = (int32_t)(rmin[c] + span * (s + 1) / S);
+    tlo[t] = s == 0 ? rmin[c] : (int32_t)((b0 + c0) * RB);
+    thi[t] = s == S - 1 ? rmax[c] + 1 : (int32_t)((b0 + c1) * RB);
     tfull[t] = (uint8_t)((s == 0 ? 1 : 0) | (s == S - 1 ? 2 : 0));
-    twork[t] = f * (s + 1) / S - f * s / S;
-    tunits[t] = (b + f) * (s + 1) / S - (b + f) * s / S;
+    twork[t] = f * c1 / nb - f * c0 / nb;
+    tunits[t] = (b + f) * c1 / nb - (b + f) * c0 / nb;
   }
+}
+
+// Row-block table of A (wave per column of the dense pointers): out[k*(nblk+1) + x] = first
+// position of A(:,k), relative to its start, whose row is >= x*RB, for x = 0..nblk.
+__global__ __launch_bounds__(256) void ablk_kernel(const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
+                                                   int64_t ncol, int32_t RB, int64_t nblk, int32_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= ncol) return;
+  const int64_t base = Acp[k], len = Acp[k + 1] - base;
+  int32_t* o = out + k * (nblk + 1);
+  for (int64_t p = lane; p < len; p += 64) {
+    const int64_t bc = Air[base + p] / RB;
+    const int64_t bp = p > 0 ? Air[base + p - 1] / RB : -1;
+    for (int64_t x = bp + 1; x <= bc; ++x) o[x] = (int32_t)p;
+  }
+  const int64_t blast = len > 0 ? Air[base + len - 1] / RB : -1;
+  for (int64_t x = blast + 1 + lane; x <= nblk; x += 64) o[x] = (int32_t)len;
 }
 
 __global__ void gather_i64_kernel(const int64_t* __restrict__ src, const int64_t* __restrict__ idx, int64_t n,
@@ -629,7 +656,8 @@ struct TSymSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 struct TSymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512, U = 4; };
 struct TNumSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 struct TNumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512, U = 4; };
-
+// (measured at scale 22: a 1024-thread workgroup with an 8192-slot table, half the sub-tiles,
+// ran 28 % slower than two 512-thread workgroups per CU with 4096 slots)
 template <class SR, class CFG, int MODE>
 static int launch_task(cbh_ctx* ctx, const TaskArgs& args, int64_t first, int64_t count, int kind = -1,
                        double bytes = 0) {
@@ -722,6 +750,10 @@ struct Plan {  // device arrays describing C = A*B (B's nonzero column slots, ta
   int32_t* order = nullptr;   // ntasks: launch order
   int64_t* nnz = nullptr;     // nzcB + 1
   int64_t* Ccp = nullptr;     // nzcB + 1
+  int32_t* Ablk = nullptr;    // A's row-block table (A.n x ablk_w), built when a column is split
+  int64_t ablk_w = 0;
+  int32_t RB = 1;
+  void* Apk = nullptr;        // numeric: A as PkRec records (built by the first numeric call)
   int64_t total_flops = 0, total_nnz = 0;
 };
 
@@ -735,6 +767,9 @@ static TaskArgs task_args(const cbh_mat* A, const cbh_mat* B, const Plan& P, cbh
   a.Bir = B->ir;
   a.Bnum = B->num;
   a.order = P.order;
+  a.Ablk = P.Ablk;
+  a.ablk_w = P.ablk_w;
+  a.RB = P.Ablk ? P.RB : 0;
   a.tcol = P.tcol;
   a.tlo = P.tlo;
   a.thi = P.thi;
@@ -767,8 +802,9 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
                      A->n, P.flop, P.rmin, P.rmax, ctx->d_err);
   CBH_HIP(ctx, hipGetLastError());
   CBH_TRY(sum_i64(ctx, S, P.flop, n, d_tot));
+  P.RB = (int32_t)std::max<int64_t>(1, (A->m + kRowBlocks - 1) / kRowBlocks);
   hipLaunchKernelGGL(task_count_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, P.flop, P.rmin, P.rmax, n,
-                     task_flops(), scnt);
+                     task_flops(), P.RB, scnt);
   CBH_HIP(ctx, hipMemsetAsync(scnt + n, 0, sizeof(int64_t), ctx->stream));
   CBH_TRY(exclusive_scan_i64(ctx, S, scnt, P.tstart, n + 1));
   int64_t h[2];
@@ -789,8 +825,16 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   CBH_TRY(S.get(&P.toff, nt + 1));
   CBH_TRY(S.get(&P.order, nt));
   hipLaunchKernelGGL(task_fill_kernel, dim3(blocks_for(n, 4)), dim3(256), 0, ctx->stream, P.tstart, P.flop, P.rmin,
-                     P.rmax, B->cp, n, P.tcol, P.tlo, P.thi, P.tfull, P.twork, P.tunits);
+                     P.rmax, B->cp, n, P.RB, P.tcol, P.tlo, P.thi, P.tfull, P.twork, P.tunits);
   CBH_HIP(ctx, hipGetLastError());
+  if (P.ntasks > n) {  // some column is split: row-block table of A for the aligned task boundaries
+    const int64_t nblk = (A->m + P.RB - 1) / P.RB;
+    P.ablk_w = nblk + 1;
+    CBH_TRY(S.get(&P.Ablk, (size_t)std::max<int64_t>(A->n, 1) * (size_t)P.ablk_w));
+    hipLaunchKernelGGL(ablk_kernel, dim3(blocks_for(A->n, 4)), dim3(256), 0, ctx->stream, P.Adense, A->ir, A->n, P.RB,
+                       nblk, P.Ablk);
+    CBH_HIP(ctx, hipGetLastError());
+  }
   CBH_HIP(ctx, hipMemsetAsync(P.tcnt, 0, sizeof(int64_t) * (nt + 1), ctx->stream));
   BinLists bl;
   CBH_TRY(make_bins(ctx, S, P.twork, P.ntasks, 0, P.order, &bl, BinCaps{kSmallCap, kSmallCap}, P.tunits));
@@ -826,11 +870,21 @@ template <class SR>
 static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat* B, Plan& P, int64_t t0, int64_t t1,
                        int64_t cbase, int32_t* Cir, void* Cnum, int64_t* launches, int64_t ccap) {
   if (t1 <= t0) return CBH_OK;
+  using VT = typename SR::val_t;
+  if (kPackedA && !P.Apk) {  // row + value records of A, shared by every phase of this product
+    PkRec<VT>* pk;
+    CBH_TRY(S.get(&pk, (size_t)std::max<int64_t>(A->nnz, 1)));
+    hipLaunchKernelGGL(pack_rec_kernel<VT>, dim3(blocks_for(A->nnz, 256)), dim3(256), 0, ctx->stream, A->ir,
+                       reinterpret_cast<const VT*>(A->num), A->nnz, pk);
+    CBH_HIP(ctx, hipGetLastError());
+    P.Apk = pk;
+  }
   BinLists bl;
   CBH_TRY(make_bins(ctx, S, P.tcnt + t0, t1 - t0, t0, P.order, &bl, BinCaps{kSmallCap, kSmallCap}, P.tunits + t0));
   TaskArgs a = task_args(A, B, P, ctx);
   a.twork = P.tcnt;
   a.toff = P.toff;
+  a.Apk = P.Apk;
   a.cbase = cbase;
   a.Cir = Cir;
   a.Cnum = Cnum;

@@ -29,6 +29,12 @@
 #pragma once
 #include "tile_kernel.h"
 
+// CBH_ABL (diagnostic builds only, combblas_amd/build.py --variant): bit 0 skips the numeric
+// commit loop, bit 1 the numeric table updates. Results are wrong; only kernel times matter.
+#ifndef CBH_ABL
+#define CBH_ABL 0
+#endif
+
 namespace cbh {
 
 enum : int { MODE_TSYM = 0, MODE_TNUM = 1 };
@@ -56,11 +62,15 @@ struct TaskArgs {
   const int64_t* Acp;  // A dense column pointers (A.n + 1)
   const int32_t* Air;
   const void* Anum;
+  const void* Apk;     // numeric: A as PkRec<val_t> records (row + value interleaved)
   const int64_t* Bcp;  // B DCSC column pointers (per nonzero column slot)
   const int32_t* Bir;
   const void* Bnum;
   const int32_t* order;  // task ids in launch order
   int64_t norder;
+  const int32_t* Ablk;   // row-block table of A: Ablk[k*ablk_w + b] = first position of A(:,k), relative
+  int64_t ablk_w;        // to its start, with row >= b*RB (b = 0..nblk); RB = 0: no table
+  int32_t RB;
   const int32_t* tcol;   // per task: column slot j
   const int32_t* tlo;    // per task: row range [lo, hi)
   const int32_t* thi;
@@ -76,26 +86,73 @@ struct TaskArgs {
   int64_t nnzA, ncolA, ntasks;
 };
 
-// first q in [lo, hi) with rows[q] >= key (rows sorted); global memory, 64-bit positions
+// Numeric gather layout: A's row id and value interleaved in one record, so that a product (and
+// the row reads of the cursor searches next to it) touches ONE cache line instead of one line of
+// ir and one of num. At scale 22 most per-sub-tile segments hold 1-3 products, so the split
+// layout fetched two partly used lines per product (PMC: 1.2 TB read per numeric launch for
+// 0.5 TB of algorithmic bytes). 16 B records for 8-byte values, 8 B otherwise.
+// Measured at scale 22 (round 1): 4 % slower than the split arrays while the cursor gallops read
+// rows (16-byte stride -> 4x the lines of ir); kept behind this switch for the speculative-segment
+// variant, which reads rows only next to the products.
+constexpr bool kPackedA = false;
+template <class V>
+struct PkRec {
+  int32_t r;
+  V v;
+};
+typedef int32_t v4i __attribute__((ext_vector_type(4)));
+typedef int32_t v2i __attribute__((ext_vector_type(2)));
+template <class V>
+__device__ __forceinline__ void ld_rec(const PkRec<V>* __restrict__ p, int32_t& r, V& v) {
+  static_assert(sizeof(PkRec<V>) == 16 || sizeof(PkRec<V>) == 8, "record size");
+  if constexpr (sizeof(PkRec<V>) == 16) {
+    const v4i x = *reinterpret_cast<const v4i*>(p);
+    r = x[0];
+    const uint64_t bits = (uint64_t)(uint32_t)x[2] | ((uint64_t)(uint32_t)x[3] << 32);
+    __builtin_memcpy(&v, &bits, sizeof(V));
+  } else {
+    const v2i x = *reinterpret_cast<const v2i*>(p);
+    r = x[0];
+    const uint32_t bits = (uint32_t)x[1];
+    __builtin_memcpy(&v, &bits, sizeof(V));  // little endian: the low bytes hold a 1- or 4-byte value
+  }
+}
+template <class V>
+__global__ void pack_rec_kernel(const int32_t* __restrict__ ir, const V* __restrict__ num, int64_t nnz,
+                                PkRec<V>* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nnz) return;
+  PkRec<V> x{};
+  x.r = ir[i];
+  x.v = num[i];
+  out[i] = x;
+}
+
+// first q in [lo, hi) with rows[q*S] >= key (rows sorted; S = stride in dwords: 1 for ir, the
+// record size for packed records); global memory, 64-bit positions. Plain binary search: an 8-ary
+// form (7 independent probes per level) measured slower at scale 22 -- the extra cache lines it
+// touches cost more than the latency it hides.
+template <int S>
 __device__ __forceinline__ int64_t lb_rows64(const int32_t* __restrict__ rows, int64_t lo, int64_t hi, int32_t key) {
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    if (rows[mid] < key) lo = mid + 1;
+    if (rows[mid * S] < key) lo = mid + 1;
     else hi = mid;
   }
   return lo;
 }
-// galloping lower bound from lo (rows[lo-1] < key is known): lo, lo+1, lo+3, lo+7, ...
+// galloping lower bound from lo (rows[(lo-1)*S] < key is known): lo, lo+1, lo+3, lo+7, ...
+template <int S>
 __device__ __forceinline__ int64_t gallop64(const int32_t* __restrict__ rows, int64_t lo, int64_t hi, int32_t key) {
   int64_t step = 1, prev = lo;
   int64_t nx = lo;
   while (nx < hi) {
-    if (rows[nx] >= key) return lb_rows64(rows, prev, nx, key);
+    if (rows[nx * S] >= key) return lb_rows64<S>(rows, prev, nx, key);
     prev = nx + 1;
     nx = lo + step;
     step <<= 1;
   }
-  return lb_rows64(rows, prev, hi, key);
+  return lb_rows64<S>(rows, prev, hi, key);
 }
 
 template <class SR, int T, int BS, int EMAX, int U, int MODE>
@@ -146,6 +203,12 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
   __shared__ int32_t s_ovf;  // overflow flag of the current sub-tile (LDS; read after barriers)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // row ids of A: the packed records in numeric mode (stride RS dwords), ir in symbolic mode
+  using Rec = PkRec<val_t>;
+  constexpr bool PK = NUM && kPackedA;
+  constexpr int RS = PK ? (int)(sizeof(Rec) / 4) : 1;
+  const int32_t* __restrict__ rowsA = PK ? reinterpret_cast<const int32_t*>(a.Apk) : a.Air;
+  const Rec* __restrict__ recA = reinterpret_cast<const Rec*>(a.Apk);
 #ifdef CBH_STAMPS
   uint64_t st_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t t_prev_ = __builtin_amdgcn_s_memtime();
@@ -207,10 +270,34 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         }
       }
       if constexpr (NUM) escale[i] = reinterpret_cast<const val_t*>(a.Bnum)[p];
-      const int64_t pos = (lo_is_start || base == end) ? base : lb_rows64(a.Air, base, end, lo);
+      // the entry is clamped to the task's rows: its end is the first row >= thi. Interior task
+      // boundaries sit on row-block boundaries, so both ends come from the block table (one
+      // load each) instead of a binary search over the A column.
+      const int32_t* blk = (a.RB > 0 && base < end) ? a.Ablk + (int64_t)k * a.ablk_w : nullptr;
+      int64_t cend = end;
+      if (!(full & 2) && base < end) {
+        if (blk && thi % a.RB == 0) cend = base + blk[thi / a.RB];
+        else cend = lb_rows64<RS>(rowsA, base, end, thi);
+      }
+      int64_t pos = base;
+      if (!lo_is_start && base < cend) {
+        if (blk) {
+          const int32_t b = lo / a.RB;
+          const int64_t s0 = base + blk[b];
+          if (lo % a.RB == 0) {
+            pos = s0;
+          } else {
+            const int64_t s1 = base + blk[b + 1];
+            pos = lb_rows64<RS>(rowsA, s0, s1 < cend ? s1 : cend, lo);
+          }
+          if (pos > cend) pos = cend;
+        } else {
+          pos = lb_rows64<RS>(rowsA, base, cend, lo);
+        }
+      }
       epos[i] = pos;
-      eend[i] = end;
-      enext[i] = pos < end ? a.Air[pos] : kNoRow;
+      eend[i] = cend;
+      enext[i] = pos < cend ? rowsA[pos * RS] : kNoRow;
     }
   };
 
@@ -231,7 +318,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
   int64_t w = wnom;
   while (lo < thi) {
     const int32_t hi = (int32_t)(((int64_t)lo + w < thi) ? lo + w : thi);
-    const bool hi_is_end = hi == thi && (full & 2);
+    const bool hi_is_end = hi == thi;  // entry ends are clamped to the task (load_entries)
     const uint32_t tw = (uint32_t)(hi - lo);
     const uint64_t scale = ((uint64_t)T << 32) / (uint64_t)tw;  // numeric order-preserving slot map
     if (bitmap) {
@@ -268,8 +355,8 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
             stop = end;
             nx2 = kNoRow;
           } else {
-            stop = gallop64(a.Air, p + 1, end, hi);
-            nx2 = stop < end ? a.Air[stop] : kNoRow;
+            stop = gallop64<RS>(rowsA, p + 1, end, hi);
+            nx2 = stop < end ? rowsA[stop * RS] : kNoRow;
           }
         }
         eoff[i] = (int32_t)(stop - p);
@@ -307,8 +394,12 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
           const int i = own[x];
           const int64_t q = qoff[i] + w0 + x;
           ow[u] = i;
-          r[u] = a.Air[q];
-          if constexpr (NUM) av[u] = reinterpret_cast<const val_t*>(a.Anum)[q];
+          if constexpr (PK) {
+            ld_rec(recA + q, r[u], av[u]);
+          } else {
+            r[u] = a.Air[q];
+            if constexpr (NUM) av[u] = reinterpret_cast<const val_t*>(a.Anum)[q];
+          }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -323,6 +414,10 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
           if (bitmap) {
             atomicOr(&words[d >> 5], 1u << (d & 31));
           } else if constexpr (NUM) {
+#if CBH_ABL & 2  // ablation build: gather only, no table update (keeps the loads alive)
+            if (r[u] == kNoRow - 1 && vv == val_t(12345)) bad |= 1 << 30;
+            continue;
+#endif
             uint32_t s = (uint32_t)(((uint64_t)d * scale) >> 32);
             bool ok = false;
             for (int probe = 0; probe < kPmax && s < (uint32_t)TA; ++probe, ++s) {
@@ -375,33 +470,31 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
       const int nwords = (int)((tw + 31) >> 5);
       for (int s = tid; s < nwords; s += BS) my_count += __popc(words[s]);
     } else if constexpr (NUM) {
-      // rank commit. Slot s goes to (occupied slots before its run) + (rank of its key in the
-      // run). Wave regions and 64-slot chunks start at run boundaries (a wave's region begins at
-      // an empty slot; a chunk whose last run continues stops before that run), so every run
-      // lies inside one chunk: run bounds come from the occupancy ballot, ranks from DPP shifts.
+      // rank commit. Slot s holding key x goes to (occupied slots before s) - (s - start of its
+      // run) + (keys of its run smaller than x). Wave w owns the 64-aligned slots
+      // [w*SPW, (w+1)*SPW); the start of the run a slot belongs to comes from the occupancy ballot
+      // or, when the run began in an earlier chunk, from the carried last empty slot. Ranks
+      // inside a run come from DPP neighbour compares when the run lies inside the chunk and is
+      // at most kDppMax+1 long; other lanes (runs crossing a chunk edge, long runs of clustered
+      // rows) count the smaller keys of their run with LDS reads.
       constexpr int SPW = ((TA + NW - 1) / NW + 63) / 64 * 64;
-      int sb = wid * SPW;
-      if (wid > 0) {
-        int found = TA;
-        for (int s0 = sb; s0 < TA; s0 += 64) {
-          const int s = s0 + lane;
-          const uint64_t em = __ballot(s < TA && keys[s] == kEmpty);
-          if (em) {
-            found = s0 + __ffsll((long long)em) - 1;
-            break;
-          }
-        }
-        sb = found < TA ? found : TA;
-      }
-      if (lane == 0) red[wid] = sb;
-      __syncthreads();
-      const int se = (wid + 1 < NW) ? red[wid + 1] : TA;
+      constexpr int kDppMax = 4;
+      const int sb = wid * SPW < TA ? wid * SPW : TA;
+      const int se = sb + SPW < TA ? sb + SPW : TA;
       int wc = 0;
       for (int s0 = sb; s0 < se; s0 += 64) {
         const int s = s0 + lane;
         wc += __popcll(__ballot(s < se && keys[s] != kEmpty));
       }
       if (lane == 0) red[NW + wid] = wc;
+      int last_empty = -1;  // last empty slot before the chunk (slot -1 acts as empty)
+      for (int s0 = sb - 64; s0 >= 0; s0 -= 64) {
+        const uint64_t em = __ballot(keys[s0 + lane] == kEmpty);
+        if (em) {
+          last_empty = s0 + 63 - __clzll(em);
+          break;
+        }
+      }
       __syncthreads();
       int64_t o = out_pos;
       int tot = 0;
@@ -412,56 +505,48 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         tot += rr;
       }
       const uint64_t lt = (1ull << lane) - 1ull;
-      int s0 = sb;
-      while (s0 < se) {
+#if CBH_ABL & 1  // ablation build: no commit loop
+      for (int s0 = se; s0 < se; s0 += 64) {
+#else
+      for (int s0 = sb; s0 < se; s0 += 64) {
+#endif
         const int s = s0 + lane;
-        const int32_t key = (s < se) ? keys[s] : kEmpty;
-        const acc_t val = (s < se) ? vals[s] : SR::identity();
+        const bool in = s < se;
+        const int32_t key = in ? keys[s] : kEmpty;
+        const acc_t val = in ? vals[s] : SR::identity();
         const bool occ = key != kEmpty;
-        uint64_t mask = __ballot(occ);
-        // the chunk's last run continues past the chunk: stop the chunk before that run
-        int cut = 64;
-        bool walk = false;
-        if ((mask >> 63) && s0 + 64 < se && keys[s0 + 64] != kEmpty) {
-          const uint64_t em = ~mask;
-          if (em) cut = 64 - __clzll(em);  // one past the last empty lane
-          else walk = true;                // a run of >= 64 slots (clustered rows): LDS walk
-        }
-        const uint64_t keep = cut == 64 ? ~0ull : ((1ull << cut) - 1ull);
-        mask &= keep;
-        const bool mine = occ && lane < cut;
+        const uint64_t mask = __ballot(occ);
+        const bool next_occ = s0 + 64 < TA && keys[s0 + 64] != kEmpty;
         const uint64_t below = ~mask & lt;
-        const uint64_t above = ~mask & ~(lt | (1ull << lane)) & keep;
-        const int rs = below ? 64 - __clzll(below) : 0;
-        const int re = above ? __ffsll((long long)above) - 1 : cut;
-        const int len = re - rs;
-        // the chunk's first run may be the tail of a >= 64-slot run begun in a walked chunk
-        const bool prev_occ = s0 > sb && keys[s0 - 1] != kEmpty;
-        const bool lw = mine && (walk || (prev_occ && rs == 0));
-        const bool dp = mine && !lw;
-        int rank = 0, lead = lane - rs;
+        const uint64_t above = ~mask & ~(lt | (1ull << lane));
+        const int rstart = below ? s0 + 64 - __clzll(below) : last_empty + 1;  // absolute slot
+        const bool right_open = !above && next_occ;  // the run continues into the next chunk
+        const int rend = above ? s0 + __ffsll((long long)above) - 1 : s0 + 64;
+        const int len = rend - rstart;
+        const bool inside = rstart >= s0 && !right_open;
+        const bool dp = occ && inside && len <= kDppMax + 1;
+        const bool lw = occ && !dp;
+        int rank = 0;
         {
           int32_t kl = key, kr = key;
-          for (int d = 1; __ballot(dp && d < len) != 0; ++d) {
-            kl = __builtin_amdgcn_update_dpp(kEmpty, kl, 0x138, 0xf, 0xf, false);  // wave_shr:1
-            kr = __builtin_amdgcn_update_dpp(kEmpty, kr, 0x130, 0xf, 0xf, false);  // wave_shl:1
-            rank += (dp && lane - d >= rs && kl < key) ? 1 : 0;
-            rank += (dp && lane + d < re && kr < key) ? 1 : 0;
+#pragma unroll
+          for (int d = 1; d <= kDppMax; ++d) {
+            if (!__ballot(dp && d < len)) break;
+            kl = __builtin_amdgcn_update_dpp(kEmpty, kl, 0x138, 0xf, 0xf, false);  // wave_shr:1 (lane - d)
+            kr = __builtin_amdgcn_update_dpp(kEmpty, kr, 0x130, 0xf, 0xf, false);  // wave_shl:1 (lane + d)
+            rank += (dp && s - d >= rstart && kl < key) ? 1 : 0;
+            rank += (dp && s + d < rend && kr < key) ? 1 : 0;
           }
         }
-        if (lw) {
-          int a0 = s;
-          while (a0 > 0 && keys[a0 - 1] != kEmpty) --a0;
-          for (int x = a0; x < TA; ++x) {
+        if (lw)
+          for (int x = rstart; x < TA; ++x) {
             const int32_t kx = keys[x];
             if (kx == kEmpty) break;
-            rank += kx < key;
+            rank += kx < key ? 1 : 0;
           }
-          lead = s - a0;
-        }
-        if (mine) {
-          const int64_t pos = o + __popcll(mask & lt) - lead + rank;
-          if (pos >= out_end || pos >= a.ccap || pos < 0) {
+        if (occ) {
+          const int64_t pos = o + __popcll(mask & lt) - (s - rstart) + rank;
+          if (pos >= out_end || pos >= a.ccap || pos < out_pos) {
             bad |= 1 << 5;
           } else {
             a.Cir[pos] = key;
@@ -469,7 +554,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
           }
         }
         o += __popcll(mask);
-        s0 += cut;
+        if (~mask) last_empty = s0 + 63 - __clzll(~mask);
       }
       out_pos += tot;
     }
@@ -482,7 +567,9 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
     const int total = block_sum_int<NW>(my_count, red);
     if (tid == 0) a.cnt[task] = total;
   } else {
+#if !(CBH_ABL & 2)
     if (tid == 0 && out_pos != out_end) atomicAdd(&a.err[0], 1);
+#endif
   }
   if (bad) guard_fail(a.err, 31 - __clz(bad), c, bad, lo);
 #ifdef CBH_STAMPS
