@@ -13,6 +13,9 @@
 //                                                     prints wall time per call (MPI_Wtime)
 //   slice <scale> <ef> <col0> <col1> <reps> <sr>      CPU baseline: A (scale, ef) times the column block
 //                                                     A(:, col0:col1) with Mult_AnXBn_Synch; prints JSON
+//   tc    <scale> <L.cbm> <C.cbm>                     Applications/TC.cpp:62-121 on one rank (C = (L*L).*L)
+//   mcl   <A.cbm> <out.cbm> <hard> <select> <recover> <pct>
+//                                                     MCLPruneRecoverySelect (ParFriends.h:185-353)
 // sr: pt_f64 | pt_i64 | max_i64 | min_i64 | bool ; kernel: hybrid | hash | hashu | heap
 #include <mpi.h>
 
@@ -238,6 +241,47 @@ static int do_slice(int scale, int ef, int64_t c0, int64_t c1, int reps) {
   return 0;
 }
 
+// Applications/TC.cpp:62-121 on one rank (global = local indices): symmetrise, set values to 1,
+// L = tril with the upper entries kept as explicit zeros, C = (L*L) .* L, triangles = sum(C).
+// Writes L and C, prints the triangle count.
+static int do_tc(int scale, const std::string& fl, const std::string& fc) {
+  typedef SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>> Mat;
+  Mat* A = gen_rmat(scale, 16);
+  A->RemoveLoops();
+  Mat AT = *A;
+  AT.Transpose();
+  *A += AT;
+  A->Apply([](int64_t) { return (int64_t)1; });
+  Mat L = *A;
+  for (auto colit = L.seq().begcol(); colit != L.seq().endcol(); ++colit)
+    for (auto nzit = L.seq().begnz(colit); nzit != L.seq().endnz(colit); ++nzit)
+      if (nzit.rowid() < colit.colid()) nzit.value() = 0;
+  Mat Lt = L;
+  Mat C = Mult_AnXBn_Synch<PlusTimesSRing<int64_t, int64_t>, int64_t, SpDCCols<int64_t, int64_t>>(L, Lt);
+  C.EWiseMult(L, false);
+  FullyDistVec<int64_t, int64_t> tri = C.Reduce(Column, std::plus<int64_t>(), static_cast<int64_t>(0));
+  const int64_t result = tri.Reduce(std::plus<int64_t>(), static_cast<int64_t>(0));
+  cbm::write(fl, from_spdccols<int64_t>(L.seq()));
+  cbm::write(fc, from_spdccols<int64_t>(C.seq()));
+  std::printf("{\"triangles\": %lld, \"nnzL\": %lld, \"nnzC\": %lld}\n", (long long)result, (long long)L.getnnz(),
+              (long long)C.getnnz());
+  delete A;
+  return 0;
+}
+
+// HipMCL post-expansion step (ParFriends.h:185-353, kselectVersion 1) on one rank: reads the
+// expanded matrix (f64), writes it after MCLPruneRecoverySelect.
+static int do_mcl(const std::string& fa, const std::string& fo, double hard, int64_t sel, int64_t rec, double pct) {
+  typedef SpDCCols<int64_t, double> DER;
+  std::shared_ptr<CommGrid> grid(new CommGrid(MPI_COMM_WORLD, 0, 0));
+  cbm::Dcsc a = cbm::read(fa);
+  SpParMat<int64_t, double, DER> A(to_spdccols<double>(a), grid);
+  MCLPruneRecoverySelect(A, hard, sel, rec, pct, 1);
+  cbm::write(fo, from_spdccols<double>(A.seq()));
+  std::printf("{\"nnz\": %lld}\n", (long long)A.getnnz());
+  return 0;
+}
+
 #define DISPATCH_SR(sr, CALL)                                                   \
   if (sr == "pt_f64") {                                                         \
     typedef PlusTimesSRing<double, double> SR;                                  \
@@ -284,6 +328,9 @@ static int run(int argc, char** argv) {
     DISPATCH_SR(sr, (do_slice<SR, NT>(std::atoi(argv[2]), std::atoi(argv[3]), std::atoll(argv[4]),
                                       std::atoll(argv[5]), std::atoi(argv[6]))));
   }
+  if (mode == "tc" && argc == 5) return do_tc(std::atoi(argv[2]), argv[3], argv[4]);
+  if (mode == "mcl" && argc == 8)
+    return do_mcl(argv[2], argv[3], std::atof(argv[4]), std::atoll(argv[5]), std::atoll(argv[6]), std::atof(argv[7]));
   std::fprintf(stderr, "bad arguments\n");
   return 2;
 }

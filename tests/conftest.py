@@ -44,3 +44,14 @@ def ctx():
     yield c
     torch.cuda.synchronize()
     c.close()
+
+
+@pytest.fixture(scope="session")
+def apps():
+    return H.load_npz(os.path.join(H.GOLDEN, "apps.npz"))
+
+
+@pytest.fixture(scope="session")
+def apps_meta():
+    with open(os.path.join(H.GOLDEN, "apps.json")) as f:
+        return json.load(f)
