@@ -73,6 +73,18 @@ SIGNATURES = {
     "cbh_ctx_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "cbh_kernel_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(cbh_kernel_stat)]),
     "cbh_kernel_stats_reset": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbh_spgemm_masked": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_ewise_mult": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_col_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p]),
+    "cbh_kselect_hist": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                        ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "cbh_kselect_pick": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_int]),
+    "cbh_kselect_value": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "cbh_prune_columns": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_rmat_edges": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                       ctypes.c_void_p]),
     "cbh_edges_to_csc": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
@@ -85,6 +97,7 @@ ERRORS = {3001: "GRIDMISMATCH", 3002: "DIMMISMATCH", 3005: "MATRIXALIAS", 4001: 
           4003: "invalid argument", 4004: "device consistency check failed", 4005: "no HIP device"}
 
 CBH_KEEP_EMPTY_COLS = 0x2
+CBH_MASK_PATTERN = 0x4
 CBH_PHASE_CHECKSUM = 0x100
 
 

@@ -1,0 +1,86 @@
+"""Host mirror of the callers around the SpGEMM hot path, all on the gfx950
+kernels of combblas_amd/csrc/apps.h behind the C-ABI (no CPU path):
+
+  MaskedSpGEMM(SR, A, B, M)   C = (A*B) .* M in one pass -- TC.cpp:108-110 (Mult_AnXBn_Synch then
+                              EWiseMult(L, false)) fused; pattern=True keeps the semiring sums
+  EWiseMult(A, B)             SpParMat::EWiseMult(B, false) -> Friends.h:834-887
+  TriangleCount(L)            TC.cpp:108-115 on one block: sum of (L*L) .* L
+  ColumnStats / Kselect /     the column operations of MCLPruneRecoverySelect (ParFriends.h:185-353),
+  PruneColumn                 SpParMat::Kselect1 (SpParMat.cpp:1413-1700), Dcsc::PruneColumn
+                              (dcsc.cpp:699-760)
+The distributed MCLPruneRecoverySelect (process-column reductions) is in parfriends.py.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from ._lib import CBH_MASK_PATTERN, check, lib
+from .semirings import Semiring
+from .spdccols import SpDCCols
+
+DBL_MIN = 2.2250738585072014e-308  # std::numeric_limits<double>::min() (Kselect1, empty column)
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def MaskedSpGEMM(SR: Semiring, A: SpDCCols, B: SpDCCols, M: SpDCCols, pattern=False) -> SpDCCols:
+    h = ctypes.c_void_p()
+    check(lib().cbh_spgemm_masked(A.ctx.h, SR.code, A.h, B.h, M.h, CBH_MASK_PATTERN if pattern else 0,
+                                  ctypes.byref(h)), A.ctx.h)
+    return SpDCCols(A.ctx, h)
+
+
+def EWiseMult(A: SpDCCols, B: SpDCCols) -> SpDCCols:
+    h = ctypes.c_void_p()
+    check(lib().cbh_ewise_mult(A.ctx.h, A.h, B.h, ctypes.byref(h)), A.ctx.h)
+    return SpDCCols(A.ctx, h)
+
+
+def TriangleCount(L: SpDCCols, L2: SpDCCols = None) -> int:
+    """TC.cpp:108-115: C = (L*L) .* L, triangles = sum(C). L2 is a second copy of L (the
+    product's operands must not alias, ParFriends.h:172-179)."""
+    from .semirings import PlusTimesSRing
+    own = L2 is None
+    if own:
+        L2 = SpDCCols.from_tensors(L.ctx, L.m, L.n, *[t.clone() for t in L.tensors()])
+    C = MaskedSpGEMM(PlusTimesSRing, L, L2, L)
+    tri = int(C.tensors()[3].sum().item()) if C.nnz else 0
+    C.free()
+    if own:
+        L2.free()
+    return tri
+
+
+def ColumnStats(A: SpDCCols, hard: float):
+    """(nnz, nnz of v > hard, sum of v > hard) per column as f64 device vectors over A's columns"""
+    dev = A.ctx.tdevice
+    out = [torch.empty(A.n, dtype=torch.float64, device=dev) for _ in range(3)]
+    check(lib().cbh_col_stats(A.ctx.h, A.h, ctypes.c_double(hard), *[_p(t) for t in out]), A.ctx.h)
+    return tuple(out)
+
+
+def kselect_hist(A: SpDCCols, aidx, nact, prefix, shift):
+    hist = torch.empty(nact * 256, dtype=torch.int32, device=A.ctx.tdevice)
+    check(lib().cbh_kselect_hist(A.ctx.h, A.h, _p(aidx), nact, _p(prefix), shift, _p(hist)), A.ctx.h)
+    return hist
+
+
+def kselect_pick(ctx, nact, hist, prefix, rank, shift):
+    check(lib().cbh_kselect_pick(ctx.h, nact, _p(hist), _p(prefix), _p(rank), shift), ctx.h)
+
+
+def kselect_value(ctx, nact, prefix):
+    out = torch.empty(nact, dtype=torch.float64, device=ctx.tdevice)
+    check(lib().cbh_kselect_value(ctx.h, nact, _p(prefix), _p(out)), ctx.h)
+    return out
+
+
+def PruneColumn(A: SpDCCols, thresh) -> SpDCCols:
+    """entries with !(v < thresh[col]) kept (SpParMat::PruneColumn(pvals, std::less))"""
+    h = ctypes.c_void_p()
+    check(lib().cbh_prune_columns(A.ctx.h, A.h, _p(thresh.contiguous()), ctypes.byref(h)), A.ctx.h)
+    return SpDCCols(A.ctx, h)

@@ -72,3 +72,33 @@ class HipBackend:
 
     def synchronize(self):
         self.ctx.synchronize()
+
+    # ------------------------------------------------------------------ callers around the hot path
+    # (C-ABI entry points of combblas_amd/csrc/apps.h; vectors are device tensors)
+    def masked(self, SR, A: SpDCCols, B: SpDCCols, M: SpDCCols, pattern=False) -> SpDCCols:
+        from .apps import MaskedSpGEMM
+        return MaskedSpGEMM(SR, A, B, M, pattern=pattern)
+
+    def ewise_mult(self, A: SpDCCols, B: SpDCCols) -> SpDCCols:
+        from .apps import EWiseMult
+        return EWiseMult(A, B)
+
+    def col_stats(self, A: SpDCCols, hard):
+        from .apps import ColumnStats
+        return ColumnStats(A, hard)
+
+    def kselect_hist(self, A: SpDCCols, aidx, nact, prefix, shift):
+        from .apps import kselect_hist
+        return kselect_hist(A, aidx, nact, prefix, shift)
+
+    def kselect_pick(self, nact, hist, prefix, rank, shift):
+        from .apps import kselect_pick
+        kselect_pick(self.ctx, nact, hist, prefix, rank, shift)
+
+    def kselect_value(self, nact, prefix):
+        from .apps import kselect_value
+        return kselect_value(self.ctx, nact, prefix)
+
+    def prune_columns(self, A: SpDCCols, thresh) -> SpDCCols:
+        from .apps import PruneColumn
+        return PruneColumn(A, thresh)

@@ -22,6 +22,7 @@
 #include "../../include/combblas_hip.h"
 #include "semiring.h"
 #include "task_kernel.h"
+#include "apps.h"
 
 using namespace cbh;
 
@@ -1499,4 +1500,222 @@ int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* p
   });
 }
 
+// ============================================================================ callers around the hot path
+// (TC's masked product, EWiseMult, HipMCL's column prune/select/recover)
+
+int cbh_spgemm_masked(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh_mat* B, const cbh_mat* M,
+                      uint32_t flags, cbh_mat** C) {
+  CBH_TRY(validate_pair(ctx, A, B));
+  if (!M || !C) return fail(ctx, CBH_E_ARG, "null mask or output");
+  if (M->m != A->m || M->n != B->n) return fail(ctx, CBH_E_DIMMISMATCH, "mask dimensions differ from A*B's");
+  if (M->dtype != A->dtype) return fail(ctx, CBH_E_ARG, "mask dtype differs from A's");
+  *C = nullptr;
+  if (A->nnz == 0 || B->nnz == 0 || M->nnz == 0) return empty_result(ctx, A->m, B->n, A->dtype, C);
+  if (B->nzc > INT32_MAX) return fail(ctx, CBH_E_ARG, "too many columns for one launch");
+  const bool pattern = (flags & CBH_MASK_PATTERN) != 0;
+  return dispatch_sr(ctx, sr, A->dtype, [&](auto srv) -> int {
+    using SR = decltype(srv);
+    using VT = typename SR::val_t;
+    Scratch S(ctx);
+    const int64_t nb = B->nzc;
+    int64_t *Adense, *mslot, *hits, *off, *flag, *pos;
+    int32_t* Tir;
+    VT* Tnum;
+    CBH_TRY(S.get(&Adense, A->n + 1));
+    CBH_TRY(S.get(&mslot, nb));
+    CBH_TRY(S.get(&hits, nb + 1));
+    CBH_TRY(S.get(&off, nb + 1));
+    CBH_TRY(S.get(&flag, nb + 1));
+    CBH_TRY(S.get(&pos, nb + 1));
+    CBH_TRY(S.get(&Tir, M->nnz));
+    CBH_TRY(S.get(&Tnum, M->nnz));
+    hipLaunchKernelGGL(densify_cp_kernel, dim3(blocks_for(A->n + 1, 256)), dim3(256), 0, ctx->stream, A->jc, A->cp,
+                       A->nzc, A->n, A->nnz, Adense);
+    hipLaunchKernelGGL(match_slots_kernel, dim3(blocks_for(nb, 256)), dim3(256), 0, ctx->stream, B->jc, nb, M->jc,
+                       M->nzc, mslot);
+    CBH_HIP(ctx, hipMemsetAsync(hits + nb, 0, sizeof(int64_t), ctx->stream));
+    MaskArgs a{Adense, A->ir, A->num, B->cp, B->ir, B->num, nb, mslot, M->cp, M->ir, M->num, Tir, Tnum, hits,
+               ctx->d_err, A->nnz, A->n};
+    if (pattern)
+      hipLaunchKernelGGL((masked_kernel<SR, 2048, 256, 256, true>), dim3((unsigned)nb), dim3(256), 0, ctx->stream, a);
+    else
+      hipLaunchKernelGGL((masked_kernel<SR, 2048, 256, 256, false>), dim3((unsigned)nb), dim3(256), 0, ctx->stream, a);
+    CBH_HIP(ctx, hipGetLastError());
+    CBH_TRY(exclusive_scan_i64(ctx, S, hits, off, nb + 1));
+    hipLaunchKernelGGL(nz_flag_kernel, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, ctx->stream, hits, nb + 1, flag);
+    CBH_TRY(exclusive_scan_i64(ctx, S, flag, pos, nb + 1));
+    int64_t h[2];
+    CBH_HIP(ctx, hipMemcpyAsync(&h[0], off + nb, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(&h[1], pos + nb, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    CBH_TRY(check_err(ctx));
+    cbh_mat* out;
+    CBH_TRY(new_mat(ctx, A->m, B->n, h[0], h[1], A->dtype, &out));
+    hipLaunchKernelGGL(gather_cols_kernel<VT>, dim3(blocks_for(nb, 4)), dim3(256), 0, ctx->stream, mslot, M->cp, hits,
+                       off, nb, Tir, Tnum, out->ir, reinterpret_cast<VT*>(out->num));
+    hipLaunchKernelGGL(compact_cols_kernel, dim3(blocks_for(nb, 256)), dim3(256), 0, ctx->stream, hits, pos, B->jc, off,
+                       nb, out->jc, out->cp);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      cbh_mat_free(ctx, out);
+      return fail(ctx, CBH_E_HIP, std::string("masked compaction: ") + hipGetErrorString(e));
+    }
+    *C = out;
+    return CBH_OK;
+  });
+}
+
+int cbh_ewise_mult(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, cbh_mat** C) {
+  if (!ctx || !A || !B || !C) return fail(ctx, CBH_E_ARG, "null argument");
+  if (A->m != B->m || A->n != B->n) return fail(ctx, CBH_E_DIMMISMATCH, "EWiseMult operands differ in shape");
+  if (A->dtype != B->dtype) return fail(ctx, CBH_E_ARG, "EWiseMult operands differ in dtype");
+  *C = nullptr;
+  if (A->nnz == 0 || B->nnz == 0) return empty_result(ctx, A->m, A->n, A->dtype, C);
+  auto run = [&](auto tag) -> int {
+    using VT = decltype(tag);
+    Scratch S(ctx);
+    const int64_t na = A->nzc;
+    int64_t *bslot, *hits, *off, *flag, *pos;
+    CBH_TRY(S.get(&bslot, na));
+    CBH_TRY(S.get(&hits, na + 1));
+    CBH_TRY(S.get(&off, na + 1));
+    CBH_TRY(S.get(&flag, na + 1));
+    CBH_TRY(S.get(&pos, na + 1));
+    hipLaunchKernelGGL(match_slots_kernel, dim3(blocks_for(na, 256)), dim3(256), 0, ctx->stream, A->jc, na, B->jc,
+                       B->nzc, bslot);
+    CBH_HIP(ctx, hipMemsetAsync(hits + na, 0, sizeof(int64_t), ctx->stream));
+    const VT* an = reinterpret_cast<const VT*>(A->num);
+    const VT* bn = reinterpret_cast<const VT*>(B->num);
+    hipLaunchKernelGGL((ewise_kernel<VT, false>), dim3(blocks_for(na, 4)), dim3(256), 0, ctx->stream, A->cp, A->ir, an,
+                       na, bslot, B->cp, B->ir, bn, hits, nullptr, nullptr, nullptr);
+    CBH_HIP(ctx, hipGetLastError());
+    CBH_TRY(exclusive_scan_i64(ctx, S, hits, off, na + 1));
+    hipLaunchKernelGGL(nz_flag_kernel, dim3(blocks_for(na + 1, 256)), dim3(256), 0, ctx->stream, hits, na + 1, flag);
+    CBH_TRY(exclusive_scan_i64(ctx, S, flag, pos, na + 1));
+    int64_t h[2];
+    CBH_HIP(ctx, hipMemcpyAsync(&h[0], off + na, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(&h[1], pos + na, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    cbh_mat* out;
+    CBH_TRY(new_mat(ctx, A->m, A->n, h[0], h[1], A->dtype, &out));
+    hipLaunchKernelGGL((ewise_kernel<VT, true>), dim3(blocks_for(na, 4)), dim3(256), 0, ctx->stream, A->cp, A->ir, an,
+                       na, bslot, B->cp, B->ir, bn, hits, off, out->ir, reinterpret_cast<VT*>(out->num));
+    hipLaunchKernelGGL(compact_cols_kernel, dim3(blocks_for(na, 256)), dim3(256), 0, ctx->stream, hits, pos, A->jc, off,
+                       na, out->jc, out->cp);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      cbh_mat_free(ctx, out);
+      return fail(ctx, CBH_E_HIP, std::string("ewise: ") + hipGetErrorString(e));
+    }
+    *C = out;
+    return CBH_OK;
+  };
+  switch (A->dtype) {
+    case CBH_F64: return run(double{});
+    case CBH_I64: return run(int64_t{});
+    case CBH_F32: return run(float{});
+    case CBH_I32: return run(int32_t{});
+    case CBH_BOOL: return run(uint8_t{});
+  }
+  return fail(ctx, CBH_E_ARG, "unknown dtype");
+}
+
+static int need_f64(cbh_ctx* ctx, const cbh_mat* A) {
+  if (!ctx || !A) return fail(ctx, CBH_E_ARG, "null argument");
+  if (A->dtype != CBH_F64) return fail(ctx, CBH_E_ARG, "the MCL column operations take f64 matrices");
+  return CBH_OK;
+}
+
+int cbh_col_stats(cbh_ctx* ctx, const cbh_mat* A, double hard, double* cnt, double* cntp, double* sump) {
+  CBH_TRY(need_f64(ctx, A));
+  if (!cnt || !cntp || !sump) return fail(ctx, CBH_E_ARG, "null output vector");
+  const size_t nb = sizeof(double) * (size_t)A->n;
+  CBH_HIP(ctx, hipMemsetAsync(cnt, 0, nb, ctx->stream));
+  CBH_HIP(ctx, hipMemsetAsync(cntp, 0, nb, ctx->stream));
+  CBH_HIP(ctx, hipMemsetAsync(sump, 0, nb, ctx->stream));
+  if (A->nzc > 0) {
+    hipLaunchKernelGGL(colstat_kernel, dim3(blocks_for(A->nzc, 4)), dim3(256), 0, ctx->stream, A->jc, A->cp,
+                       reinterpret_cast<const double*>(A->num), A->nzc, hard, cnt, cntp, sump);
+    CBH_HIP(ctx, hipGetLastError());
+  }
+  return CBH_OK;
+}
+
+int cbh_kselect_hist(cbh_ctx* ctx, const cbh_mat* A, const int32_t* active_index, int64_t nactive,
+                     const uint64_t* prefix, int shift, uint32_t* hist) {
+  CBH_TRY(need_f64(ctx, A));
+  if (shift < 0 || shift > 56 || shift % 8) return fail(ctx, CBH_E_ARG, "radix shift must be 0, 8, ..., 56");
+  if (nactive <= 0) return CBH_OK;
+  if (!active_index || !prefix || !hist) return fail(ctx, CBH_E_ARG, "null argument");
+  CBH_HIP(ctx, hipMemsetAsync(hist, 0, sizeof(uint32_t) * 256 * (size_t)nactive, ctx->stream));
+  if (A->nzc > 0) {
+    if (A->nzc > INT32_MAX) return fail(ctx, CBH_E_ARG, "too many columns for one launch");
+    hipLaunchKernelGGL(kselect_hist_kernel, dim3((unsigned)A->nzc), dim3(256), 0, ctx->stream, A->jc, A->cp,
+                       reinterpret_cast<const double*>(A->num), A->nzc, active_index, prefix, shift, hist);
+    CBH_HIP(ctx, hipGetLastError());
+  }
+  return CBH_OK;
+}
+
+int cbh_kselect_pick(cbh_ctx* ctx, int64_t nactive, const uint32_t* hist, uint64_t* prefix, int64_t* rank,
+                     int shift) {
+  if (!ctx) return CBH_E_ARG;
+  if (nactive <= 0) return CBH_OK;
+  if (!hist || !prefix || !rank) return fail(ctx, CBH_E_ARG, "null argument");
+  hipLaunchKernelGGL(kselect_pick_kernel, dim3(blocks_for(nactive, 256)), dim3(256), 0, ctx->stream, nactive, hist,
+                     prefix, rank, shift);
+  CBH_HIP(ctx, hipGetLastError());
+  return CBH_OK;
+}
+
+int cbh_kselect_value(cbh_ctx* ctx, int64_t nactive, const uint64_t* prefix, double* out) {
+  if (!ctx) return CBH_E_ARG;
+  if (nactive <= 0) return CBH_OK;
+  if (!prefix || !out) return fail(ctx, CBH_E_ARG, "null argument");
+  hipLaunchKernelGGL(kselect_value_kernel, dim3(blocks_for(nactive, 256)), dim3(256), 0, ctx->stream, nactive, prefix,
+                     out);
+  CBH_HIP(ctx, hipGetLastError());
+  return CBH_OK;
+}
+
+int cbh_prune_columns(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, cbh_mat** C) {
+  CBH_TRY(need_f64(ctx, A));
+  if (!thresh || !C) return fail(ctx, CBH_E_ARG, "null argument");
+  *C = nullptr;
+  if (A->nnz == 0) return empty_result(ctx, A->m, A->n, A->dtype, C);
+  Scratch S(ctx);
+  const int64_t nz = A->nzc;
+  int64_t *kept, *off, *flag, *pos;
+  CBH_TRY(S.get(&kept, nz + 1));
+  CBH_TRY(S.get(&off, nz + 1));
+  CBH_TRY(S.get(&flag, nz + 1));
+  CBH_TRY(S.get(&pos, nz + 1));
+  const double* num = reinterpret_cast<const double*>(A->num);
+  CBH_HIP(ctx, hipMemsetAsync(kept + nz, 0, sizeof(int64_t), ctx->stream));
+  hipLaunchKernelGGL(prune_col_kernel<false>, dim3(blocks_for(nz, 4)), dim3(256), 0, ctx->stream, A->jc, A->cp, A->ir,
+                     num, nz, thresh, kept, nullptr, nullptr, nullptr);
+  CBH_HIP(ctx, hipGetLastError());
+  CBH_TRY(exclusive_scan_i64(ctx, S, kept, off, nz + 1));
+  hipLaunchKernelGGL(nz_flag_kernel, dim3(blocks_for(nz + 1, 256)), dim3(256), 0, ctx->stream, kept, nz + 1, flag);
+  CBH_TRY(exclusive_scan_i64(ctx, S, flag, pos, nz + 1));
+  int64_t h[2];
+  CBH_HIP(ctx, hipMemcpyAsync(&h[0], off + nz, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipMemcpyAsync(&h[1], pos + nz, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  cbh_mat* out;
+  CBH_TRY(new_mat(ctx, A->m, A->n, h[0], h[1], A->dtype, &out));
+  hipLaunchKernelGGL(prune_col_kernel<true>, dim3(blocks_for(nz, 4)), dim3(256), 0, ctx->stream, A->jc, A->cp, A->ir,
+                     num, nz, thresh, kept, off, out->ir, reinterpret_cast<double*>(out->num));
+  hipLaunchKernelGGL(compact_cols_kernel, dim3(blocks_for(nz, 256)), dim3(256), 0, ctx->stream, kept, pos, A->jc, off,
+                     nz, out->jc, out->cp);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    cbh_mat_free(ctx, out);
+    return fail(ctx, CBH_E_HIP, std::string("prune: ") + hipGetErrorString(e));
+  }
+  *C = out;
+  return CBH_OK;
+}
+
 }  // extern "C"
+

@@ -178,11 +178,14 @@ def Mult_AnXBn_Synch(SR, A: SpParMat, B: SpParMat, clearA=False, clearB=False) -
     return SpParMat(C, grid, be, A.m, B.n, A.row_off, B.col_off)
 
 
-def MemEfficientSpGEMM(SR, A: SpParMat, B: SpParMat, phases=0, perProcessMemory=0, on_phase=None):
-    """Phased 2D SUMMA (ParFriends.h:449-730 without the MCL prune). phases=0 plans the phases
-    from the exact symbolic pass and `perProcessMemory` bytes (default 40 % of free HBM).
-    on_phase(C_block, c0, c1) consumes each phase's block of C (local columns [c0, c1)); without
-    it the phases are concatenated and the SpParMat C is returned."""
+def MemEfficientSpGEMM(SR, A: SpParMat, B: SpParMat, phases=0, hardThreshold=None, selectNum=0, recoverNum=0,
+                       recoverPct=0.0, kselectVersion=1, computationKernel=1, perProcessMemory=0, on_phase=None):
+    """Phased 2D SUMMA (ParFriends.h:449-730; same argument order). phases=0 plans the phases
+    from the exact symbolic pass and `perProcessMemory` bytes (default 40 % of free HBM). With a
+    hardThreshold every phase's block goes through MCLPruneRecoverySelect (:698) before it is
+    kept. on_phase(C_block, c0, c1) consumes each phase's block of C (local columns [c0, c1));
+    without it the phases are concatenated and the SpParMat C is returned. computationKernel
+    (hash / heap) selects the same device kernel: both contracts are met by it."""
     _check_dims(A, B)
     grid, stages = ProductGrid(A.commGrid, B.commGrid)
     be = A.backend
@@ -193,6 +196,8 @@ def MemEfficientSpGEMM(SR, A: SpParMat, B: SpParMat, phases=0, perProcessMemory=
     for c0, c1 in cuts:
         parts = [be.multiply(SR, a, _colslice(be, b, c0, c1)) for a, b in zip(Ab, Bb)]
         C = _merge(be, SR, parts, m, n, vdtype)
+        if hardThreshold is not None:
+            C = _mcl_block(be, C, grid.colWorld, hardThreshold, selectNum, recoverNum, recoverPct)
         if on_phase is not None:
             on_phase(C, c0, c1)
         else:
@@ -276,6 +281,112 @@ def Mult_AnXBn_SUMMA3D(SR, A: SpParMat3D, B: SpParMat3D, phases=1, perProcessMem
     w = div[g3.rankInFiber]
     Cb = _concat_cols(be, out, m, w, vdtype)
     return SpParMat3D(Cb, g3, be, A.m, B.n, True, A.row_off, B.col_off + mine0)
+
+
+def MemEfficientSpGEMM3D(SR, A: SpParMat3D, B: SpParMat3D, phases=1, hardThreshold=None, selectNum=0, recoverNum=0,
+                         recoverPct=0.0, kselectVersion=1, computationKernel=1, perProcessMemory=0):
+    """HipMCL's 3D expansion (ParFriends.h:3215-3700): per phase the layer SUMMA, the fiber
+    reduce-scatter, then MCLPruneRecoverySelect on the phase's piece as a matrix of the layer's
+    2D grid (:3683-3686: column statistics reduce over the layer's processor column)."""
+    g3 = A.commGrid3D
+    be = A.backend
+    colgroup = g3.commGridLayer.colWorld
+    got = []
+
+    def keep(C, p0, p1):
+        if hardThreshold is not None:
+            C = _mcl_block(be, C, colgroup, hardThreshold, selectNum, recoverNum, recoverPct)
+        got.append(C)
+
+    Mult_AnXBn_SUMMA3D(SR, A, B, phases=phases, perProcessMemory=perProcessMemory, on_phase=keep)
+    m, w = be.dims(got[0])[0], be.dims(got[0])[1]
+    div = _divisions3d(be.dims(B.seq)[1], g3.gridLayers)
+    mine0 = sum(div[:g3.rankInFiber])
+    Cb = _concat_cols(be, got, m, w, be.value_dtype(A.seq))
+    return SpParMat3D(Cb, g3, be, A.m, B.n, True, A.row_off, B.col_off + mine0)
+
+
+# ---------------------------------------------------------------------------- TC / MCL callers
+def EWiseMult(A: SpParMat, B: SpParMat, exclude=False) -> SpParMat:
+    """SpParMat::EWiseMult(B, false) (SpParMat.cpp, Friends.h:834-887) on identically distributed
+    matrices: the local blocks are intersected, values multiplied (TC.cpp:110)."""
+    if exclude:
+        raise NotImplementedError("EWiseMult(exclude=true) (SetDifference) is outside the hot-path scope")
+    be = A.backend
+    return SpParMat(be.ewise_mult(A.seq, B.seq), A.commGrid, be, A.m, A.n, A.row_off, A.col_off)
+
+
+def ColumnStats(be, blk, hard, colgroup=None):
+    """per-column (nnz, nnz of v > hard, sum of v > hard) of the distributed matrix's local
+    columns, summed over the processor column (A.Reduce(Column, ...), ParFriends.h:196-200)"""
+    cnt, cntp, sump = be.col_stats(blk, hard)
+    if colgroup is not None:
+        for t in (cnt, cntp, sump):
+            allreduce_(t, colgroup)
+    return cnt, cntp, sump
+
+
+def Kselect(be, blk, active, k, colgroup=None, total=None):
+    """k-th largest value of every active column (SpParMat::Kselect1, SpParMat.cpp:1413-1700):
+    sorted descending, element k-1; the smallest when the column has fewer than k entries;
+    numeric_limits<double>::min() when it is empty. Radix select over order-preserving keys, 8
+    bits per pass, the digit histograms summed over the processor column (instead of gathering
+    every rank's top-k list up the column as the reference does). Returns a dense f64 vector
+    (NaN outside `active`)."""
+    dev = be.device
+    n = be.dims(blk)[1]
+    kth = torch.full((n,), float("nan"), dtype=torch.float64, device=dev)
+    act = torch.nonzero(active).flatten()
+    nact = int(act.numel())
+    if nact == 0:
+        return kth
+    if total is None:
+        total = ColumnStats(be, blk, float("-inf"), colgroup)[0]
+    aidx = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    aidx[act] = torch.arange(nact, dtype=torch.int32, device=dev)
+    tot = total[act].to(torch.int64)
+    rank = torch.where(tot >= k, torch.full_like(tot, k - 1), tot - 1).contiguous()
+    prefix = torch.zeros(nact, dtype=torch.int64, device=dev)  # uint64 key bits
+    for shift in range(56, -1, -8):
+        hist = be.kselect_hist(blk, aidx, nact, prefix, shift)
+        if colgroup is not None:
+            allreduce_(hist, colgroup)
+        be.kselect_pick(nact, hist, prefix, rank, shift)
+    vals = be.kselect_value(nact, prefix)
+    kth[act] = torch.where(tot > 0, vals, torch.full_like(vals, 2.2250738585072014e-308))
+    return kth
+
+
+def _mcl_block(be, A, colgroup, hardThreshold, selectNum, recoverNum, recoverPct):
+    """ParFriends.h:185-353 on a local block whose columns may be split over `colgroup`"""
+    inf = float("-inf")
+    cnt, cntp, sump = ColumnStats(be, A, hardThreshold, colgroup)  # unpruned nnz, pruned nnz, pruned sums
+    prune = torch.full_like(cnt, hardThreshold)
+    rec = (cntp < recoverNum) & (cnt > cntp) & (sump < recoverPct)
+    if bool(rec.any()):
+        prune = torch.where(rec, Kselect(be, A, rec, recoverNum, colgroup, cnt), prune)
+    if selectNum > 0:
+        sel = ~rec & (cntp > selectNum)
+        if bool(sel.any()):
+            prune = torch.where(sel, Kselect(be, A, sel, selectNum, colgroup, cnt), prune)
+            if recoverNum > 0:
+                S = be.prune_columns(A, prune)
+                _, cnt1, sum1 = ColumnStats(be, S, inf, colgroup)
+                be.free(S)
+                s2 = sel & (cnt1 < recoverNum) & (sum1 < recoverPct)
+                if bool(s2.any()):
+                    prune = torch.where(s2, Kselect(be, A, s2, recoverNum, colgroup, cnt), prune)
+    out = be.prune_columns(A, prune)
+    be.free(A)
+    return out
+
+
+def MCLPruneRecoverySelect(A: SpParMat, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion=1):
+    """ParFriends.h:185-353: prune entries below per-column thresholds -- hardThreshold, or the
+    selectNum-th / recoverNum-th largest entry for columns needing selection / recovery. A is
+    pruned in place (its local block replaced), as in the reference."""
+    A.seq = _mcl_block(A.backend, A.seq, A.commGrid.colWorld, hardThreshold, selectNum, recoverNum, recoverPct)
+    return A
 
 
 def PSpGEMM(SR, A, B, **kw):

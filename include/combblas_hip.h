@@ -167,6 +167,34 @@ typedef struct cbh_kernel_stat {
 int cbh_kernel_stats(cbh_ctx* ctx, int kind, cbh_kernel_stat* out);
 int cbh_kernel_stats_reset(cbh_ctx* ctx);
 
+/* ---------------------------------------------------------------- callers around the hot path
+ * (device kernels in combblas_amd/csrc/apps.h)                           */
+/* C = (A*B) .* M in one pass: Applications/TC.cpp:108-110 (Mult_AnXBn_Synch(L, L) then
+ * C.EWiseMult(L, false), Friends.h:834-887). Pattern = pattern(A*B) ∩ pattern(M) (explicit zeros
+ * count), rows ascending; values SR-sum * M(i,j), or the SR-sum alone with CBH_MASK_PATTERN.   */
+#define CBH_MASK_PATTERN 0x4u
+int cbh_spgemm_masked(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh_mat* B, const cbh_mat* M,
+                      uint32_t flags, cbh_mat** C);
+/* C = A .* B (SpParMat::EWiseMult(B, false) -> Friends.h:834-887): intersection, values A*B. */
+int cbh_ewise_mult(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, cbh_mat** C);
+/* HipMCL column operations on f64 blocks (ParFriends.h:185-353). Vectors are device arrays over
+ * the block's n columns.
+ *   cbh_col_stats      cnt = nnz per column, cntp / sump = count / sum of the entries > hard
+ *                      (A.Reduce(Column,...) and Prune(v <= hard).Reduce(Column,...), :196-200)
+ *   cbh_kselect_*      SpParMat::Kselect1 (SpParMat.cpp:1413-1700) as an 8-pass radix select:
+ *                      per pass, hist (nactive x 256) of the keys matching prefix above the digit
+ *                      at `shift` (56, 48, ..., 0), then pick the digit holding rank (descending).
+ *                      Histograms may be summed over a processor column between the two calls.
+ *                      active_index[col] = slot in the active list or -1.
+ *   cbh_prune_columns  keep entries with !(v < thresh[col]) (Dcsc::PruneColumn, dcsc.cpp:699-760) */
+int cbh_col_stats(cbh_ctx* ctx, const cbh_mat* A, double hard, double* cnt, double* cntp, double* sump);
+int cbh_kselect_hist(cbh_ctx* ctx, const cbh_mat* A, const int32_t* active_index, int64_t nactive,
+                     const uint64_t* prefix, int shift, uint32_t* hist);
+int cbh_kselect_pick(cbh_ctx* ctx, int64_t nactive, const uint32_t* hist, uint64_t* prefix, int64_t* rank,
+                     int shift);
+int cbh_kselect_value(cbh_ctx* ctx, int64_t nactive, const uint64_t* prefix, double* out);
+int cbh_prune_columns(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, cbh_mat** C);
+
 /* ---------------------------------------------------------------- inputs (host side) */
 int cbh_rmat_edges(int scale, uint64_t userseed, int64_t start_edge, int64_t end_edge, int64_t* src,
                    int64_t* dst);

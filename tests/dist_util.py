@@ -22,6 +22,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
 
 import helpers as H  # noqa: E402
 
@@ -97,6 +98,62 @@ class OracleBackend:
 
     def synchronize(self):
         pass
+
+    # ---- callers around the hot path (numpy restatements, oracle/apps_oracle.py)
+    def ewise_mult(self, A, B):
+        import apps_oracle as AO
+        return self._from_dcsc(AO.ewise_mult(A.dcsc(), B.dcsc()))
+
+    def masked(self, SR, A, B, M, pattern=False):
+        import apps_oracle as AO
+        C = self.multiply(SR, A, B).dcsc()
+        ones = H.Dcsc(M.m, M.n, M.jc.numpy(), M.cp.numpy(), M.ir.numpy(), np.ones(M.ir.numel(), C.num.dtype))
+        return self._from_dcsc(AO.ewise_mult(C, ones if pattern else M.dcsc()))
+
+    @staticmethod
+    def col_stats(A, hard):
+        import apps_oracle as AO
+        return tuple(torch.from_numpy(x) for x in AO.column_stats(A.dcsc(), hard))
+
+    @staticmethod
+    def kselect_hist(A, aidx, nact, prefix, shift):
+        d = A.dcsc()
+        hist = np.zeros((nact, 256), np.int32)
+        ai = aidx.numpy()[d.cols()]
+        sel = ai >= 0
+        b = d.num[sel].astype(np.float64).view(np.uint64)
+        key = np.where(b >> np.uint64(63), ~b, b | np.uint64(1 << 63))
+        himask = np.uint64(0) if shift >= 56 else np.uint64((0xFFFFFFFFFFFFFFFF << (shift + 8)) & 0xFFFFFFFFFFFFFFFF)
+        pre = prefix.numpy().view(np.uint64)[ai[sel]]
+        match = (key & himask) == pre
+        dig = ((key >> np.uint64(shift)) & np.uint64(255)).astype(np.int64)
+        np.add.at(hist, (ai[sel][match], dig[match]), 1)
+        return torch.from_numpy(hist.ravel())
+
+    @staticmethod
+    def kselect_pick(nact, hist, prefix, rank, shift):
+        h = hist.numpy().reshape(nact, 256)
+        pv, rv = prefix.numpy().view(np.uint64), rank.numpy()
+        for a in range(nact):
+            r = int(rv[a])
+            if r < 0:
+                continue
+            b = 255
+            while b > 0 and r >= h[a, b]:
+                r -= int(h[a, b])
+                b -= 1
+            pv[a] |= np.uint64(b) << np.uint64(shift)
+            rv[a] = r
+
+    @staticmethod
+    def kselect_value(nact, prefix):
+        k = prefix.numpy().view(np.uint64)
+        b = np.where(k >> np.uint64(63), k & np.uint64(0x7FFFFFFFFFFFFFFF), ~k)
+        return torch.from_numpy(b.view(np.float64).copy())
+
+    def prune_columns(self, A, thresh):
+        import apps_oracle as AO
+        return self._from_dcsc(AO.prune_column(A.dcsc(), thresh.numpy()))
 
 
 def _free_port():
