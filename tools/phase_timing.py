@@ -1,31 +1,49 @@
-"""Dev tool: host wall time of consecutive phased products, and a check that the inputs are
-left untouched by every call (GPU box)."""
-import os, sys, time
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+#!/usr/bin/env python3
+"""Times the phased R-MAT A^2 product NCALLS times (GPU box tool; diagnostic, not the bench).
+
+    python tools/phase_timing.py SCALE NCALLS
+
+Prints one "call i: <ms> ms nnz=<n>" line per call and, last, the per-kernel stats of the final
+call as a dict literal (tools/gpu_ab.sh parses it). With CBH_LIB=stamps CBH_DIAG=1 the library
+prints per-sub-bin launch times and phase cycle shares to stderr.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+
 import numpy as np
-import combblas_amd as cb
 
-scale = int(sys.argv[1]) if len(sys.argv) > 1 else 22
-ncalls = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-A = cb.rmat(scale, dtype=np.float64)
-ctx = cb.Context(0, torch_allocator=False)
-dA, dB = cb.SpDCCols.from_host(ctx, A), cb.SpDCCols.from_host(ctx, A)
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def same(h):
-    return (np.array_equal(h.ir, A.ir) and np.array_equal(h.cp, A.cp) and np.array_equal(h.jc, A.jc)
-            and np.array_equal(h.num, A.num))
+def main():
+    scale = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    ncalls = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    import combblas_amd as cb
 
-
-for it in range(ncalls):
-    if it == 2:
+    A = cb.rmat(scale, 16, dtype=np.float64)
+    ctx = cb.Context(0, torch_allocator=False)
+    dA = cb.SpDCCols.from_host(ctx, A)
+    dB = cb.SpDCCols.from_host(ctx, A)
+    del A
+    ks = {}
+    for i in range(ncalls):
+        ctx.synchronize()
         ctx.enable_timing(True)
-    t = time.perf_counter()
-    try:
+        ctx.reset_kernel_stats()
+        t0 = time.perf_counter()
         st = cb.PhasedSpGEMM(cb.PlusTimesSRing, dA, dB)
         ctx.synchronize()
-        print(f"call {it}: {time.perf_counter() - t:.3f} s phases={st['phases']} nnz={st['nnz']}", flush=True)
-    except Exception as e:
-        print(f"call {it} failed: {e}", flush=True)
-    print(f"  inputs intact: A {same(dA.to_host())} B {same(dB.to_host())}", flush=True)
-print(ctx.kernel_stats())
+        dt = time.perf_counter() - t0
+        ks = ctx.kernel_stats()
+        ctx.enable_timing(False)
+        print(f"call {i}: {dt * 1e3:.1f} ms nnz={st['nnz']} flops={st['flops']} "
+              f"GFLOP/s={2 * st['flops'] / dt / 1e9:.2f}", flush=True)
+    print(repr(ks), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
