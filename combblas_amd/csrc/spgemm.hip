@@ -16,7 +16,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/combblas_hip.h"
@@ -48,6 +50,11 @@ struct cbh_ctx {
     size_t e0, e1;
     double bytes;
   };
+  // stream-ordered block cache of the default allocator (see dalloc): free blocks by size and
+  // the size of every live block
+  std::multimap<size_t, void*> cache;
+  std::unordered_map<void*, size_t> live;
+  size_t cached_bytes = 0;
   std::vector<hipEvent_t> evpool;
   size_t evused = 0;
   std::vector<Rec> recs;
@@ -95,6 +102,22 @@ static int fail(cbh_ctx* ctx, int code, const std::string& msg) {
   return code;
 }
 
+// Default device allocator: a per-context cache of hipMalloc'd blocks, reused in stream order.
+// Every kernel and copy of a context runs on its one stream, so a block freed by an earlier call
+// can be handed to a later allocation without a sync: the stream finishes the old users first.
+// (hipMallocAsync's default pool, used before, handed overlapping blocks to live allocations on
+// repeated phased products in processes where torch had not initialised HIP first.)
+// Sizes are rounded to 512 B (< 1 MiB) or 2 MiB; a cached block is reused for a request of at
+// least half its size. On OOM the cache is released (after a stream sync) and the request retried.
+static size_t alloc_class(size_t bytes) {
+  return bytes < (size_t(1) << 20) ? (bytes + 511) & ~size_t(511) : (bytes + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+}
+static void release_cache(cbh_ctx* ctx) {
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& kv : ctx->cache) (void)hipFree(kv.second);
+  ctx->cache.clear();
+  ctx->cached_bytes = 0;
+}
 template <class T>
 static int dalloc(cbh_ctx* ctx, T** p, size_t count) {
   *p = nullptr;
@@ -105,17 +128,42 @@ static int dalloc(cbh_ctx* ctx, T** p, size_t count) {
     if (!*p) return fail(ctx, CBH_E_OOM, "allocator callback failed for " + std::to_string(bytes) + " bytes");
     return CBH_OK;
   }
-  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(p), bytes, ctx->stream);
-  if (e != hipSuccess) {
-    *p = nullptr;
-    return fail(ctx, CBH_E_OOM, "hipMallocAsync(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+  const size_t cls = alloc_class(bytes);
+  auto it = ctx->cache.lower_bound(cls);
+  if (it != ctx->cache.end() && it->first / 2 <= cls) {
+    void* q = it->second;
+    ctx->live[q] = it->first;
+    ctx->cached_bytes -= it->first;
+    ctx->cache.erase(it);
+    *p = reinterpret_cast<T*>(q);
+    return CBH_OK;
   }
+  void* q = nullptr;
+  hipError_t e = hipMalloc(&q, cls);
+  if (e != hipSuccess && !ctx->cache.empty()) {
+    (void)hipGetLastError();
+    release_cache(ctx);
+    e = hipMalloc(&q, cls);
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(ctx, CBH_E_OOM, "hipMalloc(" + std::to_string(cls) + "): " + hipGetErrorString(e));
+  }
+  ctx->live[q] = cls;
+  *p = reinterpret_cast<T*>(q);
   return CBH_OK;
 }
 static void dfree(cbh_ctx* ctx, void* p) {
   if (!p) return;
-  if (ctx->release) ctx->release(ctx->alloc_user, p, ctx->stream);
-  else (void)hipFreeAsync(p, ctx->stream);
+  if (ctx->release) {
+    ctx->release(ctx->alloc_user, p, ctx->stream);
+    return;
+  }
+  auto it = ctx->live.find(p);
+  if (it == ctx->live.end()) return;  // not ours (wrapped device arrays are never freed here)
+  ctx->cache.emplace(it->second, p);
+  ctx->cached_bytes += it->second;
+  ctx->live.erase(it);
 }
 
 // RAII holder for scratch allocations of one call.
@@ -996,14 +1044,6 @@ int cbh_ctx_create(int device, cbh_ctx** out) {
       delete c;
       return CBH_E_HIP;
     }
-  {  // keep memory freed by hipFreeAsync mapped in the device pool: phase buffers of ~100 GB
-     // are re-requested every product and re-mapping them costs seconds.
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-      uint64_t thr = UINT64_MAX;
-      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-    }
-  }
   if (hipMalloc(&c->d_err, 16 * sizeof(int)) != hipSuccess || hipMemset(c->d_err, 0, 16 * sizeof(int)) != hipSuccess) {
     delete c;
     return CBH_E_HIP;
@@ -1020,6 +1060,8 @@ int cbh_ctx_destroy(cbh_ctx* ctx) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->evpool) (void)hipEventDestroy(e);
   if (ctx->ws) (void)hipFree(ctx->ws);
+  release_cache(ctx);
+  for (auto& kv : ctx->live) (void)hipFree(kv.first);  // matrices not freed by the caller
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return CBH_OK;
@@ -1315,7 +1357,11 @@ int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh
       if (ctx->ws) (void)hipFree(ctx->ws);
       ctx->ws = nullptr;
       ctx->ws_bytes = 0;
-      CBH_HIP(ctx, hipMalloc(&ctx->ws, (size_t)need));
+      if (hipMalloc(&ctx->ws, (size_t)need) != hipSuccess) {
+        (void)hipGetLastError();
+        release_cache(ctx);
+        CBH_HIP(ctx, hipMalloc(&ctx->ws, (size_t)need));
+      }
       ctx->ws_bytes = need;
     }
     ir = reinterpret_cast<int32_t*>(ctx->ws);

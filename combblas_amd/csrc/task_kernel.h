@@ -155,6 +155,39 @@ __device__ __forceinline__ int64_t gallop64(const int32_t* __restrict__ rows, in
   return lb_rows64<S>(rows, prev, hi, key);
 }
 
+// Segment stop without a dependent chain: the W rows after lo are loaded at once (independent
+// loads, mostly one cache line) and the stop is the count of them below key (rows are sorted).
+// At scale 22 a sub-tile segment holds 1-3 products, so one round trip settles nearly every
+// entry; the galloping search above needed 3-5 dependent round trips. Longer segments fall back
+// to galloping. Also returns the row at the stop (kNoRow past hi), the next sub-tile's cursor row.
+#ifndef CBH_GALLOP
+#define CBH_GALLOP 0  // diagnostic builds: 1 = the galloping search alone (round-1 behaviour)
+#endif
+template <int S, int W>
+__device__ __forceinline__ int64_t probe_stop64(const int32_t* __restrict__ rows, int64_t lo, int64_t hi, int32_t key,
+                                                int32_t& row_at) {
+  if constexpr (!CBH_GALLOP) {
+    int32_t v[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) v[w] = (lo + w < hi) ? rows[(lo + w) * S] : kNoRow;
+    int c = 0;
+    int32_t at = kNoRow;
+#pragma unroll
+    for (int w = W - 1; w >= 0; --w) {
+      c += v[w] < key ? 1 : 0;
+      at = v[w] >= key ? v[w] : at;
+    }
+    if (c < W) {
+      row_at = at;
+      return lo + c;
+    }
+    lo += W;
+  }
+  const int64_t stop = gallop64<S>(rows, lo, hi, key);
+  row_at = stop < hi ? rows[stop * S] : kNoRow;
+  return stop;
+}
+
 template <class SR, int T, int BS, int EMAX, int U, int MODE>
 struct TaskCfg {
   static constexpr bool NUM = MODE == MODE_TNUM;
@@ -355,8 +388,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
             stop = end;
             nx2 = kNoRow;
           } else {
-            stop = gallop64<RS>(rowsA, p + 1, end, hi);
-            nx2 = stop < end ? rowsA[stop * RS] : kNoRow;
+            stop = probe_stop64<RS, 8>(rowsA, p + 1, end, hi, nx2);
           }
         }
         eoff[i] = (int32_t)(stop - p);
@@ -548,6 +580,8 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
           const int64_t pos = o + __popcll(mask & lt) - (s - rstart) + rank;
           if (pos >= out_end || pos >= a.ccap || pos < out_pos) {
             bad |= 1 << 5;
+          } else if ((CBH_ABL & 4) && key != kNoRow - 7) {  // ablation build: no stores
+            bad |= (val == acc_t(12345)) ? 1 << 29 : 0;
           } else {
             a.Cir[pos] = key;
             reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(val);
