@@ -685,6 +685,17 @@ __global__ __launch_bounds__(256) void ablk_kernel(const int64_t* __restrict__ A
   for (int64_t x = blast + 1 + lane; x <= nblk; x += 64) o[x] = (int32_t)len;
 }
 
+// entries of every task that may run chunked (more than the smallest EMAX), else 0
+constexpr int64_t kChunkMin = 256;
+__global__ void chunk_count_kernel(const int32_t* __restrict__ tcol, const int64_t* __restrict__ Bcp, int64_t ntasks,
+                                   int64_t emin, int64_t* __restrict__ cnt) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntasks) return;
+  const int32_t c = tcol[t];
+  const int64_t ne = Bcp[c + 1] - Bcp[c];
+  cnt[t] = ne > emin ? ne : 0;
+}
+
 __global__ void gather_i64_kernel(const int64_t* __restrict__ src, const int64_t* __restrict__ idx, int64_t n,
                                   int64_t* __restrict__ dst) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -705,6 +716,9 @@ struct TSymSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 struct TSymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512, U = 4; };
 struct TNumSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 struct TNumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512, U = 4; };
+static_assert(kChunkMin <= TSymSmall::EMAX && kChunkMin <= TSymLarge::EMAX && kChunkMin <= TNumSmall::EMAX &&
+                  kChunkMin <= TNumLarge::EMAX,
+              "every chunked task needs HBM cursor state");
 // (measured at scale 22: a 1024-thread workgroup with an 8192-slot table, half the sub-tiles,
 // ran 28 % slower than two 512-thread workgroups per CU with 4096 slots)
 template <class SR, class CFG, int MODE>
@@ -803,6 +817,10 @@ struct Plan {  // device arrays describing C = A*B (B's nonzero column slots, ta
   int64_t ablk_w = 0;
   int32_t RB = 1;
   void* Apk = nullptr;        // numeric: A as PkRec records (built by the first numeric call)
+  int64_t* goff = nullptr;    // ntasks + 1: HBM cursor-state offsets of chunked tasks (null: none)
+  int64_t* gcur0 = nullptr;
+  int64_t* gcur1 = nullptr;
+  int64_t* gend = nullptr;
   int64_t total_flops = 0, total_nnz = 0;
 };
 
@@ -828,6 +846,10 @@ static TaskArgs task_args(const cbh_mat* A, const cbh_mat* B, const Plan& P, cbh
   a.ncolA = A->n;
   a.ntasks = P.ntasks;
   a.ccap = INT64_MAX;
+  a.goff = P.goff;
+  a.gcur0 = P.gcur0;
+  a.gcur1 = P.gcur1;
+  a.gend = P.gend;
   return a;
 }
 
@@ -883,6 +905,26 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
     hipLaunchKernelGGL(ablk_kernel, dim3(blocks_for(A->n, 4)), dim3(256), 0, ctx->stream, P.Adense, A->ir, A->n, P.RB,
                        nblk, P.Ablk);
     CBH_HIP(ctx, hipGetLastError());
+  }
+  {  // HBM cursor state for tasks with more B entries than the smallest chunk (EMAX)
+    int64_t* gcnt;
+    CBH_TRY(S.get(&gcnt, nt + 1));
+    CBH_TRY(S.get(&P.goff, nt + 1));
+    hipLaunchKernelGGL(chunk_count_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.tcol, B->cp,
+                       P.ntasks, (int64_t)kChunkMin, gcnt);
+    CBH_HIP(ctx, hipGetLastError());
+    CBH_HIP(ctx, hipMemsetAsync(gcnt + P.ntasks, 0, sizeof(int64_t), ctx->stream));
+    CBH_TRY(exclusive_scan_i64(ctx, S, gcnt, P.goff, P.ntasks + 1));
+    int64_t gtot = 0;
+    CBH_HIP(ctx, hipMemcpyAsync(&gtot, P.goff + P.ntasks, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (gtot > 0) {
+      CBH_TRY(S.get(&P.gcur0, (size_t)gtot));
+      CBH_TRY(S.get(&P.gcur1, (size_t)gtot));
+      CBH_TRY(S.get(&P.gend, (size_t)gtot));
+    } else {
+      P.goff = nullptr;
+    }
   }
   CBH_HIP(ctx, hipMemsetAsync(P.tcnt, 0, sizeof(int64_t) * (nt + 1), ctx->stream));
   BinLists bl;

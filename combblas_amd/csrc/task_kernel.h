@@ -34,6 +34,10 @@
 #ifndef CBH_ABL
 #define CBH_ABL 0
 #endif
+// Planned numeric sub-tile fill, in eighths of the T home slots (the table has T + kGuard slots).
+#ifndef CBH_FILL
+#define CBH_FILL 4
+#endif
 
 namespace cbh {
 
@@ -84,6 +88,13 @@ struct TaskArgs {
   int64_t ccap;
   int* err;
   int64_t nnzA, ncolA, ntasks;
+  // chunked tasks (more than EMAX entries): entry cursors kept in HBM between sub-tiles, double
+  // buffered so that a retried sub-tile restarts from the last committed cursors; goff = per-task
+  // offset into them (null: cursors are re-derived from A every sub-tile)
+  const int64_t* goff;
+  int64_t* gcur0;
+  int64_t* gcur1;
+  int64_t* gend;
 };
 
 // Numeric gather layout: A's row id and value interleaved in one record, so that a product (and
@@ -267,7 +278,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
   bool bitmap = false;
   int64_t R;
   {
-    constexpr int64_t cap = T / 2;
+    constexpr int64_t cap = NUM ? (int64_t)T * CBH_FILL / 8 : T / 2;  // numeric: outputs per sub-tile
     R = (work + cap - 1) / cap;
     if (!NUM) {
       const int64_t Rb = (span + 32ll * T - 1) / (32ll * T);
@@ -287,7 +298,22 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
   // (global atomics with return values) inside a hot loop makes the compiler drain vmcnt there
   int bad = 0;  // bit k: guard site k violated
   // entry state of entries [first, first+cnt): cursor at the first row >= lo
-  auto load_entries = [&](int64_t first, int cnt, int32_t lo, bool lo_is_start) {
+  const bool gstate = chunked && a.goff != nullptr;
+  const int64_t go = gstate ? a.goff[task] : 0;
+  int par = 0;  // which HBM cursor buffer holds the committed cursors
+  auto load_entries = [&](int64_t first, int cnt, int32_t lo, bool lo_is_start, bool from_state) {
+    if (from_state) {  // later sub-tile of a chunked task: cursor and end from HBM, no search
+      const int64_t* gc = par ? a.gcur1 : a.gcur0;
+      for (int i = tid; i < cnt; i += BS) {
+        const int64_t p = e0 + first + i;
+        if constexpr (NUM) escale[i] = reinterpret_cast<const val_t*>(a.Bnum)[p];
+        const int64_t pos = gc[go + first + i], cend = a.gend[go + first + i];
+        epos[i] = pos;
+        eend[i] = cend;
+        enext[i] = pos < cend ? rowsA[pos * RS] : kNoRow;
+      }
+      return;
+    }
     for (int i = tid; i < cnt; i += BS) {
       const int64_t p = e0 + first + i;
       const int32_t k = a.Bir[p];
@@ -330,12 +356,13 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
       }
       epos[i] = pos;
       eend[i] = cend;
+      if (gstate) a.gend[go + first + i] = cend;
       enext[i] = pos < cend ? rowsA[pos * RS] : kNoRow;
     }
   };
 
   if (!chunked) {
-    load_entries(0, (int)ne, tlo, (full & 1) != 0);
+    load_entries(0, (int)ne, tlo, (full & 1) != 0, false);
     __syncthreads();
   }
   CBH_STAMP(0);
@@ -373,7 +400,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
       if (chunked) {
         const int64_t first = (int64_t)ch * EMAX;
         nec = (int)((ne - first) < EMAX ? (ne - first) : EMAX);
-        load_entries(first, nec, lo, lo == tlo && (full & 1));
+        load_entries(first, nec, lo, lo == tlo && (full & 1), gstate && lo != tlo);
         __syncthreads();
       }
       // segment of every entry inside [lo, hi): idle entries (next row >= hi) cost one LDS read
@@ -480,6 +507,11 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         CBH_STAMP(5);
       }
       if (!bitmap && __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+      if (gstate) {  // this chunk's cursors after the sub-tile, into the other buffer
+        int64_t* gn = par ? a.gcur0 : a.gcur1;
+        for (int i = tid; i < nec; i += BS) gn[go + (int64_t)ch * EMAX + i] = qoff[i] + eoff[i + 1];
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the stores land before the barrier
+      }
       if (chunked) __syncthreads();  // entry state is reloaded by the next chunk
     }
     if (!bitmap && __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {  // table could not hold the sub-tile: halve the row range, redo
@@ -493,24 +525,25 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
       continue;
     }
     CBH_STAMP(8);
+    par ^= gstate ? 1 : 0;  // the cursors written during this sub-tile are now the committed ones
     if (!chunked)  // advance the cursors past the committed sub-tile
       for (int i = tid; i < (int)ne; i += BS) {
         epos[i] = qoff[i] + eoff[i + 1];
         enext[i] = enext2[i];
       }
+    CBH_STAMP(9);
     if (bitmap) {
       const int nwords = (int)((tw + 31) >> 5);
       for (int s = tid; s < nwords; s += BS) my_count += __popc(words[s]);
     } else if constexpr (NUM) {
       // rank commit. Slot s holding key x goes to (occupied slots before s) - (s - start of its
       // run) + (keys of its run smaller than x). Wave w owns the 64-aligned slots
-      // [w*SPW, (w+1)*SPW); the start of the run a slot belongs to comes from the occupancy ballot
-      // or, when the run began in an earlier chunk, from the carried last empty slot. Ranks
-      // inside a run come from DPP neighbour compares when the run lies inside the chunk and is
-      // at most kDppMax+1 long; other lanes (runs crossing a chunk edge, long runs of clustered
-      // rows) count the smaller keys of their run with LDS reads.
+      // [w*SPW, (w+1)*SPW), one slot per lane per step; a lane reads the 8 slots on either side of
+      // its own at once, which gives the run's extent and the rank for every run of <= 17 slots
+      // without a dependent chain (runs crossing a 64-slot step included). Longer runs (clustered
+      // rows) walk LDS. Round 1's DPP-neighbour form walked LDS for every run crossing a step
+      // edge or longer than 5 slots: those serial walks were 30 % of the numeric kernel.
       constexpr int SPW = ((TA + NW - 1) / NW + 63) / 64 * 64;
-      constexpr int kDppMax = 4;
       const int sb = wid * SPW < TA ? wid * SPW : TA;
       const int se = sb + SPW < TA ? sb + SPW : TA;
       int wc = 0;
@@ -519,15 +552,8 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         wc += __popcll(__ballot(s < se && keys[s] != kEmpty));
       }
       if (lane == 0) red[NW + wid] = wc;
-      int last_empty = -1;  // last empty slot before the chunk (slot -1 acts as empty)
-      for (int s0 = sb - 64; s0 >= 0; s0 -= 64) {
-        const uint64_t em = __ballot(keys[s0 + lane] == kEmpty);
-        if (em) {
-          last_empty = s0 + 63 - __clzll(em);
-          break;
-        }
-      }
       __syncthreads();
+      CBH_STAMP(10);
       int64_t o = out_pos;
       int tot = 0;
 #pragma unroll
@@ -548,47 +574,52 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         const acc_t val = in ? vals[s] : SR::identity();
         const bool occ = key != kEmpty;
         const uint64_t mask = __ballot(occ);
-        const bool next_occ = s0 + 64 < TA && keys[s0 + 64] != kEmpty;
-        const uint64_t below = ~mask & lt;
-        const uint64_t above = ~mask & ~(lt | (1ull << lane));
-        const int rstart = below ? s0 + 64 - __clzll(below) : last_empty + 1;  // absolute slot
-        const bool right_open = !above && next_occ;  // the run continues into the next chunk
-        const int rend = above ? s0 + __ffsll((long long)above) - 1 : s0 + 64;
-        const int len = rend - rstart;
-        const bool inside = rstart >= s0 && !right_open;
-        const bool dp = occ && inside && len <= kDppMax + 1;
-        const bool lw = occ && !dp;
-        int rank = 0;
-        {
-          int32_t kl = key, kr = key;
-#pragma unroll
-          for (int d = 1; d <= kDppMax; ++d) {
-            if (!__ballot(dp && d < len)) break;
-            kl = __builtin_amdgcn_update_dpp(kEmpty, kl, 0x138, 0xf, 0xf, false);  // wave_shr:1 (lane - d)
-            kr = __builtin_amdgcn_update_dpp(kEmpty, kr, 0x130, 0xf, 0xf, false);  // wave_shl:1 (lane + d)
-            rank += (dp && s - d >= rstart && kl < key) ? 1 : 0;
-            rank += (dp && s + d < rend && kr < key) ? 1 : 0;
-          }
-        }
-        if (lw)
-          for (int x = rstart; x < TA; ++x) {
-            const int32_t kx = keys[x];
-            if (kx == kEmpty) break;
-            rank += kx < key ? 1 : 0;
-          }
         if (occ) {
-          const int64_t pos = o + __popcll(mask & lt) - (s - rstart) + rank;
+          // the kWin slots on either side (independent LDS reads, one latency): the run's extent
+          // around s and the keys of it smaller than key, branch-free while the run stays in the
+          // window (runs of <= 2*kWin+1 slots; the LDS walk below covers longer ones)
+          constexpr int kWin = 8;
+          int32_t kl[kWin], kr[kWin];
+#pragma unroll
+          for (int d = 0; d < kWin; ++d) {
+            const int xl = s - 1 - d, xr = s + 1 + d;
+            kl[d] = keys[xl >= 0 ? xl : 0];
+            kr[d] = keys[xr < TA ? xr : TA - 1];
+            if (xl < 0) kl[d] = kEmpty;
+            if (xr >= TA) kr[d] = kEmpty;
+          }
+          bool lgo = true, rgo = true;
+          int left = 0, right = 0, rank = 0;
+#pragma unroll
+          for (int d = 0; d < kWin; ++d) {
+            lgo = lgo && kl[d] != kEmpty;
+            rgo = rgo && kr[d] != kEmpty;
+            left += lgo ? 1 : 0;
+            right += rgo ? 1 : 0;
+            rank += (lgo && kl[d] < key) ? 1 : 0;
+            rank += (rgo && kr[d] < key) ? 1 : 0;
+          }
+          if (lgo || rgo) {  // the run extends past the window (clustered rows)
+            int rs = s - left, re = s + right + 1;
+            if (lgo)
+              while (rs > 0 && keys[rs - 1] != kEmpty) --rs;
+            if (rgo)
+              while (re < TA && keys[re] != kEmpty) ++re;
+            rank = 0;
+            for (int x = rs; x < re; ++x) rank += keys[x] < key ? 1 : 0;
+            left = s - rs;
+          }
+          const int64_t pos = o + __popcll(mask & lt) - left + rank;
           if (pos >= out_end || pos >= a.ccap || pos < out_pos) {
             bad |= 1 << 5;
           } else if ((CBH_ABL & 4) && key != kNoRow - 7) {  // ablation build: no stores
-            bad |= (val == acc_t(12345)) ? 1 << 29 : 0;
+            bad |= (key == kNoRow - 3 && val == acc_t(12345)) ? 1 << 29 : 0;
           } else {
             a.Cir[pos] = key;
             reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(val);
           }
         }
         o += __popcll(mask);
-        if (~mask) last_empty = s0 + 63 - __clzll(~mask);
       }
       out_pos += tot;
     }
