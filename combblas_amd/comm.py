@@ -7,6 +7,8 @@ subset of its collectives for device tensors.
 
 The reference's MPI calls each helper replaces:
   bcast      MPI_Bcast of the Dcsc arrays            SpParHelper::BCastMatrix, SpParHelper.cpp:581-599
+  ibcast     MPI_Ibcast of the Dcsc arrays           SpParHelper::IBCastMatrix (Mult_AnXBn_Overlap,
+                                                     ParFriends.h:1150-1200)
   allgather  MPI_Allgather of the 4 essentials        SpParHelper::GetSetSizes, SpParHelper.cpp:797-808
   alltoallv  MPI_Alltoall(profile) + MPI_Alltoallv    Mult_AnXBn_SUMMA3D, ParFriends.h:3137-3160
   allreduce  MPI_Allreduce                            (phase planning, statistics)
@@ -53,6 +55,37 @@ def bcast(t: torch.Tensor, root: int, g: Group) -> torch.Tensor:
         return t
     dist.broadcast(t, src=src, group=g.pg)
     return t
+
+
+class _Done:
+    def wait(self):
+        return None
+
+
+class _StagedBcast:
+    """an async broadcast of a host copy; wait() lands it in the device tensor"""
+
+    def __init__(self, work, h, t, copy):
+        self.work, self.h, self.t, self.copy = work, h, t, copy
+
+    def wait(self):
+        self.work.wait()
+        if self.copy:
+            self.t.copy_(self.h)
+
+
+def ibcast(t: torch.Tensor, root: int, g: Group):
+    """Non-blocking broadcast of `t` from group rank `root`; returns a request with wait().
+
+    With RCCL the copy runs on the communicator's stream while the caller's stream keeps
+    computing; wait() makes the caller's current stream wait for it (no host sync)."""
+    if g.size == 1 or t.numel() == 0:
+        return _Done()
+    src = g.global_rank(root)
+    if _staged(t):
+        h = t.cpu() if g.rank == root else torch.empty(t.shape, dtype=t.dtype)
+        return _StagedBcast(dist.broadcast(h, src=src, group=g.pg, async_op=True), h, t, g.rank != root)
+    return dist.broadcast(t, src=src, group=g.pg, async_op=True)
 
 
 def allgather_i64(vals, g: Group, device) -> torch.Tensor:

@@ -12,6 +12,12 @@
                                                layer partial is cut into nlayers column ranges
                                                (divisions3d), exchanged with an alltoallv and the
                                                received pieces merged.
+  Mult_AnXBn_Overlap   ParFriends.h:1110-1235  Synch with the broadcasts of stage i+1 posted (non-blocking, on
+                                               RCCL's stream) before stage i's local multiply.
+  Mult_AnXBn_DoubleBuff ParFriends.h:798-997   A split by columns and B by rows into halves; each stage
+                                               multiplies the halves in turn, so only half of A's and
+                                               B's received blocks are resident at a time (overlapped
+                                               like Overlap).
   PSpGEMM              SpParMat.h:454-467      dispatch on the operand type.
 
 MI355X design: every block is device-resident and every collective moves HBM tensors
@@ -27,7 +33,7 @@ import numpy as np
 import torch
 
 from ._lib import CombBLASHipError
-from .comm import allgather_i64, allreduce_, alltoallv, bcast
+from .comm import allgather_i64, allreduce_, alltoallv, bcast, ibcast
 from .commgrid import ProductGrid
 from .spparmat import SpParMat, SpParMat3D, block_range
 
@@ -98,6 +104,37 @@ def _bcast_block(be, blk, ess, root, group, vdtype):
     return blk if group.rank == root else be.wrap(m, n, cp, jc, ir, num)
 
 
+def _ibcast_block(be, blk, ess, root, group, vdtype):
+    """SpParHelper::IBCastMatrix: the non-blocking form of _bcast_block -> (block, requests)"""
+    m, n, nnz, nzc = ess[root]
+    if group.rank == root:
+        cp, jc, ir, num = be.arrays(blk)
+    else:
+        dev = be.device
+        cp = torch.empty(nzc + 1, dtype=torch.int64, device=dev)
+        jc = torch.empty(nzc, dtype=torch.int64, device=dev)
+        ir = torch.empty(nnz, dtype=torch.int32, device=dev)
+        num = torch.empty(nnz, dtype=vdtype, device=dev)
+    reqs = [ibcast(t, root, group) for t in (cp, jc, ir, num)]
+    return (blk if group.rank == root else be.wrap(m, n, cp, jc, ir, num)), reqs
+
+
+def _rowrange(be, blk, r0, r1):
+    """the entries of a block with rows in [r0, r1), same dimensions (Split of the transposed
+    block in Mult_AnXBn_DoubleBuff, ParFriends.h:822-828, without the two transposes)"""
+    m, n, nnz, nzc = be.dims(blk)
+    cp, jc, ir, num = be.arrays(blk)
+    if nnz == 0 or (r0 <= 0 and r1 >= m):
+        return blk
+    keep = (ir >= r0) & (ir < r1)
+    col_of = torch.repeat_interleave(torch.arange(nzc, device=ir.device), cp[1:] - cp[:-1])
+    cnt = torch.zeros(nzc, dtype=torch.int64, device=ir.device).index_add_(0, col_of, keep.to(torch.int64))
+    nz = cnt > 0
+    cpn = torch.zeros(int(nz.sum().item()) + 1, dtype=torch.int64, device=ir.device)
+    cpn[1:] = torch.cumsum(cnt[nz], 0)
+    return be.wrap(m, n, cpn, jc[nz].contiguous(), ir[keep].contiguous(), num[keep].contiguous())
+
+
 def _check_dims(A, B):
     if A.getncol() != B.getnrow():
         raise CombBLASHipError(DIMMISMATCH, f"Can not multiply, dimensions does not match {A.getncol()} != {B.getnrow()}")
@@ -165,6 +202,90 @@ def Mult_AnXBn_Synch(SR, A: SpParMat, B: SpParMat, clearA=False, clearB=False) -
     for i in range(stages):
         Ai = _bcast_block(be, A.seq, Aess, i, grid.rowWorld, vdtype)
         Bi = _bcast_block(be, B.seq, Bess, i, grid.colWorld, vdtype)
+        tomerge.append(be.multiply(SR, Ai, Bi))
+        if i != Aself:
+            be.free(Ai)
+        if i != Bself:
+            be.free(Bi)
+    C = _merge(be, SR, tomerge, m, n, vdtype)
+    if clearA:
+        be.free(A.seq)
+    if clearB:
+        be.free(B.seq)
+    return SpParMat(C, grid, be, A.m, B.n, A.row_off, B.col_off)
+
+
+def Mult_AnXBn_Overlap(SR, A: SpParMat, B: SpParMat, clearA=False, clearB=False) -> SpParMat:
+    """2D SUMMA with communication overlapped (ParFriends.h:1110-1235): the broadcasts of stage
+    i+1 are posted before stage i's local multiply, so RCCL moves the next blocks over xGMI while
+    the gfx950 kernels run. Same result as Mult_AnXBn_Synch."""
+    _check_dims(A, B)
+    grid, stages = ProductGrid(A.commGrid, B.commGrid)
+    be = A.backend
+    vdtype = be.value_dtype(A.seq)
+    Aess = _essentials(be, A.seq, grid.rowWorld)
+    Bess = _essentials(be, B.seq, grid.colWorld)
+    Aself, Bself = grid.GetRankInProcRow(), grid.GetRankInProcCol()
+    m, n = be.dims(A.seq)[0], be.dims(B.seq)[1]
+
+    def post(i):
+        return (_ibcast_block(be, A.seq, Aess, i, grid.rowWorld, vdtype),
+                _ibcast_block(be, B.seq, Bess, i, grid.colWorld, vdtype))
+
+    tomerge = []
+    nxt = post(0)
+    for i in range(stages):
+        (Ai, ra), (Bi, rb) = nxt
+        for r in ra + rb:
+            r.wait()
+        if i + 1 < stages:
+            nxt = post(i + 1)
+        tomerge.append(be.multiply(SR, Ai, Bi))
+        if i != Aself:
+            be.free(Ai)
+        if i != Bself:
+            be.free(Bi)
+    C = _merge(be, SR, tomerge, m, n, vdtype)
+    if clearA:
+        be.free(A.seq)
+    if clearB:
+        be.free(B.seq)
+    return SpParMat(C, grid, be, A.m, B.n, A.row_off, B.col_off)
+
+
+def Mult_AnXBn_DoubleBuff(SR, A: SpParMat, B: SpParMat, clearA=False, clearB=False) -> SpParMat:
+    """ParFriends.h:798-997: A's local block is split by columns and B's by rows at the same
+    point (A1*B1 + A2*B2 = A*B), and every stage multiplies the two halves in turn, so the
+    received buffers hold half blocks. The 2*stages partials are merged once. The next half's
+    broadcasts are posted before the current half is multiplied (as in Mult_AnXBn_Overlap)."""
+    _check_dims(A, B)
+    grid, stages = ProductGrid(A.commGrid, B.commGrid)
+    be = A.backend
+    vdtype = be.value_dtype(A.seq)
+    m, n = be.dims(A.seq)[0], be.dims(B.seq)[1]
+    # SpDCCols::Split at ncol/2 (SpDCCols.cpp): every rank splits its own A block's columns and
+    # its own B block's rows; at stage i both come from blocks of inner dimension k_i, so the
+    # halves broadcast in one step always pair up
+    ka, kb = be.dims(A.seq)[1], be.dims(B.seq)[0]
+    halves = [(_colslice(be, A.seq, 0, ka // 2), _rowrange(be, B.seq, 0, kb // 2)),
+              (_colslice(be, A.seq, ka // 2, ka), _rowrange(be, B.seq, kb // 2, kb))]
+    ess = [(_essentials(be, a, grid.rowWorld), _essentials(be, b, grid.colWorld)) for a, b in halves]
+    Aself, Bself = grid.GetRankInProcRow(), grid.GetRankInProcCol()
+    order = [(i, x) for i in range(stages) for x in range(2)]
+
+    def post(j):
+        i, x = order[j]
+        (a, b), (ea, eb) = halves[x], ess[x]
+        return (_ibcast_block(be, a, ea, i, grid.rowWorld, vdtype), _ibcast_block(be, b, eb, i, grid.colWorld, vdtype))
+
+    tomerge = []
+    nxt = post(0)
+    for j, (i, x) in enumerate(order):
+        (Ai, ra), (Bi, rb) = nxt
+        for r in ra + rb:
+            r.wait()
+        if j + 1 < len(order):
+            nxt = post(j + 1)
         tomerge.append(be.multiply(SR, Ai, Bi))
         if i != Aself:
             be.free(Ai)

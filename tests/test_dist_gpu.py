@@ -42,6 +42,10 @@ def _gpu_worker(rank, world, scale, tag, mode, phases, budget, layers):
         dB = SpParMat.distribute(h, grid, be)
         if mode == "synch":
             C = pf.Mult_AnXBn_Synch(SR, dA, dB)
+        elif mode == "overlap":
+            C = pf.Mult_AnXBn_Overlap(SR, dA, dB)
+        elif mode == "doublebuff":
+            C = pf.Mult_AnXBn_DoubleBuff(SR, dA, dB)
         else:
             C = pf.MemEfficientSpGEMM(SR, dA, dB, phases=phases, perProcessMemory=budget)
     g = C.gather_host()
@@ -64,6 +68,13 @@ def _check(res, golden):
 def test_gpu_summa2d_2x2(golden, tag):
     res = run_world(_gpu_worker, 4, 12, tag, "synch", 1, 0, 1, timeout=150)
     _check(res, golden["digests"][f"rmat12_{tag}"])
+
+
+@pytest.mark.parametrize("mode", ["overlap", "doublebuff"])
+def test_gpu_summa2d_overlap_doublebuff(golden, mode):
+    """Mult_AnXBn_Overlap / Mult_AnXBn_DoubleBuff (non-blocking stage broadcasts) on the device"""
+    res = run_world(_gpu_worker, 4, 12, "pt_i64", mode, 1, 0, 1, timeout=150)
+    _check(res, golden["digests"]["rmat12_pt_i64"])
 
 
 def test_gpu_summa2d_phased(golden):
