@@ -85,6 +85,11 @@ SIGNATURES = {
     "cbh_kselect_value": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "cbh_prune_columns": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_tuples_to_dcsc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                          ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_dcsc_to_tuples": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p]),
     "cbh_rmat_edges": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                       ctypes.c_void_p]),
     "cbh_edges_to_csc": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
@@ -99,6 +104,7 @@ ERRORS = {3001: "GRIDMISMATCH", 3002: "DIMMISMATCH", 3005: "MATRIXALIAS", 4001: 
 CBH_KEEP_EMPTY_COLS = 0x2
 CBH_MASK_PATTERN = 0x4
 CBH_PHASE_CHECKSUM = 0x100
+CBH_TUPLES_DROP_LOOPS = 0x1
 
 
 class CombBLASHipError(RuntimeError):

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcombblas_hip.so")
 SOURCES = ["spgemm.hip", "rmat.cpp"]
-HEADERS = ["semiring.h", "tile_kernel.h", "task_kernel.h", "apps.h", "host_util.h", os.path.join("..", "..", "include", "combblas_hip.h")]
+HEADERS = ["semiring.h", "tile_kernel.h", "task_kernel.h", "apps.h", "convert.h", "host_util.h", os.path.join("..", "..", "include", "combblas_hip.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("CBH_OFFLOAD_ARCH", "gfx950")
 

@@ -25,6 +25,7 @@
 #include "semiring.h"
 #include "task_kernel.h"
 #include "apps.h"
+#include "convert.h"
 
 using namespace cbh;
 
@@ -1807,3 +1808,104 @@ int cbh_prune_columns(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, cbh_
 
 }  // extern "C"
 
+// ============================================================================ format conversions
+// SURVEY.md §8(f)3 (kernels in convert.h): the SpTuples -> SpDCCols build and back, on the device.
+template <class V>
+static void launch_tuple_reduce(cbh_ctx* ctx, const uint64_t* key, const int64_t* perm, const int64_t* head,
+                                const int64_t* pos, int64_t nnz, int64_t m, const void* vin, int32_t* ir, uint64_t* ukey,
+                                void* vout) {
+  hipLaunchKernelGGL(tuple_reduce_kernel<V>, dim3(blocks_for(nnz, 256)), dim3(256), 0, ctx->stream, key, perm, head, pos,
+                     nnz, m, reinterpret_cast<const V*>(vin), ir, ukey, reinterpret_cast<V*>(vout));
+}
+
+extern "C" int cbh_tuples_to_dcsc(cbh_ctx* ctx, int64_t m, int64_t n, int64_t nnz, const int32_t* rows,
+                                  const int64_t* cols, const void* vals, cbh_dtype dtype, uint32_t flags,
+                                  cbh_mat** out) {
+  if (!ctx || !out || nnz < 0 || m < 0 || n < 0 || dtype_size(dtype) == 0 || (nnz > 0 && (!rows || !cols || !vals)))
+    return fail(ctx, CBH_E_ARG, "bad tuples_to_dcsc arguments");
+  *out = nullptr;
+  if (m > INT32_MAX) return fail(ctx, CBH_E_DIMMISMATCH, "local row count exceeds 32-bit row ids");
+  if (nnz > INT32_MAX) return fail(ctx, CBH_E_ARG, "at most 2^31-1 tuples per conversion");
+  if (m > 0 && n > (int64_t)(UINT64_MAX / 2 / (uint64_t)m)) return fail(ctx, CBH_E_ARG, "m*n exceeds 63-bit keys");
+  if (nnz == 0 || m == 0 || n == 0) return empty_result(ctx, m, n, dtype, out);
+  Scratch S(ctx);
+  uint64_t *k0, *k1, *ukey;
+  int64_t *i0, *i1, *head, *pos, *flag, *cpos;
+  int32_t* ir;
+  char* vout;
+  const size_t vs = dtype_size(dtype);
+  CBH_TRY(S.get(&k0, nnz));
+  CBH_TRY(S.get(&k1, nnz));
+  CBH_TRY(S.get(&i0, nnz));
+  CBH_TRY(S.get(&i1, nnz));
+  CBH_TRY(S.get(&head, nnz + 1));
+  CBH_TRY(S.get(&pos, nnz + 1));
+  hipLaunchKernelGGL(tuple_keys_kernel, dim3(blocks_for(nnz, 256)), dim3(256), 0, ctx->stream, rows, cols, nnz, m, n,
+                     k0, i0, ctx->d_err);
+  CBH_HIP(ctx, hipGetLastError());
+  int end_bit = 1;
+  while (end_bit < 64 && (((uint64_t)m * (uint64_t)n - 1) >> end_bit) != 0) ++end_bit;
+  size_t tmp = 0;
+  CBH_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, k0, k1, i0, i1, (int)nnz, 0, end_bit, ctx->stream));
+  char* t;
+  CBH_TRY(S.get(&t, tmp));
+  CBH_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(t, tmp, k0, k1, i0, i1, (int)nnz, 0, end_bit, ctx->stream));
+  hipLaunchKernelGGL(tuple_heads_kernel, dim3(blocks_for(nnz, 256)), dim3(256), 0, ctx->stream, k1, nnz, m,
+                     (flags & CBH_TUPLES_DROP_LOOPS) != 0, head);
+  CBH_HIP(ctx, hipMemsetAsync(head + nnz, 0, sizeof(int64_t), ctx->stream));
+  CBH_TRY(exclusive_scan_i64(ctx, S, head, pos, nnz + 1));
+  int64_t u = 0;
+  CBH_HIP(ctx, hipMemcpyAsync(&u, pos + nnz, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (u == 0) {
+    CBH_TRY(check_err(ctx));
+    return empty_result(ctx, m, n, dtype, out);
+  }
+  CBH_TRY(S.get(&ir, u));
+  CBH_TRY(S.get(&ukey, u));
+  CBH_TRY(S.get(&vout, u * vs));
+  CBH_TRY(S.get(&flag, u + 1));
+  CBH_TRY(S.get(&cpos, u + 1));
+  switch (dtype) {
+    case CBH_F64: launch_tuple_reduce<double>(ctx, k1, i1, head, pos, nnz, m, vals, ir, ukey, vout); break;
+    case CBH_I64: launch_tuple_reduce<int64_t>(ctx, k1, i1, head, pos, nnz, m, vals, ir, ukey, vout); break;
+    case CBH_F32: launch_tuple_reduce<float>(ctx, k1, i1, head, pos, nnz, m, vals, ir, ukey, vout); break;
+    case CBH_I32: launch_tuple_reduce<int32_t>(ctx, k1, i1, head, pos, nnz, m, vals, ir, ukey, vout); break;
+    default: launch_tuple_reduce<uint8_t>(ctx, k1, i1, head, pos, nnz, m, vals, ir, ukey, vout); break;
+  }
+  CBH_HIP(ctx, hipGetLastError());
+  hipLaunchKernelGGL(col_heads_kernel, dim3(blocks_for(u, 256)), dim3(256), 0, ctx->stream, ukey, u, m, flag);
+  CBH_HIP(ctx, hipMemsetAsync(flag + u, 0, sizeof(int64_t), ctx->stream));
+  CBH_TRY(exclusive_scan_i64(ctx, S, flag, cpos, u + 1));
+  int64_t nzc = 0;
+  CBH_HIP(ctx, hipMemcpyAsync(&nzc, cpos + u, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  cbh_mat* M;
+  CBH_TRY(new_mat(ctx, m, n, u, nzc, dtype, &M));
+  hipLaunchKernelGGL(col_fill_kernel, dim3(blocks_for(u, 256)), dim3(256), 0, ctx->stream, ukey, flag, cpos, u, m, M->jc,
+                     M->cp);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(M->cp + nzc, &u, sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(M->ir, ir, sizeof(int32_t) * u, hipMemcpyDeviceToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(M->num, vout, vs * u, hipMemcpyDeviceToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  int rc = e == hipSuccess ? check_err(ctx) : fail(ctx, CBH_E_HIP, std::string("tuples_to_dcsc: ") + hipGetErrorString(e));
+  if (rc != CBH_OK) {
+    cbh_mat_free(ctx, M);
+    return rc;
+  }
+  *out = M;
+  return CBH_OK;
+}
+
+extern "C" int cbh_dcsc_to_tuples(cbh_ctx* ctx, const cbh_mat* M, int32_t* rows, int64_t* cols, void* vals) {
+  if (!ctx || !M || (M->nnz > 0 && (!rows || !cols || !vals))) return fail(ctx, CBH_E_ARG, "bad dcsc_to_tuples arguments");
+  if (M->nnz == 0) return CBH_OK;
+  CBH_HIP(ctx, hipMemcpyAsync(rows, M->ir, sizeof(int32_t) * M->nnz, hipMemcpyDeviceToDevice, ctx->stream));
+  CBH_HIP(ctx, hipMemcpyAsync(vals, M->num, dtype_size(M->dtype) * M->nnz, hipMemcpyDeviceToDevice, ctx->stream));
+  hipLaunchKernelGGL(expand_cols_kernel, dim3(blocks_for(M->nzc, 4)), dim3(256), 0, ctx->stream, M->jc, M->cp, M->nzc,
+                     cols);
+  CBH_HIP(ctx, hipGetLastError());
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return CBH_OK;
+}

@@ -198,6 +198,35 @@ class SpDCCols:
         check(lib().cbh_mat_wrap_device(ctx.h, ctypes.byref(s), code, ctypes.byref(h)), ctx.h)
         return SpDCCols(ctx, h, keepalive=(cp, jc, ir, num))
 
+    @staticmethod
+    def from_tuples(ctx: Context, m, n, rows, cols, vals, removeloops=False):
+        """SpDCCols(SpTuples) from device COO tensors (rows int32, cols int64, vals) in any order,
+        duplicates combined (sum; OR for bool) -- SpTuples.cpp:70-118 + SpDCCols.cpp:109-183 on
+        the device (cbh_tuples_to_dcsc)."""
+        torch = _torch()
+        code = {torch.float64: 0, torch.int64: 1, torch.uint8: 2, torch.bool: 2, torch.float32: 3,
+                torch.int32: 4}[vals.dtype]
+        rows = rows.to(torch.int32).contiguous()
+        cols = cols.to(torch.int64).contiguous()
+        vals = (vals.to(torch.uint8) if vals.dtype == torch.bool else vals).contiguous()
+        h = ctypes.c_void_p()
+        check(lib().cbh_tuples_to_dcsc(ctx.h, int(m), int(n), rows.numel(), ctypes.c_void_p(rows.data_ptr()),
+                                       ctypes.c_void_p(cols.data_ptr()), ctypes.c_void_p(vals.data_ptr()), code,
+                                       _lib.CBH_TUPLES_DROP_LOOPS if removeloops else 0, ctypes.byref(h)), ctx.h)
+        return SpDCCols(ctx, h)
+
+    def to_tuples(self):
+        """SpTuples(const SpDCCols&): (rows int32, cols int64, vals) device tensors, column-sorted"""
+        torch = _torch()
+        dev = self.ctx.tdevice or torch.device("cuda", self.ctx.device)
+        rows = torch.empty(self.nnz, dtype=torch.int32, device=dev)
+        cols = torch.empty(self.nnz, dtype=torch.int64, device=dev)
+        vals = torch.empty(self.nnz, dtype=torch_dtype(self.dtype_code), device=dev)
+        torch.cuda.synchronize(dev)
+        check(lib().cbh_dcsc_to_tuples(self.ctx.h, self.h, ctypes.c_void_p(rows.data_ptr()),
+                                       ctypes.c_void_p(cols.data_ptr()), ctypes.c_void_p(vals.data_ptr())), self.ctx.h)
+        return rows, cols, vals
+
     def tensors(self):
         """(cp, jc, ir, num) as torch tensors viewing device memory (no copy)."""
         if self._keep is not None:

@@ -195,6 +195,19 @@ int cbh_kselect_pick(cbh_ctx* ctx, int64_t nactive, const uint32_t* hist, uint64
 int cbh_kselect_value(cbh_ctx* ctx, int64_t nactive, const uint64_t* prefix, double* out);
 int cbh_prune_columns(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, cbh_mat** C);
 
+/* ---------------------------------------------------------------- format conversions (device)
+ *   cbh_tuples_to_dcsc  device COO (rows, cols, vals; any order, duplicates allowed) -> a DCSC block:
+ *                       SpTuples::SortColBased + duplicate combination (sum; OR for bool, as
+ *                       SpTuples(edges) SpTuples.cpp:70-118 and RemoveDuplicates :271-300 with the
+ *                       default SumOp) + SpDCCols(const SpTuples&) SpDCCols.cpp:109-183.
+ *                       CBH_TUPLES_DROP_LOOPS removes row == col entries (removeloops). nnz < 2^31.
+ *   cbh_dcsc_to_tuples  a DCSC block -> device COO, column-sorted (SpTuples(const SpDCCols&),
+ *                       SpTuples.cpp:181-200); buffers of M's nnz entries. */
+#define CBH_TUPLES_DROP_LOOPS 0x1u
+int cbh_tuples_to_dcsc(cbh_ctx* ctx, int64_t m, int64_t n, int64_t nnz, const int32_t* rows, const int64_t* cols,
+                       const void* vals, cbh_dtype dtype, uint32_t flags, cbh_mat** out);
+int cbh_dcsc_to_tuples(cbh_ctx* ctx, const cbh_mat* M, int32_t* rows, int64_t* cols, void* vals);
+
 /* ---------------------------------------------------------------- inputs (host side) */
 int cbh_rmat_edges(int scale, uint64_t userseed, int64_t start_edge, int64_t end_edge, int64_t* src,
                    int64_t* dst);
