@@ -34,7 +34,7 @@ sys.path.insert(0, HERE)
 METRIC = "semiring GFLOP/s for R-MAT A² SpGEMM at 1/2/4/8 GPUs; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
 DOMINANT = "num_large"
-DOMINANT_KERNEL = "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 4, 1>"
+DOMINANT_KERNEL = "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 8, 1>"
 
 
 def parse():

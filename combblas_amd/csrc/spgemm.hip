@@ -714,9 +714,15 @@ __global__ void add_i64_kernel(const int64_t* __restrict__ x, const int64_t* __r
 
 // task-kernel configurations: T slots, BS threads, EMAX entries per chunk, U products per thread
 struct TSymSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
-struct TSymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512, U = 4; };
+#ifndef CBH_SYM_U
+#define CBH_SYM_U 8
+#endif
+#ifndef CBH_NUM_U
+#define CBH_NUM_U 8
+#endif
+struct TSymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512, U = CBH_SYM_U; };
 struct TNumSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
-struct TNumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512, U = 4; };
+struct TNumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512, U = CBH_NUM_U; };
 static_assert(kChunkMin <= TSymSmall::EMAX && kChunkMin <= TSymLarge::EMAX && kChunkMin <= TNumSmall::EMAX &&
                   kChunkMin <= TNumLarge::EMAX,
               "every chunked task needs HBM cursor state");

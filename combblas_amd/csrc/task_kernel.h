@@ -207,6 +207,9 @@ struct TaskCfg {
   static constexpr int TA = NUM ? T + kGuard : T;  // slots (symbolic: 32-bit words, keys or bitmap)
   static constexpr int NW = BS / 64;
   static constexpr int WIN = U * BS;
+  // owner map entries are entry indices (< EMAX): 16 bits leave LDS room for larger windows
+  using own_t = int16_t;
+  static_assert(EMAX < 32768, "owner map entries are 16-bit");
   static constexpr size_t al(size_t x) { return (x + 15) & ~size_t(15); }
   static constexpr size_t o_keys = 0;
   static constexpr size_t o_vals = al(o_keys + sizeof(int32_t) * TA);
@@ -218,7 +221,7 @@ struct TaskCfg {
   static constexpr size_t o_next2 = al(o_next + sizeof(int32_t) * EMAX);
   static constexpr size_t o_off = al(o_next2 + sizeof(int32_t) * EMAX);
   static constexpr size_t o_own = al(o_off + sizeof(int32_t) * (EMAX + 1));
-  static constexpr size_t o_red = al(o_own + sizeof(int32_t) * WIN);
+  static constexpr size_t o_red = al(o_own + sizeof(own_t) * WIN);
   static constexpr size_t bytes = al(o_red + sizeof(int32_t) * (2 * NW + 4));
 };
 
@@ -242,7 +245,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
   int32_t* enext = reinterpret_cast<int32_t*>(smem + C::o_next);  // row at the cursor (kNoRow: done)
   int32_t* enext2 = reinterpret_cast<int32_t*>(smem + C::o_next2);  // row at the sub-tile's stop
   int32_t* eoff = reinterpret_cast<int32_t*>(smem + C::o_off);
-  int32_t* own = reinterpret_cast<int32_t*>(smem + C::o_own);
+  typename C::own_t* own = reinterpret_cast<typename C::own_t*>(smem + C::o_own);
   int32_t* red = reinterpret_cast<int32_t*>(smem + C::o_red);
   __shared__ int32_t s_ovf;  // overflow flag of the current sub-tile (LDS; read after barriers)
 
@@ -430,11 +433,11 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
       int carry = -1;  // owner of the product just before the window
       for (int w0 = 0; w0 < P; w0 += WIN) {
         const int wn = (P - w0) < WIN ? (P - w0) : WIN;
-        for (int x = tid; x < WIN; x += BS) own[x] = (x == 0) ? carry : -1;
+        for (int x = tid; x < WIN; x += BS) own[x] = (typename C::own_t)((x == 0) ? carry : -1);
         __syncthreads();
         for (int i = tid; i < nec; i += BS) {
           const int s0 = eoff[i];
-          if (s0 >= w0 && s0 < w0 + wn && eoff[i + 1] > s0) own[s0 - w0] = i;
+          if (s0 >= w0 && s0 < w0 + wn && eoff[i + 1] > s0) own[s0 - w0] = (typename C::own_t)i;
         }
         __syncthreads();
         block_max_scan<BS, WIN>(own, red);

@@ -162,8 +162,8 @@ __device__ __forceinline__ void block_scan_excl(int32_t* x, int n, int* red) {
 }
 
 // In-place inclusive prefix-max of own[0..WIN) (LDS); each thread owns E = WIN/BS contiguous slots.
-template <int BS, int WIN>
-__device__ __forceinline__ void block_max_scan(int32_t* own, int* red) {
+template <int BS, int WIN, class OT = int32_t>
+__device__ __forceinline__ void block_max_scan(OT* own, int* red) {
   constexpr int E = WIN / BS, NW = BS / 64;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   int v[E];
@@ -190,7 +190,7 @@ __device__ __forceinline__ void block_max_scan(int32_t* own, int* red) {
     if (w < wid) wpre = red[w] > wpre ? red[w] : wpre;
   const int carry = ex > wpre ? ex : wpre;
 #pragma unroll
-  for (int e = 0; e < E; ++e) own[tid * E + e] = v[e] > carry ? v[e] : carry;
+  for (int e = 0; e < E; ++e) own[tid * E + e] = (OT)(v[e] > carry ? v[e] : carry);
   __syncthreads();
 }
 
