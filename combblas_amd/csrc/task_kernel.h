@@ -35,6 +35,12 @@
 #define CBH_ABL 0
 #endif
 // Planned numeric sub-tile fill, in eighths of the T home slots (the table has T + kGuard slots).
+#ifndef CBH_KWIN
+#define CBH_KWIN 8  // numeric commit: neighbour slots read on either side of an occupied slot
+#endif
+#ifndef CBH_RBC
+#define CBH_RBC 0  // numeric insert: 1 = read the slot before the CAS (diagnostic A/B)
+#endif
 #ifndef CBH_FILL
 #define CBH_FILL 4
 #endif
@@ -483,7 +489,13 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
             uint32_t s = (uint32_t)(((uint64_t)d * scale) >> 32);
             bool ok = false;
             for (int probe = 0; probe < kPmax && s < (uint32_t)TA; ++probe, ++s) {
+#if CBH_RBC
+              const int32_t k0 = keys[s];
+              if (k0 != kEmpty && k0 != r[u]) continue;
+              const int32_t k = k0 == kEmpty ? atomicCAS(&keys[s], kEmpty, r[u]) : k0;
+#else
               const int32_t k = atomicCAS(&keys[s], kEmpty, r[u]);
+#endif
               if (k == kEmpty || k == r[u]) {
                 SR::lds_acc(&vals[s], vv);
                 ok = true;
@@ -581,7 +593,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
           // the kWin slots on either side (independent LDS reads, one latency): the run's extent
           // around s and the keys of it smaller than key, branch-free while the run stays in the
           // window (runs of <= 2*kWin+1 slots; the LDS walk below covers longer ones)
-          constexpr int kWin = 8;
+          constexpr int kWin = CBH_KWIN;
           int32_t kl[kWin], kr[kWin];
 #pragma unroll
           for (int d = 0; d < kWin; ++d) {
