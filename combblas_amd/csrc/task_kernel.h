@@ -41,6 +41,9 @@
 #ifndef CBH_RBC
 #define CBH_RBC 0  // numeric insert: 1 = read the slot before the CAS (diagnostic A/B)
 #endif
+#ifndef CBH_CQ
+#define CBH_CQ 1  // numeric commit: 1 = per-wave queue of occupied slots, committed 64 at a time
+#endif
 #ifndef CBH_FILL
 #define CBH_FILL 4
 #endif
@@ -578,6 +581,87 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         tot += rr;
       }
       const uint64_t lt = (1ull << lane) - 1ull;
+      // slot s (occupied, key, val) of the wave's occupied slots in slot order goes to
+      // base - (s - start of its run) + (keys of its run smaller than key)
+      auto emit = [&](int s, int32_t key, acc_t val, int64_t base) {
+        // the kWin slots on either side (independent LDS reads, one latency): the run's extent
+        // around s and the keys of it smaller than key, branch-free while the run stays in the
+        // window (runs of <= 2*kWin+1 slots; the LDS walk below covers longer ones)
+        constexpr int kWin = CBH_KWIN;
+        int32_t kl[kWin], kr[kWin];
+#pragma unroll
+        for (int d = 0; d < kWin; ++d) {
+          const int xl = s - 1 - d, xr = s + 1 + d;
+          kl[d] = keys[xl >= 0 ? xl : 0];
+          kr[d] = keys[xr < TA ? xr : TA - 1];
+          if (xl < 0) kl[d] = kEmpty;
+          if (xr >= TA) kr[d] = kEmpty;
+        }
+        bool lgo = true, rgo = true;
+        int left = 0, right = 0, rank = 0;
+#pragma unroll
+        for (int d = 0; d < kWin; ++d) {
+          lgo = lgo && kl[d] != kEmpty;
+          rgo = rgo && kr[d] != kEmpty;
+          left += lgo ? 1 : 0;
+          right += rgo ? 1 : 0;
+          rank += (lgo && kl[d] < key) ? 1 : 0;
+          rank += (rgo && kr[d] < key) ? 1 : 0;
+        }
+        if (lgo || rgo) {  // the run extends past the window (clustered rows)
+          int rs = s - left, re = s + right + 1;
+          if (lgo)
+            while (rs > 0 && keys[rs - 1] != kEmpty) --rs;
+          if (rgo)
+            while (re < TA && keys[re] != kEmpty) ++re;
+          rank = 0;
+          for (int x = rs; x < re; ++x) rank += keys[x] < key ? 1 : 0;
+          left = s - rs;
+        }
+        const int64_t pos = base - left + rank;
+        if (pos >= out_end || pos >= a.ccap || pos < out_pos) {
+          bad |= 1 << 5;
+        } else if ((CBH_ABL & 4) && key != kNoRow - 7) {  // ablation build: no stores
+          bad |= (key == kNoRow - 3 && val == acc_t(12345)) ? 1 << 29 : 0;
+        } else {
+          a.Cir[pos] = key;
+          reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(val);
+        }
+      };
+#if CBH_CQ
+      // occupied slots are queued per wave (slot order, in enext2: dead until the next sub-tile's
+      // entries pass) and committed 64 at a time, so the window reads run on full waves instead of
+      // on the ~half of the lanes whose slot is occupied
+      static_assert(NW * 128 * sizeof(int16_t) <= EMAX * sizeof(int32_t) && TA < 32768, "commit queue");
+      int16_t* cq = reinterpret_cast<int16_t*>(enext2) + wid * 128;
+      int qn = 0;  // queued slots (wave-uniform)
+#if CBH_ABL & 1  // ablation build: no commit loop
+      for (int s0 = se; s0 < se; s0 += 64) {
+#else
+      for (int s0 = sb; s0 < se; s0 += 64) {
+#endif
+        const int s = s0 + lane;
+        const bool occ = s < se && keys[s] != kEmpty;
+        const uint64_t mask = __ballot(occ);
+        if (occ) cq[qn + __popcll(mask & lt)] = (int16_t)s;
+        qn += __popcll(mask);
+        __builtin_amdgcn_wave_barrier();
+        if (qn >= 64) {
+          const int sq = cq[lane];
+          emit(sq, keys[sq], vals[sq], o + lane);
+          o += 64;
+          qn -= 64;
+          const int16_t rest = lane < qn ? cq[64 + lane] : (int16_t)0;
+          __builtin_amdgcn_wave_barrier();
+          if (lane < qn) cq[lane] = rest;
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+      if (lane < qn) {
+        const int sq = cq[lane];
+        emit(sq, keys[sq], vals[sq], o + lane);
+      }
+#else
 #if CBH_ABL & 1  // ablation build: no commit loop
       for (int s0 = se; s0 < se; s0 += 64) {
 #else
@@ -589,53 +673,10 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         const acc_t val = in ? vals[s] : SR::identity();
         const bool occ = key != kEmpty;
         const uint64_t mask = __ballot(occ);
-        if (occ) {
-          // the kWin slots on either side (independent LDS reads, one latency): the run's extent
-          // around s and the keys of it smaller than key, branch-free while the run stays in the
-          // window (runs of <= 2*kWin+1 slots; the LDS walk below covers longer ones)
-          constexpr int kWin = CBH_KWIN;
-          int32_t kl[kWin], kr[kWin];
-#pragma unroll
-          for (int d = 0; d < kWin; ++d) {
-            const int xl = s - 1 - d, xr = s + 1 + d;
-            kl[d] = keys[xl >= 0 ? xl : 0];
-            kr[d] = keys[xr < TA ? xr : TA - 1];
-            if (xl < 0) kl[d] = kEmpty;
-            if (xr >= TA) kr[d] = kEmpty;
-          }
-          bool lgo = true, rgo = true;
-          int left = 0, right = 0, rank = 0;
-#pragma unroll
-          for (int d = 0; d < kWin; ++d) {
-            lgo = lgo && kl[d] != kEmpty;
-            rgo = rgo && kr[d] != kEmpty;
-            left += lgo ? 1 : 0;
-            right += rgo ? 1 : 0;
-            rank += (lgo && kl[d] < key) ? 1 : 0;
-            rank += (rgo && kr[d] < key) ? 1 : 0;
-          }
-          if (lgo || rgo) {  // the run extends past the window (clustered rows)
-            int rs = s - left, re = s + right + 1;
-            if (lgo)
-              while (rs > 0 && keys[rs - 1] != kEmpty) --rs;
-            if (rgo)
-              while (re < TA && keys[re] != kEmpty) ++re;
-            rank = 0;
-            for (int x = rs; x < re; ++x) rank += keys[x] < key ? 1 : 0;
-            left = s - rs;
-          }
-          const int64_t pos = o + __popcll(mask & lt) - left + rank;
-          if (pos >= out_end || pos >= a.ccap || pos < out_pos) {
-            bad |= 1 << 5;
-          } else if ((CBH_ABL & 4) && key != kNoRow - 7) {  // ablation build: no stores
-            bad |= (key == kNoRow - 3 && val == acc_t(12345)) ? 1 << 29 : 0;
-          } else {
-            a.Cir[pos] = key;
-            reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(val);
-          }
-        }
+        if (occ) emit(s, key, val, o + __popcll(mask & lt));
         o += __popcll(mask);
       }
+#endif
       out_pos += tot;
     }
     lo = hi;
