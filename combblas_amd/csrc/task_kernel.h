@@ -44,6 +44,9 @@
 #ifndef CBH_CQ
 #define CBH_CQ 1  // numeric commit: 1 = per-wave queue of occupied slots, committed 64 at a time
 #endif
+#ifndef CBH_EQ
+#define CBH_EQ 0  // 1 = block-wide queue of the entries active in a sub-tile for the segment probe
+#endif
 #ifndef CBH_FILL
 #define CBH_FILL 4
 #endif
@@ -242,6 +245,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
   constexpr bool NUM = C::NUM;
   constexpr int TA = C::TA, NW = C::NW, WIN = C::WIN;
   static_assert((T & (T - 1)) == 0, "table size must be a power of two");
+  static_assert(!CBH_EQ || WIN >= EMAX, "the entry queue fits the owner map");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int32_t* keys = reinterpret_cast<int32_t*>(smem + C::o_keys);
@@ -257,6 +261,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
   typename C::own_t* own = reinterpret_cast<typename C::own_t*>(smem + C::o_own);
   int32_t* red = reinterpret_cast<int32_t*>(smem + C::o_red);
   __shared__ int32_t s_ovf;  // overflow flag of the current sub-tile (LDS; read after barriers)
+  __shared__ int32_t s_nq;   // queued active entries of the current chunk (CBH_EQ)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // row ids of A: the packed records in numeric mode (stride RS dwords), ir in symbolic mode
@@ -402,7 +407,10 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         if constexpr (NUM) vals[s] = SR::identity();
       }
     }
-    if (tid == 0) __hip_atomic_store(&s_ovf, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (tid == 0) {
+      __hip_atomic_store(&s_ovf, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      s_nq = 0;
+    }
     const int count_before = my_count;
     __syncthreads();
     CBH_STAMP(1);
@@ -416,6 +424,33 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         __syncthreads();
       }
       // segment of every entry inside [lo, hi): idle entries (next row >= hi) cost one LDS read
+#if CBH_EQ
+      // active entries are queued block-wide (in `own`, free until the window loop) so the probe
+      // loads issue from as few waves as there are active entries, not from every wave
+      for (int i = tid; i < nec; i += BS) {
+        const int32_t nx = enext[i];
+        if (nx < hi && !hi_is_end) {
+          own[atomicAdd(&s_nq, 1)] = (typename C::own_t)i;
+        } else {
+          eoff[i] = nx < hi ? (int32_t)(eend[i] - epos[i]) : 0;
+          enext2[i] = nx < hi ? kNoRow : nx;
+        }
+      }
+      __syncthreads();
+      {
+        const int nq = s_nq;
+        for (int j = tid; j < nq; j += BS) {
+          const int i = own[j];
+          const int64_t p = epos[i];
+          int32_t nx2 = enext[i];
+          const int64_t stop = probe_stop64<RS, 8>(rowsA, p + 1, eend[i], hi, nx2);
+          eoff[i] = (int32_t)(stop - p);
+          enext2[i] = nx2;
+        }
+      }
+      __syncthreads();
+      if (tid == 0) s_nq = 0;
+#else
       for (int i = tid; i < nec; i += BS) {
         const int32_t nx = enext[i];
         const int64_t p = epos[i];
@@ -434,6 +469,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         enext2[i] = nx2;
       }
       __syncthreads();
+#endif
       CBH_STAMP(2);
       block_scan_excl<BS>(eoff, nec, red);
       for (int i = tid; i < nec; i += BS) qoff[i] = epos[i] - eoff[i];
