@@ -44,6 +44,9 @@
 #ifndef CBH_CQ
 #define CBH_CQ 1  // numeric commit: 1 = per-wave queue of occupied slots, committed 64 at a time
 #endif
+#ifndef CBH_VCLR
+#define CBH_VCLR 0  // 1 = the numeric commit resets the values it reads (the clear skips them)
+#endif
 #ifndef CBH_EQ
 #define CBH_EQ 0  // 1 = block-wide queue of the entries active in a sub-tile for the segment probe
 #endif
@@ -393,6 +396,9 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
 
   int32_t lo = tlo;
   int64_t w = wnom;
+  // vals needs a full clear before the first sub-tile and after an overflowed one; a committed
+  // sub-tile leaves it cleared (CBH_VCLR)
+  bool vdirty = true;
   while (lo < thi) {
     const int32_t hi = (int32_t)(((int64_t)lo + w < thi) ? lo + w : thi);
     const bool hi_is_end = hi == thi;  // entry ends are clamped to the task (load_entries)
@@ -404,8 +410,10 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
     } else {
       for (int s = tid; s < TA; s += BS) {
         keys[s] = kEmpty;
-        if constexpr (NUM) vals[s] = SR::identity();
+        if constexpr (NUM)
+          if (!CBH_VCLR || vdirty) vals[s] = SR::identity();
       }
+      vdirty = false;
     }
     if (tid == 0) {
       __hip_atomic_store(&s_ovf, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -571,6 +579,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
     if (!bitmap && __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {  // table could not hold the sub-tile: halve the row range, redo
       __syncthreads();
       my_count = count_before;
+      vdirty = true;
       if (tw == 1) {
         if (tid == 0) atomicOr(&a.err[1], 1);
         return;
@@ -620,6 +629,9 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
       // slot s (occupied, key, val) of the wave's occupied slots in slot order goes to
       // base - (s - start of its run) + (keys of its run smaller than key)
       auto emit = [&](int s, int32_t key, acc_t val, int64_t base) {
+#if CBH_VCLR
+        vals[s] = SR::identity();  // only this lane reads vals[s]: the next sub-tile's clear skips vals
+#endif
         // the kWin slots on either side (independent LDS reads, one latency): the run's extent
         // around s and the keys of it smaller than key, branch-free while the run stays in the
         // window (runs of <= 2*kWin+1 slots; the LDS walk below covers longer ones)
