@@ -54,26 +54,46 @@ def parse():
 
 
 def cpu_baseline(scale, ef, frac):
-    """Reference Mult_AnXBn_Synch (MPI+OpenMP, 1 rank) on a bounded column sample of the same
-    product, C = A * A(:, 0:n*frac), on this host's cores. Falls back to the oracle port."""
+    """Reference Mult_AnXBn_Synch (MPI+OpenMP) on a bounded column sample of the same product,
+    C = A * A(:, c % stride == 0) (stride = 1/frac: the sample spreads over every processor column
+    of a multi-rank grid), on this host's cores: one untimed warm-up call, median of 3 timed calls,
+    for 1 rank x all cores and 4 ranks (2x2 grid) x cores/4; the faster layout is reported.
+    Falls back to the oracle port when oracle/_ref is absent."""
     n = 1 << scale
-    c1 = max(1, int(n * frac))
+    stride = max(1, round(1 / frac))
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     ref = os.path.join(HERE, "oracle", "_ref", "ref_harness")
-    sample = f"C = A*A(:,0:{c1}) of R-MAT scale {scale} ef {ef} (1/{round(1 / frac)} of B's columns), 1 run"
+    sample = f"C = A*A(:, 0:{n}:{stride}) of R-MAT scale {scale} ef {ef} (1/{stride} of B's columns, strided)"
     if os.path.exists(ref):
-        env = dict(os.environ, OMP_NUM_THREADS=str(cores))
-        try:
-            r = subprocess.run([ref, "slice", str(scale), str(ef), "0", str(c1), "1", "pt_f64"], env=env, cwd="/tmp",
-                               capture_output=True, text=True, timeout=900)
-            line = [l for l in r.stdout.splitlines() if l.startswith("{")]
-            if r.returncode == 0 and line:
-                d = json.loads(line[-1])
-                return {"value": round(d["gflops"], 6), "unit": "GFLOP/s", "cores": d["threads"], "kind": "reference",
-                        "sample": sample + f": {d['flops']} flops in {d['median_s']:.3f} s (Mult_AnXBn_Synch, "
-                                           "oracle/_ref built from the reference sources)"}
-        except Exception as e:  # noqa: BLE001
-            print(f"reference CPU baseline failed: {e}", file=sys.stderr)
+        best, tried = None, []
+        mpirun = "/opt/conda/bin/mpirun"
+        layouts = [(1, cores)] + ([(4, max(1, cores // 4))] if cores >= 4 and os.path.exists(mpirun) else [])
+        for ranks, thr in layouts:
+            env = dict(os.environ, OMP_NUM_THREADS=str(thr),
+                       LD_LIBRARY_PATH="/usr/lib/x86_64-linux-gnu:/opt/conda/lib")
+            cmd = [ref, "slice", str(scale), str(ef), "0", str(n), "3", "pt_f64", str(stride)]
+            if ranks > 1:
+                cmd = [mpirun, "-np", str(ranks)] + cmd
+            try:
+                r = subprocess.run(cmd, env=env, cwd="/tmp", capture_output=True, text=True, timeout=600)
+                line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+                if r.returncode == 0 and line:
+                    d = json.loads(line[-1])
+                    tried.append(f"{ranks}x{thr}: {d['gflops']:.4f} GFLOP/s (median {d['median_s']:.3f} s)")
+                    if best is None or d["gflops"] > best["gflops"]:
+                        best = d
+                else:
+                    tried.append(f"{ranks}x{thr}: failed rc={r.returncode}")
+            except Exception as e:  # noqa: BLE001
+                tried.append(f"{ranks}x{thr}: {e}")
+        if best is not None:
+            return {"value": round(best["gflops"], 6), "unit": "GFLOP/s", "cores": best["ranks"] * best["threads"],
+                    "kind": "reference",
+                    "sample": sample + f": {best['flops']} flops, median of {best['reps']} after 1 warm-up = "
+                                       f"{best['median_s']:.3f} s on {best['ranks']} rank(s) x {best['threads']} "
+                                       f"threads (Mult_AnXBn_Synch, oracle/_ref built from the reference sources); "
+                                       f"layouts tried: " + "; ".join(tried)}
+        print("reference CPU baseline failed: " + "; ".join(tried), file=sys.stderr)
     # port: the oracle restatement (tests-only code, used here only as the CPU baseline leg)
     sys.path.insert(0, os.path.join(HERE, "tests"))
     import helpers as H
@@ -81,14 +101,22 @@ def cpu_baseline(scale, ef, frac):
 
     A = cb.rmat(scale, ef, dtype=np.float64)
     d = H.Dcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num)
-    B = d.col_slice(0, c1)
+    keep = np.nonzero(d.jc % stride == 0)[0]
+    B = H.Dcsc(d.m, d.n, d.jc[keep], np.concatenate([[0], np.cumsum(np.diff(d.cp)[keep])]),
+               np.concatenate([d.ir[d.cp[i]:d.cp[i + 1]] for i in keep]),
+               np.concatenate([d.num[d.cp[i]:d.cp[i + 1]] for i in keep]))
     O = H.Oracle()
-    t0 = time.perf_counter()
-    C = O.spgemm(d, B, "plus_times", "hybrid", threads=cores)
-    dt = time.perf_counter() - t0
+    O.spgemm(d, B, "plus_times", "hybrid", threads=cores)  # warm-up
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        C = O.spgemm(d, B, "plus_times", "hybrid", threads=cores)
+        ts.append(time.perf_counter() - t0)
+    dt = sorted(ts)[1]
     flops = O.symbolic(d, B, threads=cores)[0]
     return {"value": round(2 * flops / dt / 1e9, 6), "unit": "GFLOP/s", "cores": cores, "kind": "port",
-            "sample": sample + f": {flops} flops in {dt:.3f} s (oracle restatement), nnzC {C.nnz}"}
+            "sample": sample + f": {flops} flops, median of 3 after 1 warm-up = {dt:.3f} s (oracle restatement), "
+                               f"nnzC {C.nnz}"}
 
 
 def grid_shape(world):
@@ -100,6 +128,26 @@ def grid_shape(world):
         if world % layers == 0 and math.isqrt(world // layers) ** 2 == world // layers:
             return layers
     return world
+
+
+def product_value_sum(A):
+    """closed form of sum(A*A) under PlusTimes: sum_k colsum_k(A) * rowsum_k(A) (exact: integer
+    multiplicities)"""
+    colsum = np.zeros(A.n, np.float64)
+    colsum[A.jc] = np.add.reduceat(A.num.astype(np.float64), A.cp[:-1]) if A.nnz else 0
+    rowsum = np.bincount(A.ir, weights=A.num.astype(np.float64), minlength=A.m)
+    return int(np.dot(colsum.astype(np.int64), rowsum.astype(np.int64)))
+
+
+def reference_digest(scale, ef):
+    """order-sensitive digest of the whole f64 product computed by the reference's own
+    LocalHybridSpGEMM (tests/golden/make_golden_s22.py), when it is on file for this size"""
+    p = os.path.join(HERE, "tests", "golden", f"scale{scale}.json")
+    try:
+        g = json.load(open(p))
+        return g["pt_f64"]["total"]["digest"] if g.get("edgefactor") == ef else None
+    except Exception:  # noqa: BLE001
+        return None
 
 
 def host_flops(A):
@@ -147,6 +195,7 @@ def main():
     SR = cb.PlusTimesSRing
     A = cb.rmat(args.scale, args.edgefactor, dtype=np.float64)
     nnzA = A.nnz
+    closed_sum = product_value_sum(A)
     if world == 1:
         # ------------------------------------------------------------ 1 GPU: device phase loop
         ctx = cb.Context(local, torch_allocator=False)
@@ -161,7 +210,7 @@ def main():
 
         def verify():
             sv = cb.PhasedSpGEMM(SR, dA, dB, checksum=True)
-            return sv["nnz"], sv["value_sum"]
+            return sv["nnz"], sv["value_sum"], sv["digest"]
         parallelism = "1 GPU"
     else:
         # ------------------------------------------------------------ N GPUs: SUMMA over RCCL
@@ -208,7 +257,7 @@ def main():
             acc.clear()
             acc["sum"] = 0.0
             run()
-            return acc["nnz"], acc["sum"]
+            return acc["nnz"], acc["sum"], None
 
     for _ in range(args.warmup):
         st = step()
@@ -253,12 +302,16 @@ def main():
 
     check = None
     if not args.no_verify:
-        nz, vs = verify()
+        nz, vs, dg = verify()
         nnz_all = allreduce(float(nz), dist.ReduceOp.SUM if world > 1 else None)
         vsum = allreduce(vs, dist.ReduceOp.SUM if world > 1 else None)
         known = {22: 24766243778, 20: 3284757756, 18: 425342972, 16: 53638834, 14: 6471508}.get(args.scale)
-        check = {"nnzC": int(nnz_all), "value_sum": vsum, "expected_nnzC": known,
-                 "ok": (known is None or int(nnz_all) == known)}
+        gold = reference_digest(args.scale, args.edgefactor)
+        check = {"nnzC": int(nnz_all), "expected_nnzC": known, "value_sum": vsum,
+                 "expected_value_sum": float(closed_sum), "digest": str(dg) if dg is not None else None,
+                 "reference_digest": gold}
+        check["ok"] = bool((known is None or int(nnz_all) == known) and vsum == float(closed_sum)
+                           and (dg is None or gold is None or str(dg) == gold))
 
     if rank == 0:
         base = None

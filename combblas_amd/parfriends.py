@@ -152,21 +152,26 @@ def _stage_blocks(A, B, grid, stages):
     return Ab, Bb, vdtype
 
 
-def _phase_cuts(be, Ab, Bb, ncols, phases, budget_entries, group=None):
+def _phase_cuts(be, Ab, Bb, ncols, phases, budget_entries, groups=()):
     """Column ranges [c0, c1) of the local output block. With phases <= 0 they are planned from
-    the exact per-column nnz of the stage partials (summed over `group`, so that every rank of
-    a fiber cuts identically), each phase's partials staying within budget_entries."""
+    the exact per-column nnz of the stage partials, each phase's partials staying within
+    budget_entries. The counts and the budget are reduced over every group in `groups` in turn
+    (the ranks that share this block's column space: the processor column in 2D; the fiber, then
+    the layer's processor column in 3D), so that every rank whose later collectives pair up
+    (MCLPruneRecoverySelect's column reductions, the fiber reduce-scatter) cuts identically --
+    the reference's equivalent is one global phase count (MPI_MAX over World, ParFriends.h:494)."""
     if phases and phases > 0:
         return [block_range(ncols, phases, p) for p in range(phases)]
-    if group is not None:  # every rank of the fiber must cut identically
-        t = torch.tensor([budget_entries], dtype=torch.int64, device=be.device)
-        budget_entries = int(allreduce_(t, group, torch.distributed.ReduceOp.MIN).item())
+    t = torch.tensor([budget_entries], dtype=torch.int64, device=be.device)
+    for g in groups:
+        allreduce_(t, g, torch.distributed.ReduceOp.MIN)
+    budget_entries = int(t.item())
     col = torch.zeros(ncols + 1, dtype=torch.int64, device=be.device)
     for a, b in zip(Ab, Bb):
         if be.dims(b)[3]:
             col.index_add_(0, be.arrays(b)[1], be.col_nnz(a, b))
-    if group is not None:
-        allreduce_(col, group)
+    for g in groups:
+        allreduce_(col, g)
     cum = np.concatenate([[0], np.cumsum(col[:ncols].cpu().numpy())])
     cuts, c0 = [], 0
     while c0 < ncols:
@@ -312,7 +317,8 @@ def MemEfficientSpGEMM(SR, A: SpParMat, B: SpParMat, phases=0, hardThreshold=Non
     be = A.backend
     Ab, Bb, vdtype = _stage_blocks(A, B, grid, stages)
     m, n = be.dims(A.seq)[0], be.dims(B.seq)[1]
-    cuts = _phase_cuts(be, Ab, Bb, n, phases, _budget_entries(be, vdtype, perProcessMemory, 2))
+    cuts = _phase_cuts(be, Ab, Bb, n, phases, _budget_entries(be, vdtype, perProcessMemory, 2),
+                       groups=(grid.colWorld,))
     out = []
     for c0, c1 in cuts:
         parts = [be.multiply(SR, a, _colslice(be, b, c0, c1)) for a, b in zip(Ab, Bb)]
@@ -384,7 +390,8 @@ def Mult_AnXBn_SUMMA3D(SR, A: SpParMat3D, B: SpParMat3D, phases=1, perProcessMem
     be = A.backend
     Ab, Bb, vdtype = _stage_blocks(A, B, grid, stages)
     m, n = be.dims(A.seq)[0], be.dims(B.seq)[1]
-    cuts = _phase_cuts(be, Ab, Bb, n, phases, _budget_entries(be, vdtype, perProcessMemory, 3), group=g3.fiberWorld)
+    cuts = _phase_cuts(be, Ab, Bb, n, phases, _budget_entries(be, vdtype, perProcessMemory, 3),
+                       groups=(g3.fiberWorld, grid.colWorld))
     div = _divisions3d(n, g3.gridLayers)
     out, mine0 = [], 0
     for c0, c1 in cuts:

@@ -87,7 +87,11 @@ class Context:
             torch = _torch()
 
             def _alloc(user, nbytes, stream):
-                t = torch.empty(int(nbytes), dtype=torch.uint8, device=self.tdevice)
+                # the block belongs to the library's stream (whatever stream is current in the
+                # caller): torch's caching allocator then reuses it only in that stream's order,
+                # which is the order every library kernel and free happens in
+                with torch.cuda.stream(self.tstream):
+                    t = torch.empty(int(nbytes), dtype=torch.uint8, device=self.tdevice)
                 p = t.data_ptr()
                 self._live[p] = t
                 return p

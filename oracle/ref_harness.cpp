@@ -11,15 +11,22 @@
 //   merge <sr> <out.cbm> <in1.cbm> ...                MultiwayMerge (MultiwayMerge.h:411)
 //   synch <sr> <A.cbm> <B.cbm> <out.cbm|-> [reps]     Mult_AnXBn_Synch on a 1x1 grid (ParFriends.h:1004),
 //                                                     prints wall time per call (MPI_Wtime)
-//   slice <scale> <ef> <col0> <col1> <reps> <sr>      CPU baseline: A (scale, ef) times the column block
-//                                                     A(:, col0:col1) with Mult_AnXBn_Synch; prints JSON
+//   slice <scale> <ef> <col0> <col1> <reps> <sr> [stride]
+//                                                     CPU baseline: A (scale, ef) times the columns
+//                                                     c0 <= c < c1, (c-c0) % stride == 0 of A, with
+//                                                     Mult_AnXBn_Synch on any square rank count; JSON
+//   digest <scale> <ef> <block> <sr>                 digest + value sum of the whole C = A*A by column
+//                                                     blocks of B (LocalHybridSpGEMM), one JSON line per block
 //   tc    <scale> <L.cbm> <C.cbm>                     Applications/TC.cpp:62-121 on one rank (C = (L*L).*L)
 //   mcl   <A.cbm> <out.cbm> <hard> <select> <recover> <pct>
 //                                                     MCLPruneRecoverySelect (ParFriends.h:185-353)
 // sr: pt_f64 | pt_i64 | max_i64 | min_i64 | bool ; kernel: hybrid | hash | hashu | heap
 #include <mpi.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cstring>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -189,39 +196,47 @@ static int do_gen(int scale, int ef, const std::string& fo) {
 
 // CPU baseline on a bounded column block of the north-star workload: C = A * A(:, c0:c1).
 template <class SR, class NT>
-static int do_slice(int scale, int ef, int64_t c0, int64_t c1, int reps) {
+static int do_slice(int scale, int ef, int64_t c0, int64_t c1, int reps, int64_t stride) {
+  // Any square number of MPI ranks p (mpirun -np p): the generator distributes A over the
+  // sqrt(p) x sqrt(p) grid exactly as TC.cpp does, B = A(:, c0:c1) via SpParMat::PruneI on global
+  // column ids (all n columns kept, as a ColSplit piece), one untimed warm-up call, then `reps`
+  // timed Mult_AnXBn_Synch calls (barrier + MPI_Wtime, max over ranks); prints the median.
   typedef SpDCCols<int64_t, NT> DER;
-  std::shared_ptr<CommGrid> grid(new CommGrid(MPI_COMM_WORLD, 0, 0));
+  int rank = 0, nprocs = 1;
+  MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+  MPI_Comm_size(MPI_COMM_WORLD, &nprocs);
   double tg0 = now();
   auto* G = gen_rmat(scale, ef);
   double tg1 = now();
-  cbm::Dcsc a = from_spdccols<int64_t>(G->seq());
-  delete G;
-  // B = A(:, c0:c1) keeping all n columns (empty outside the block), as a ColSplit piece would.
-  cbm::Dcsc b;
-  b.vtype = a.vtype;
-  b.m = a.m;
-  b.n = a.n;
-  b.cp.push_back(0);
-  for (int64_t i = 0; i < a.nzc(); ++i) {
-    if (a.jc[i] < c0 || a.jc[i] >= c1) continue;
-    b.jc.push_back(a.jc[i]);
-    for (int64_t p = a.cp[i]; p < a.cp[i + 1]; ++p) {
-      b.ir.push_back(a.ir[p]);
-      b.vi.push_back(a.vi[p]);
-    }
-    b.cp.push_back((int64_t)b.ir.size());
+  typedef SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>> GMat;
+  GMat GB(*G);
+  GB.PruneI([c0, c1, stride](const std::tuple<int64_t, int64_t, int64_t>& t) {
+    const int64_t c = std::get<1>(t);
+    return c < c0 || c >= c1 || (c - c0) % stride != 0;
+  });
+  // flops = sum_k nnz(A(:,k)) * nnz(B(k,:)) (EstimateFLOP's count; the reference's EstimateFLOP
+  // faults on ranks whose B block is empty, so the same sum is formed from two Reduce()s)
+  int64_t flops = 0;
+  {
+    auto one = [](int64_t) { return (int64_t)1; };
+    FullyDistVec<int64_t, int64_t> ca = G->Reduce(Column, std::plus<int64_t>(), (int64_t)0, one);
+    FullyDistVec<int64_t, int64_t> rb = GB.Reduce(Row, std::plus<int64_t>(), (int64_t)0, one);
+    int64_t loc = 0;
+    for (int64_t i = 0; i < ca.LocArrSize(); ++i) loc += ca.GetLocArr()[i] * rb.GetLocArr()[i];
+    MPI_Allreduce(&loc, &flops, 1, MPI_INT64_T, MPI_SUM, MPI_COMM_WORLD);
   }
-  SpParMat<int64_t, NT, DER> A(to_spdccols<NT>(a), grid);
-  SpParMat<int64_t, NT, DER> B(to_spdccols<NT>(b), grid);
-  int64_t flops = EstimateFLOP<SR>(A, B);
+  SpParMat<int64_t, NT, DER> A(*G);
+  SpParMat<int64_t, NT, DER> B(GB);
+  delete G;
   std::vector<double> ts;
   int64_t nnzc = 0;
-  for (int r = 0; r < reps; ++r) {
+  for (int r = -1; r < reps; ++r) {  // r = -1: warm-up
+    MPI_Barrier(MPI_COMM_WORLD);
     double t0 = now();
     SpParMat<int64_t, NT, DER> C = Mult_AnXBn_Synch<SR, NT, DER>(A, B);
-    double t1 = now();
-    ts.push_back(t1 - t0);
+    double t1 = now(), dt = t1 - t0, mx = 0;
+    MPI_Allreduce(&dt, &mx, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+    if (r >= 0) ts.push_back(mx);
     nnzc = C.getnnz();
   }
   std::sort(ts.begin(), ts.end());
@@ -234,10 +249,88 @@ static int do_slice(int scale, int ef, int64_t c0, int64_t c1, int reps) {
     nthreads = omp_get_num_threads();
   }
 #endif
-  std::printf("{\"flops\": %lld, \"nnzC\": %lld, \"median_s\": %.6f, \"min_s\": %.6f, \"reps\": %d, "
-              "\"gflops\": %.6f, \"threads\": %d, \"gen_s\": %.3f, \"col0\": %lld, \"col1\": %lld}\n",
-              (long long)flops, (long long)nnzc, med, ts[0], reps, 2.0 * flops / med / 1e9, nthreads, tg1 - tg0,
-              (long long)c0, (long long)c1);
+  if (rank == 0)
+    std::printf("{\"flops\": %lld, \"nnzC\": %lld, \"median_s\": %.6f, \"min_s\": %.6f, \"max_s\": %.6f, "
+                "\"reps\": %d, \"warmup\": 1, \"gflops\": %.6f, \"ranks\": %d, \"threads\": %d, \"gen_s\": %.3f, "
+                "\"col0\": %lld, \"col1\": %lld, \"stride\": %lld}\n",
+                (long long)flops, (long long)nnzc, med, ts.front(), ts.back(), reps, 2.0 * flops / med / 1e9, nprocs,
+                nthreads, tg1 - tg0, (long long)c0, (long long)c1, (long long)stride);
+  return 0;
+}
+
+// Digest of the WHOLE product C = A*A (R-MAT scale, ef) computed by the reference's own
+// LocalHybridSpGEMM (mtSpGEMM.h:212-460) one column block of B at a time (B = A(:, c0:c1), all n
+// columns kept, as a ColSplit piece), so that the output never has to be held at once (scale 22:
+// 24.8 G entries). Entries are visited in C order (columns ascending, rows as the kernel emits
+// them) with a running global index, so the sum over blocks is the same order-sensitive digest
+// as tests/helpers.py digest() / the device checksum_kernel over the whole C. Prints one JSON line
+// per block and a final total.
+static inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+template <class NT>
+static uint64_t bits_of(NT v) {
+  if (std::is_same<NT, double>::value) {
+    uint64_t b;
+    std::memcpy(&b, &v, 8);
+    return b;
+  }
+  return (uint64_t)(int64_t)v;
+}
+template <class SR, class NT>
+static int do_digest(int scale, int ef, int64_t block) {
+  auto* G = gen_rmat(scale, ef);
+  cbm::Dcsc a = from_spdccols<int64_t>(G->seq());
+  delete G;
+  SpDCCols<int64_t, NT>* A = to_spdccols<NT>(a);
+  // column sums and row sums of A for the closed form sum(C) = sum_k colsum_k(A) * rowsum_k(A)
+  uint64_t gidx = 0, dig = 0;
+  long double vsum_exact = 0;
+  for (int64_t c0 = 0; c0 < a.n; c0 += block) {
+    const int64_t c1 = std::min<int64_t>(a.n, c0 + block);
+    cbm::Dcsc b;
+    b.vtype = a.vtype;
+    b.m = a.m;
+    b.n = a.n;
+    b.cp.push_back(0);
+    for (int64_t i = 0; i < a.nzc(); ++i) {
+      if (a.jc[i] < c0 || a.jc[i] >= c1) continue;
+      b.jc.push_back(a.jc[i]);
+      for (int64_t p = a.cp[i]; p < a.cp[i + 1]; ++p) {
+        b.ir.push_back(a.ir[p]);
+        b.vi.push_back(a.vi[p]);
+      }
+      b.cp.push_back((int64_t)b.ir.size());
+    }
+    SpDCCols<int64_t, NT>* B = to_spdccols<NT>(b);
+    double t0 = now();
+    SpTuples<int64_t, NT>* C = LocalHybridSpGEMM<SR, NT>(*A, *B, false, false);
+    double t1 = now();
+    const int64_t nnz = C->getnnz();
+    uint64_t bd = 0;
+    double bs = 0;
+    for (int64_t i = 0; i < nnz; ++i) {
+      const NT v = C->numvalue(i);
+      const uint64_t p = gidx + (uint64_t)i;
+      bd += mix64(p ^ mix64((uint64_t)C->colindex(i) ^ mix64((uint64_t)(uint32_t)C->rowindex(i) ^ mix64(bits_of<NT>(v)))));
+      bs += (double)v;
+    }
+    std::printf("{\"block\": [%lld, %lld], \"gbase\": %llu, \"nnz\": %lld, \"sum\": %.1f, \"digest\": \"%llu\", "
+                "\"kernel_s\": %.3f}\n",
+                (long long)c0, (long long)c1, (unsigned long long)gidx, (long long)nnz, bs, (unsigned long long)bd,
+                t1 - t0);
+    std::fflush(stdout);
+    gidx += (uint64_t)nnz;
+    dig += bd;
+    vsum_exact += bs;
+    delete C;
+    delete B;
+  }
+  std::printf("{\"total\": true, \"nnz\": %llu, \"sum\": %.1f, \"digest\": \"%llu\"}\n", (unsigned long long)gidx,
+              (double)vsum_exact, (unsigned long long)dig);
+  delete A;
   return 0;
 }
 
@@ -323,10 +416,15 @@ static int run(int argc, char** argv) {
     int reps = argc > 6 ? std::atoi(argv[6]) : 1;
     DISPATCH_SR(sr, (do_synch<SR, NT>(argv[3], argv[4], argv[5], reps)));
   }
-  if (mode == "slice" && argc == 8) {
+  if (mode == "slice" && (argc == 8 || argc == 9)) {
     std::string sr = argv[7];
+    const int64_t stride = argc == 9 ? std::max<int64_t>(1, std::atoll(argv[8])) : 1;
     DISPATCH_SR(sr, (do_slice<SR, NT>(std::atoi(argv[2]), std::atoi(argv[3]), std::atoll(argv[4]),
-                                      std::atoll(argv[5]), std::atoi(argv[6]))));
+                                      std::atoll(argv[5]), std::atoi(argv[6]), stride)));
+  }
+  if (mode == "digest" && argc == 6) {
+    std::string sr = argv[5];
+    DISPATCH_SR(sr, (do_digest<SR, NT>(std::atoi(argv[2]), std::atoi(argv[3]), std::atoll(argv[4]))));
   }
   if (mode == "tc" && argc == 5) return do_tc(std::atoi(argv[2]), argv[3], argv[4]);
   if (mode == "mcl" && argc == 8)

@@ -311,3 +311,15 @@ def random_dcsc(rng, m, n, density, dtype=np.float64, empty_cols=0.0):
     else:
         vals = rng.integers(-5, 6, rows.size).astype(dtype)
     return Dcsc.from_coo(m, n, rows, cols, np.asarray(vals, dtype))
+
+
+# ------------------------------------------------------------------ closed forms
+def product_value_sum(A: Dcsc, B: Dcsc = None):
+    """sum of all values of A*B under PlusTimes = sum_k colsum_k(A) * rowsum_k(B) (exact in int64
+    for multiplicity-valued R-MAT; a size-independent property of the whole product)."""
+    B = A if B is None else B
+    colsum = np.zeros(A.n, np.int64)
+    colsum[A.jc] = np.add.reduceat(A.num.astype(np.int64), A.cp[:-1]) if A.nnz else 0
+    rowsum = np.bincount(B.ir, weights=None, minlength=B.m).astype(np.int64) if B.num.dtype == bool else \
+        np.bincount(B.ir, weights=B.num.astype(np.float64), minlength=B.m).astype(np.int64)
+    return int(np.dot(colsum, rowsum))

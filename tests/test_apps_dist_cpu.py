@@ -81,7 +81,7 @@ def test_tc_2x2_vs_reference(apps, apps_meta):
     assert int(got.num.sum()) == apps_meta["tc"]["10"]["triangles"] == 78452
 
 
-def _mcl_worker(rank, world, mode, params, phases):
+def _mcl_worker(rank, world, mode, params, phases, ppm=0):
     from combblas_amd import parfriends as pf
     from combblas_amd.commgrid import CommGrid, CommGrid3D
     from combblas_amd.semirings import PlusTimesSRing
@@ -97,20 +97,24 @@ def _mcl_worker(rank, world, mode, params, phases):
             g3 = CommGrid3D(2)
             dA = SpParMat3D.distribute(A, g3, be, colsplit=True)
             dB = SpParMat3D.distribute(A, g3, be, colsplit=False)
-            C = pf.MemEfficientSpGEMM3D(PlusTimesSRing, dA, dB, phases=phases, **kw)
+            C = pf.MemEfficientSpGEMM3D(PlusTimesSRing, dA, dB, phases=phases, perProcessMemory=ppm, **kw)
         else:
             grid = CommGrid()
             dA, dB = SpParMat.distribute(A, grid, be), SpParMat.distribute(A, grid, be)
-            C = pf.MemEfficientSpGEMM(PlusTimesSRing, dA, dB, phases=phases, **kw)
+            C = pf.MemEfficientSpGEMM(PlusTimesSRing, dA, dB, phases=phases, perProcessMemory=ppm, **kw)
         res.append(C.gather_host())
     return (_out(res[0]), _out(res[1])) if rank == 0 else None
 
 
-@pytest.mark.parametrize("mode,world,phases", [("2d", 4, 3), ("3d", 8, 2)])
-def test_mcl_prune_distributed(apps, apps_meta, mode, world, phases):
+# phases=0 plans the phases from the exact symbolic pass under a small per-process budget (many
+# phases; every rank's local counts differ): the cuts must still agree across the ranks whose
+# column reductions pair up, or the prune's collectives would hang or mix columns
+@pytest.mark.parametrize("mode,world,phases,ppm", [("2d", 4, 3, 0), ("3d", 8, 2, 0), ("2d", 4, 0, 96 * 1024),
+                                                    ("3d", 8, 0, 64 * 1024)])
+def test_mcl_prune_distributed(apps, apps_meta, mode, world, phases, ppm):
     p = apps_meta["mcl"]["0"]
     params = (p["hard"], p["select"], p["recover"], p["pct"])
-    raw, pruned = run_world(_mcl_worker, world, mode, params, phases)
+    raw, pruned = run_world(_mcl_worker, world, mode, params, phases, ppm)
     A2, got = _dc(raw), _dc(pruned)
     ref = apps["mcl_A2"]
     assert np.array_equal(A2.jc, ref.jc) and np.array_equal(A2.cp, ref.cp) and np.array_equal(A2.ir, ref.ir)
