@@ -86,8 +86,8 @@ __global__ __launch_bounds__(BS) void masked_kernel(MaskArgs a) {
         int64_t s = 0, e = 0;
         if (k >= 0 && k < a.ncolA) {
           const int64_t base = a.Acp[k], end = a.Acp[k + 1];
-          s = lb_rows64<1>(a.Air, base, end, rlo);
-          e = lb_rows64<1>(a.Air, s, end, rhi + 1);  // row ids are < m < 2^31 - 1
+          s = lb_rows64(a.Air, base, end, rlo);
+          e = lb_rows64(a.Air, s, end, rhi + 1);  // row ids are < m < 2^31 - 1
         } else {
           guard_fail(a.err, 20, c, k);
         }
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256) void ewise_kernel(const int64_t* __restrict__ 
       int64_t q = 0;
       if (p < p1) {
         const int32_t r = Air[p];
-        q = lb_rows64<1>(Bir, b0, b1, r);
+        q = lb_rows64(Bir, b0, b1, r);
         hit = q < b1 && Bir[q] == r;
       }
       const uint64_t m = __ballot(hit);

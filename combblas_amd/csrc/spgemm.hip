@@ -621,7 +621,7 @@ static int64_t task_flops() {
 
 // Row blocks: C's rows are cut into blocks of RB rows (kRowBlocks blocks); interior task
 // boundaries of a split column sit on block boundaries, where the row-block table of A gives
-// every entry's position directly (ablk_kernel).
+// every hub entry's position directly (hub_fill_kernel); short columns bisect.
 constexpr int64_t kRowBlocks = 128;
 
 __global__ void task_count_kernel(const int64_t* __restrict__ flop, const int32_t* __restrict__ rmin,
@@ -668,15 +668,31 @@ __global__ __launch_bounds__(256) void task_fill_kernel(const int64_t* __restric
   }
 }
 
-// Row-block table of A (wave per column of the dense pointers): out[k*(nblk+1) + x] = first
-// position of A(:,k), relative to its start, whose row is >= x*RB, for x = 0..nblk.
-__global__ __launch_bounds__(256) void ablk_kernel(const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
-                                                   int64_t ncol, int32_t RB, int64_t nblk, int32_t* __restrict__ out) {
+// Row-block table of the hub columns of A (>= kHubMin entries; wave per hub column):
+// out[h*(nblk+1) + x] = first position of A(:,k), relative to its start, whose row is >= x*RB,
+// for x = 0..nblk. Task boundaries (multiples of RB) and the stop search of long segments
+// (task_kernel.h stop_search) read it; short columns bisect instead. At scale 22: 288 K hub
+// columns (82 % of A's entries), 149 MB, instead of a table over all 4.2 M columns.
+constexpr int64_t kHubMin = 32;
+__global__ void hub_flag_kernel(const int64_t* __restrict__ Acp, int64_t ncol, int64_t minlen, int64_t* __restrict__ flag) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < ncol) flag[k] = (Acp[k + 1] - Acp[k]) >= minlen ? 1 : 0;
+}
+__global__ void hub_index_kernel(const int64_t* __restrict__ flag, const int64_t* __restrict__ pos, int64_t ncol,
+                                 int32_t* __restrict__ hidx) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < ncol) hidx[k] = flag[k] ? (int32_t)pos[k] : -1;
+}
+__global__ __launch_bounds__(256) void hub_fill_kernel(const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
+                                                       const int32_t* __restrict__ hidx, int64_t ncol, int32_t RB,
+                                                       int64_t nblk, int32_t* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (k >= ncol) return;
+  const int32_t h = hidx[k];
+  if (h < 0) return;
   const int64_t base = Acp[k], len = Acp[k + 1] - base;
-  int32_t* o = out + k * (nblk + 1);
+  int32_t* o = out + (int64_t)h * (nblk + 1);
   for (int64_t p = lane; p < len; p += 64) {
     const int64_t bc = Air[base + p] / RB;
     const int64_t bp = p > 0 ? Air[base + p - 1] / RB : -1;
@@ -820,10 +836,10 @@ struct Plan {  // device arrays describing C = A*B (B's nonzero column slots, ta
   int32_t* order = nullptr;   // ntasks: launch order
   int64_t* nnz = nullptr;     // nzcB + 1
   int64_t* Ccp = nullptr;     // nzcB + 1
-  int32_t* Ablk = nullptr;    // A's row-block table (A.n x ablk_w), built when a column is split
-  int64_t ablk_w = 0;
+  int32_t* hidx = nullptr;    // hub row-block table of A (see hub_fill_kernel)
+  int32_t* htab = nullptr;
+  int64_t nblk = 0;
   int32_t RB = 1;
-  void* Apk = nullptr;        // numeric: A as PkRec records (built by the first numeric call)
   int64_t* goff = nullptr;    // ntasks + 1: HBM cursor-state offsets of chunked tasks (null: none)
   int64_t* gcur0 = nullptr;
   int64_t* gcur1 = nullptr;
@@ -841,9 +857,10 @@ static TaskArgs task_args(const cbh_mat* A, const cbh_mat* B, const Plan& P, cbh
   a.Bir = B->ir;
   a.Bnum = B->num;
   a.order = P.order;
-  a.Ablk = P.Ablk;
-  a.ablk_w = P.ablk_w;
-  a.RB = P.Ablk ? P.RB : 0;
+  a.hidx = P.hidx;
+  a.htab = P.htab;
+  a.nblk = P.nblk;
+  a.RB = P.htab ? P.RB : 0;
   a.tcol = P.tcol;
   a.tlo = P.tlo;
   a.thi = P.thi;
@@ -905,13 +922,27 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   hipLaunchKernelGGL(task_fill_kernel, dim3(blocks_for(n, 4)), dim3(256), 0, ctx->stream, P.tstart, P.flop, P.rmin,
                      P.rmax, B->cp, n, P.RB, P.tcol, P.tlo, P.thi, P.tfull, P.twork, P.tunits);
   CBH_HIP(ctx, hipGetLastError());
-  if (P.ntasks > n) {  // some column is split: row-block table of A for the aligned task boundaries
-    const int64_t nblk = (A->m + P.RB - 1) / P.RB;
-    P.ablk_w = nblk + 1;
-    CBH_TRY(S.get(&P.Ablk, (size_t)std::max<int64_t>(A->n, 1) * (size_t)P.ablk_w));
-    hipLaunchKernelGGL(ablk_kernel, dim3(blocks_for(A->n, 4)), dim3(256), 0, ctx->stream, P.Adense, A->ir, A->n, P.RB,
-                       nblk, P.Ablk);
-    CBH_HIP(ctx, hipGetLastError());
+  {  // row-block table of A's hub columns: task boundaries and long-segment stops
+    int64_t *hflag, *hpos;
+    CBH_TRY(S.get(&hflag, A->n + 1));
+    CBH_TRY(S.get(&hpos, A->n + 1));
+    CBH_TRY(S.get(&P.hidx, std::max<int64_t>(A->n, 1)));
+    hipLaunchKernelGGL(hub_flag_kernel, dim3(blocks_for(A->n, 256)), dim3(256), 0, ctx->stream, P.Adense, A->n, kHubMin,
+                       hflag);
+    CBH_HIP(ctx, hipMemsetAsync(hflag + A->n, 0, sizeof(int64_t), ctx->stream));
+    CBH_TRY(exclusive_scan_i64(ctx, S, hflag, hpos, A->n + 1));
+    int64_t nhub = 0;
+    CBH_HIP(ctx, hipMemcpyAsync(&nhub, hpos + A->n, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (nhub > 0) {
+      P.nblk = (A->m + P.RB - 1) / P.RB;
+      hipLaunchKernelGGL(hub_index_kernel, dim3(blocks_for(A->n, 256)), dim3(256), 0, ctx->stream, hflag, hpos, A->n,
+                         P.hidx);
+      CBH_TRY(S.get(&P.htab, (size_t)nhub * (size_t)(P.nblk + 1)));
+      hipLaunchKernelGGL(hub_fill_kernel, dim3(blocks_for(A->n, 4)), dim3(256), 0, ctx->stream, P.Adense, A->ir, P.hidx,
+                         A->n, P.RB, P.nblk, P.htab);
+      CBH_HIP(ctx, hipGetLastError());
+    }
   }
   {  // HBM cursor state for tasks with more B entries than the smallest chunk (EMAX)
     int64_t* gcnt;
@@ -968,21 +999,11 @@ template <class SR>
 static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat* B, Plan& P, int64_t t0, int64_t t1,
                        int64_t cbase, int32_t* Cir, void* Cnum, int64_t* launches, int64_t ccap) {
   if (t1 <= t0) return CBH_OK;
-  using VT = typename SR::val_t;
-  if (kPackedA && !P.Apk) {  // row + value records of A, shared by every phase of this product
-    PkRec<VT>* pk;
-    CBH_TRY(S.get(&pk, (size_t)std::max<int64_t>(A->nnz, 1)));
-    hipLaunchKernelGGL(pack_rec_kernel<VT>, dim3(blocks_for(A->nnz, 256)), dim3(256), 0, ctx->stream, A->ir,
-                       reinterpret_cast<const VT*>(A->num), A->nnz, pk);
-    CBH_HIP(ctx, hipGetLastError());
-    P.Apk = pk;
-  }
   BinLists bl;
   CBH_TRY(make_bins(ctx, S, P.tcnt + t0, t1 - t0, t0, P.order, &bl, BinCaps{kSmallCap, kSmallCap}, P.tunits + t0));
   TaskArgs a = task_args(A, B, P, ctx);
   a.twork = P.tcnt;
   a.toff = P.toff;
-  a.Apk = P.Apk;
   a.cbase = cbase;
   a.Cir = Cir;
   a.Cnum = Cnum;

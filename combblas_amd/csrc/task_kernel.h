@@ -9,9 +9,11 @@
 // Inside a task the range is processed in SUB-TILES that fit one LDS table, one after another.
 // Every B entry k of the column keeps, in LDS, a cursor into its row-sorted A column and the row
 // at that cursor: an entry with no product in the current sub-tile costs one LDS read (no global
-// traffic), an active one gallops forward from its cursor. Products of a sub-tile are flattened
-// (LDS scan of segment lengths), each thread gathers U of them before any table update
-// (memory-level parallelism), and an owner map (segment starts + block max-scan) names the entry.
+// traffic); an active one finds the end of its segment (stop_search: 8 independent row loads,
+// then, for long A columns, the row-block table of the hub columns bounds the search to one
+// block). Products of a sub-tile are flattened (LDS scan of segment lengths), each thread
+// gathers U of them before any table update (memory-level parallelism), and an owner map
+// (segment starts + block max-scan) names the entry.
 //
 //   symbolic (MODE_TSYM): distinct rows of the task -> cnt[task]        [estimateNNZ_Hash, mtSpGEMM.h:806-933]
 //            sub-tile = an LDS bitmap over 32*T rows (exact, no hashing) or, for sparse ranges,
@@ -24,40 +26,17 @@
 //            Commit without sorting: keys in different runs of occupied slots are already in
 //            order, so slot s goes to (occupied slots before its run) + (rank of
 //            its key inside the run) -- replaces the per-column std::sort (mtSpGEMM.h:434).
-// Columns with more than EMAX entries are processed in entry chunks whose cursors are re-derived
-// by binary search every sub-tile (slower path; rare on R-MAT: 16 % of scale-22 flops).
+// Columns with more than EMAX entries are processed in entry chunks whose cursors live in HBM
+// between sub-tiles (double-buffered, so that a retried sub-tile restarts from committed ones).
 #pragma once
 #include "tile_kernel.h"
-
-// CBH_ABL (diagnostic builds only, combblas_amd/build.py --variant): bit 0 skips the numeric
-// commit loop, bit 1 the numeric table updates. Results are wrong; only kernel times matter.
-#ifndef CBH_ABL
-#define CBH_ABL 0
-#endif
-// Planned numeric sub-tile fill, in eighths of the T home slots (the table has T + kGuard slots).
-#ifndef CBH_KWIN
-#define CBH_KWIN 8  // numeric commit: neighbour slots read on either side of an occupied slot
-#endif
-#ifndef CBH_RBC
-#define CBH_RBC 0  // numeric insert: 1 = read the slot before the CAS (diagnostic A/B)
-#endif
-#ifndef CBH_CQ
-#define CBH_CQ 1  // numeric commit: 1 = per-wave queue of occupied slots, committed 64 at a time
-#endif
-#ifndef CBH_VCLR
-#define CBH_VCLR 0  // 1 = the numeric commit resets the values it reads (the clear skips them)
-#endif
-#ifndef CBH_EQ
-#define CBH_EQ 0  // 1 = block-wide queue of the entries active in a sub-tile for the segment probe
-#endif
-#ifndef CBH_FILL
-#define CBH_FILL 4
-#endif
 
 namespace cbh {
 
 enum : int { MODE_TSYM = 0, MODE_TNUM = 1 };
 constexpr int32_t kNoRow = 0x7fffffff;
+constexpr int kFill8 = 4;  // numeric sub-tile: planned outputs, in eighths of the T home slots
+constexpr int kWin = 8;    // numeric commit: neighbour slots read on either side of an occupied slot
 
 // Diagnostic build only (-DCBH_STAMPS, libcombblas_hip_stamps.so): thread 0 of every workgroup
 // adds the s_memtime cycles of each kernel phase (delimited by block barriers) into g_stamps.
@@ -81,14 +60,17 @@ struct TaskArgs {
   const int64_t* Acp;  // A dense column pointers (A.n + 1)
   const int32_t* Air;
   const void* Anum;
-  const void* Apk;     // numeric: A as PkRec<val_t> records (row + value interleaved)
   const int64_t* Bcp;  // B DCSC column pointers (per nonzero column slot)
   const int32_t* Bir;
   const void* Bnum;
   const int32_t* order;  // task ids in launch order
   int64_t norder;
-  const int32_t* Ablk;   // row-block table of A: Ablk[k*ablk_w + b] = first position of A(:,k), relative
-  int64_t ablk_w;        // to its start, with row >= b*RB (b = 0..nblk); RB = 0: no table
+  // row-block table of the HUB columns of A (>= kHubMin entries): hidx[k] = hub id or -1,
+  // htab[h*(nblk+1) + b] = first position of A(:,k), relative to its start, whose row is
+  // >= b*RB (b = 0..nblk). Task boundaries sit on multiples of RB; RB = 0: no table.
+  const int32_t* hidx;
+  const int32_t* htab;
+  int64_t nblk;
   int32_t RB;
   const int32_t* tcol;   // per task: column slot j
   const int32_t* tlo;    // per task: row range [lo, hi)
@@ -105,112 +87,75 @@ struct TaskArgs {
   int64_t nnzA, ncolA, ntasks;
   // chunked tasks (more than EMAX entries): entry cursors kept in HBM between sub-tiles, double
   // buffered so that a retried sub-tile restarts from the last committed cursors; goff = per-task
-  // offset into them (null: cursors are re-derived from A every sub-tile)
+  // offset into them
   const int64_t* goff;
   int64_t* gcur0;
   int64_t* gcur1;
   int64_t* gend;
 };
 
-// Numeric gather layout: A's row id and value interleaved in one record, so that a product (and
-// the row reads of the cursor searches next to it) touches ONE cache line instead of one line of
-// ir and one of num. At scale 22 most per-sub-tile segments hold 1-3 products, so the split
-// layout fetched two partly used lines per product (PMC: 1.2 TB read per numeric launch for
-// 0.5 TB of algorithmic bytes). 16 B records for 8-byte values, 8 B otherwise.
-// Measured at scale 22 (round 1): 4 % slower than the split arrays while the cursor gallops read
-// rows (16-byte stride -> 4x the lines of ir); kept behind this switch for the speculative-segment
-// variant, which reads rows only next to the products.
-constexpr bool kPackedA = false;
-template <class V>
-struct PkRec {
-  int32_t r;
-  V v;
-};
-typedef int32_t v4i __attribute__((ext_vector_type(4)));
-typedef int32_t v2i __attribute__((ext_vector_type(2)));
-template <class V>
-__device__ __forceinline__ void ld_rec(const PkRec<V>* __restrict__ p, int32_t& r, V& v) {
-  static_assert(sizeof(PkRec<V>) == 16 || sizeof(PkRec<V>) == 8, "record size");
-  if constexpr (sizeof(PkRec<V>) == 16) {
-    const v4i x = *reinterpret_cast<const v4i*>(p);
-    r = x[0];
-    const uint64_t bits = (uint64_t)(uint32_t)x[2] | ((uint64_t)(uint32_t)x[3] << 32);
-    __builtin_memcpy(&v, &bits, sizeof(V));
-  } else {
-    const v2i x = *reinterpret_cast<const v2i*>(p);
-    r = x[0];
-    const uint32_t bits = (uint32_t)x[1];
-    __builtin_memcpy(&v, &bits, sizeof(V));  // little endian: the low bytes hold a 1- or 4-byte value
-  }
-}
-template <class V>
-__global__ void pack_rec_kernel(const int32_t* __restrict__ ir, const V* __restrict__ num, int64_t nnz,
-                                PkRec<V>* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nnz) return;
-  PkRec<V> x{};
-  x.r = ir[i];
-  x.v = num[i];
-  out[i] = x;
-}
-
-// first q in [lo, hi) with rows[q*S] >= key (rows sorted; S = stride in dwords: 1 for ir, the
-// record size for packed records); global memory, 64-bit positions. Plain binary search: an 8-ary
-// form (7 independent probes per level) measured slower at scale 22 -- the extra cache lines it
-// touches cost more than the latency it hides.
-template <int S>
+// first q in [lo, hi) with rows[q] >= key (rows sorted); global memory, 64-bit positions.
 __device__ __forceinline__ int64_t lb_rows64(const int32_t* __restrict__ rows, int64_t lo, int64_t hi, int32_t key) {
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    if (rows[mid * S] < key) lo = mid + 1;
+    if (rows[mid] < key) lo = mid + 1;
     else hi = mid;
   }
   return lo;
 }
-// galloping lower bound from lo (rows[(lo-1)*S] < key is known): lo, lo+1, lo+3, lo+7, ...
-template <int S>
+// galloping lower bound from lo (rows[lo-1] < key is known): lo, lo+1, lo+3, lo+7, ...
 __device__ __forceinline__ int64_t gallop64(const int32_t* __restrict__ rows, int64_t lo, int64_t hi, int32_t key) {
   int64_t step = 1, prev = lo;
   int64_t nx = lo;
   while (nx < hi) {
-    if (rows[nx * S] >= key) return lb_rows64<S>(rows, prev, nx, key);
+    if (rows[nx] >= key) return lb_rows64(rows, prev, nx, key);
     prev = nx + 1;
     nx = lo + step;
     step <<= 1;
   }
-  return lb_rows64<S>(rows, prev, hi, key);
+  return lb_rows64(rows, prev, hi, key);
 }
 
-// Segment stop without a dependent chain: the W rows after lo are loaded at once (independent
-// loads, mostly one cache line) and the stop is the count of them below key (rows are sorted).
-// At scale 22 a sub-tile segment holds 1-3 products, so one round trip settles nearly every
-// entry; the galloping search above needed 3-5 dependent round trips. Longer segments fall back
-// to galloping. Also returns the row at the stop (kNoRow past hi), the next sub-tile's cursor row.
-#ifndef CBH_GALLOP
-#define CBH_GALLOP 0  // diagnostic builds: 1 = the galloping search alone (round-1 behaviour)
-#endif
-template <int S, int W>
-__device__ __forceinline__ int64_t probe_stop64(const int32_t* __restrict__ rows, int64_t lo, int64_t hi, int32_t key,
-                                                int32_t& row_at) {
-  if constexpr (!CBH_GALLOP) {
-    int32_t v[W];
+// End of an active entry's segment inside the sub-tile: first q in [lo, hi) with rows[q] >= key.
+// The W rows after lo are loaded at once (independent loads, mostly one cache line): at scale 22
+// most segments of short A columns end there in one round trip. Past them, a hub column's
+// row-block table (blk: first position of each RB-row block, relative to the column start
+// `base`) bounds the stop to one block -- a few dozen rows of one or two cache lines -- instead
+// of a galloping search of ~2 log2(segment) dependent loads; short columns gallop. Also returns
+// the row at the stop (kNoRow past hi), the next sub-tile's cursor row.
+template <int W>
+__device__ __forceinline__ int64_t stop_search(const int32_t* __restrict__ rows, int64_t lo, int64_t hi, int32_t key,
+                                               const int32_t* __restrict__ blk, int64_t base, int32_t RB,
+                                               int32_t& row_at) {
+  int32_t v[W];
 #pragma unroll
-    for (int w = 0; w < W; ++w) v[w] = (lo + w < hi) ? rows[(lo + w) * S] : kNoRow;
-    int c = 0;
-    int32_t at = kNoRow;
+  for (int w = 0; w < W; ++w) v[w] = (lo + w < hi) ? rows[lo + w] : kNoRow;
+  int c = 0;
+  int32_t at = kNoRow;
 #pragma unroll
-    for (int w = W - 1; w >= 0; --w) {
-      c += v[w] < key ? 1 : 0;
-      at = v[w] >= key ? v[w] : at;
-    }
-    if (c < W) {
-      row_at = at;
-      return lo + c;
-    }
-    lo += W;
+  for (int w = W - 1; w >= 0; --w) {
+    c += v[w] < key ? 1 : 0;
+    at = v[w] >= key ? v[w] : at;
   }
-  const int64_t stop = gallop64<S>(rows, lo, hi, key);
-  row_at = stop < hi ? rows[stop * S] : kNoRow;
+  if (c < W) {
+    row_at = at;
+    return lo + c;
+  }
+  lo += W;
+  int64_t stop;
+  if (blk != nullptr) {
+    const int32_t b = key / RB;
+    const int64_t s0 = base + blk[b];
+    if (key % RB == 0) {
+      stop = s0 > lo ? s0 : lo;  // s0 is exactly the first row >= key (>= lo: rows[lo-1] < key)
+    } else {
+      const int64_t s1 = base + blk[b + 1];
+      stop = lb_rows64(rows, s0 > lo ? s0 : lo, s1 < hi ? s1 : hi, key);
+    }
+  } else {
+    stop = gallop64(rows, lo, hi, key);
+  }
+  row_at = stop < hi ? rows[stop] : kNoRow;
   return stop;
 }
 
@@ -230,11 +175,11 @@ struct TaskCfg {
   static constexpr size_t o_vals = al(o_keys + sizeof(int32_t) * TA);
   static constexpr size_t o_pos = al(o_vals + (NUM ? sizeof(acc_t) * TA : 0));
   static constexpr size_t o_end = al(o_pos + sizeof(int64_t) * EMAX);
-  static constexpr size_t o_qoff = al(o_end + sizeof(int64_t) * EMAX);
-  static constexpr size_t o_scale = al(o_qoff + sizeof(int64_t) * EMAX);
+  static constexpr size_t o_scale = al(o_end + sizeof(int64_t) * EMAX);
   static constexpr size_t o_next = al(o_scale + (NUM ? sizeof(val_t) * EMAX : 0));
   static constexpr size_t o_next2 = al(o_next + sizeof(int32_t) * EMAX);
-  static constexpr size_t o_off = al(o_next2 + sizeof(int32_t) * EMAX);
+  static constexpr size_t o_col = al(o_next2 + sizeof(int32_t) * EMAX);
+  static constexpr size_t o_off = al(o_col + sizeof(int32_t) * EMAX);
   static constexpr size_t o_own = al(o_off + sizeof(int32_t) * (EMAX + 1));
   static constexpr size_t o_red = al(o_own + sizeof(own_t) * WIN);
   static constexpr size_t bytes = al(o_red + sizeof(int32_t) * (2 * NW + 4));
@@ -248,31 +193,26 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
   constexpr bool NUM = C::NUM;
   constexpr int TA = C::TA, NW = C::NW, WIN = C::WIN;
   static_assert((T & (T - 1)) == 0, "table size must be a power of two");
-  static_assert(!CBH_EQ || WIN >= EMAX, "the entry queue fits the owner map");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int32_t* keys = reinterpret_cast<int32_t*>(smem + C::o_keys);
   uint32_t* words = reinterpret_cast<uint32_t*>(smem + C::o_keys);
   acc_t* vals = reinterpret_cast<acc_t*>(smem + C::o_vals);
-  int64_t* epos = reinterpret_cast<int64_t*>(smem + C::o_pos);    // cursor (absolute index into A)
-  int64_t* eend = reinterpret_cast<int64_t*>(smem + C::o_end);    // end of the A column
-  int64_t* qoff = reinterpret_cast<int64_t*>(smem + C::o_qoff);   // epos - exclusive offset
+  // epos: cursor (absolute index into A); between the segment scan and the end of the sub-tile
+  // it holds cursor - exclusive offset (the gather base of the entry's products)
+  int64_t* epos = reinterpret_cast<int64_t*>(smem + C::o_pos);
+  int64_t* eend = reinterpret_cast<int64_t*>(smem + C::o_end);    // end of the A column in the task
   val_t* escale = reinterpret_cast<val_t*>(smem + C::o_scale);    // B value
   int32_t* enext = reinterpret_cast<int32_t*>(smem + C::o_next);  // row at the cursor (kNoRow: done)
   int32_t* enext2 = reinterpret_cast<int32_t*>(smem + C::o_next2);  // row at the sub-tile's stop
+  int32_t* ecol = reinterpret_cast<int32_t*>(smem + C::o_col);    // A column id
   int32_t* eoff = reinterpret_cast<int32_t*>(smem + C::o_off);
   typename C::own_t* own = reinterpret_cast<typename C::own_t*>(smem + C::o_own);
   int32_t* red = reinterpret_cast<int32_t*>(smem + C::o_red);
   __shared__ int32_t s_ovf;  // overflow flag of the current sub-tile (LDS; read after barriers)
-  __shared__ int32_t s_nq;   // queued active entries of the current chunk (CBH_EQ)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  // row ids of A: the packed records in numeric mode (stride RS dwords), ir in symbolic mode
-  using Rec = PkRec<val_t>;
-  constexpr bool PK = NUM && kPackedA;
-  constexpr int RS = PK ? (int)(sizeof(Rec) / 4) : 1;
-  const int32_t* __restrict__ rowsA = PK ? reinterpret_cast<const int32_t*>(a.Apk) : a.Air;
-  const Rec* __restrict__ recA = reinterpret_cast<const Rec*>(a.Apk);
+  const int32_t* __restrict__ rowsA = a.Air;
 #ifdef CBH_STAMPS
   uint64_t st_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t t_prev_ = __builtin_amdgcn_s_memtime();
@@ -298,7 +238,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
   bool bitmap = false;
   int64_t R;
   {
-    constexpr int64_t cap = NUM ? (int64_t)T * CBH_FILL / 8 : T / 2;  // numeric: outputs per sub-tile
+    constexpr int64_t cap = NUM ? (int64_t)T * kFill8 / 8 : T / 2;  // numeric: outputs per sub-tile
     R = (work + cap - 1) / cap;
     if (!NUM) {
       const int64_t Rb = (span + 32ll * T - 1) / (32ll * T);
@@ -317,67 +257,60 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
   // violated bounds guards are recorded in a register and reported once at the end: a guard_fail
   // (global atomics with return values) inside a hot loop makes the compiler drain vmcnt there
   int bad = 0;  // bit k: guard site k violated
+  auto hub_blk = [&](int32_t k) -> const int32_t* {
+    if (a.RB <= 0) return nullptr;
+    const int32_t h = a.hidx[k];
+    return h >= 0 ? a.htab + (int64_t)h * (a.nblk + 1) : nullptr;
+  };
   // entry state of entries [first, first+cnt): cursor at the first row >= lo
-  const bool gstate = chunked && a.goff != nullptr;
+  const bool gstate = chunked;
   const int64_t go = gstate ? a.goff[task] : 0;
   int par = 0;  // which HBM cursor buffer holds the committed cursors
   auto load_entries = [&](int64_t first, int cnt, int32_t lo, bool lo_is_start, bool from_state) {
-    if (from_state) {  // later sub-tile of a chunked task: cursor and end from HBM, no search
-      const int64_t* gc = par ? a.gcur1 : a.gcur0;
-      for (int i = tid; i < cnt; i += BS) {
-        const int64_t p = e0 + first + i;
-        if constexpr (NUM) escale[i] = reinterpret_cast<const val_t*>(a.Bnum)[p];
-        const int64_t pos = gc[go + first + i], cend = a.gend[go + first + i];
-        epos[i] = pos;
-        eend[i] = cend;
-        enext[i] = pos < cend ? rowsA[pos * RS] : kNoRow;
-      }
-      return;
-    }
     for (int i = tid; i < cnt; i += BS) {
       const int64_t p = e0 + first + i;
       const int32_t k = a.Bir[p];
-      int64_t base = 0, end = 0;
+      if constexpr (NUM) escale[i] = reinterpret_cast<const val_t*>(a.Bnum)[p];
       if (k < 0 || k >= a.ncolA) {
         bad |= 1 << 1;
-      } else {
-        base = a.Acp[k];
-        end = a.Acp[k + 1];
-        if (base < 0 || end < base || end > a.nnzA) {
-          bad |= 1 << 2;
-          base = end = 0;
-        }
+        ecol[i] = 0;
+        epos[i] = eend[i] = 0;
+        enext[i] = kNoRow;
+        continue;
       }
-      if constexpr (NUM) escale[i] = reinterpret_cast<const val_t*>(a.Bnum)[p];
+      ecol[i] = k;
+      if (from_state) {  // later sub-tile of a chunked task: cursor and end from HBM, no search
+        const int64_t* gc = par ? a.gcur1 : a.gcur0;
+        const int64_t pos = gc[go + first + i], cend = a.gend[go + first + i];
+        epos[i] = pos;
+        eend[i] = cend;
+        enext[i] = pos < cend ? rowsA[pos] : kNoRow;
+        continue;
+      }
+      int64_t base = a.Acp[k], end = a.Acp[k + 1];
+      if (base < 0 || end < base || end > a.nnzA) {
+        bad |= 1 << 2;
+        base = end = 0;
+      }
       // the entry is clamped to the task's rows: its end is the first row >= thi. Interior task
-      // boundaries sit on row-block boundaries, so both ends come from the block table (one
-      // load each) instead of a binary search over the A column.
-      const int32_t* blk = (a.RB > 0 && base < end) ? a.Ablk + (int64_t)k * a.ablk_w : nullptr;
+      // boundaries sit on row-block boundaries, so a hub column finds both ends in its block
+      // table (one load each); short columns bisect.
+      const int32_t* blk = base < end ? hub_blk(k) : nullptr;
       int64_t cend = end;
       if (!(full & 2) && base < end) {
         if (blk && thi % a.RB == 0) cend = base + blk[thi / a.RB];
-        else cend = lb_rows64<RS>(rowsA, base, end, thi);
+        else cend = lb_rows64(rowsA, base, end, thi);
       }
       int64_t pos = base;
       if (!lo_is_start && base < cend) {
-        if (blk) {
-          const int32_t b = lo / a.RB;
-          const int64_t s0 = base + blk[b];
-          if (lo % a.RB == 0) {
-            pos = s0;
-          } else {
-            const int64_t s1 = base + blk[b + 1];
-            pos = lb_rows64<RS>(rowsA, s0, s1 < cend ? s1 : cend, lo);
-          }
-          if (pos > cend) pos = cend;
-        } else {
-          pos = lb_rows64<RS>(rowsA, base, cend, lo);
-        }
+        if (blk && lo % a.RB == 0) pos = base + blk[lo / a.RB];
+        else pos = lb_rows64(rowsA, base, cend, lo);
+        if (pos > cend) pos = cend;
       }
       epos[i] = pos;
       eend[i] = cend;
       if (gstate) a.gend[go + first + i] = cend;
-      enext[i] = pos < cend ? rowsA[pos * RS] : kNoRow;
+      enext[i] = pos < cend ? rowsA[pos] : kNoRow;
     }
   };
 
@@ -396,9 +329,6 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
 
   int32_t lo = tlo;
   int64_t w = wnom;
-  // vals needs a full clear before the first sub-tile and after an overflowed one; a committed
-  // sub-tile leaves it cleared (CBH_VCLR)
-  bool vdirty = true;
   while (lo < thi) {
     const int32_t hi = (int32_t)(((int64_t)lo + w < thi) ? lo + w : thi);
     const bool hi_is_end = hi == thi;  // entry ends are clamped to the task (load_entries)
@@ -410,15 +340,10 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
     } else {
       for (int s = tid; s < TA; s += BS) {
         keys[s] = kEmpty;
-        if constexpr (NUM)
-          if (!CBH_VCLR || vdirty) vals[s] = SR::identity();
+        if constexpr (NUM) vals[s] = SR::identity();
       }
-      vdirty = false;
     }
-    if (tid == 0) {
-      __hip_atomic_store(&s_ovf, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      s_nq = 0;
-    }
+    if (tid == 0) __hip_atomic_store(&s_ovf, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const int count_before = my_count;
     __syncthreads();
     CBH_STAMP(1);
@@ -428,37 +353,10 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
       if (chunked) {
         const int64_t first = (int64_t)ch * EMAX;
         nec = (int)((ne - first) < EMAX ? (ne - first) : EMAX);
-        load_entries(first, nec, lo, lo == tlo && (full & 1), gstate && lo != tlo);
+        load_entries(first, nec, lo, lo == tlo && (full & 1), lo != tlo);
         __syncthreads();
       }
       // segment of every entry inside [lo, hi): idle entries (next row >= hi) cost one LDS read
-#if CBH_EQ
-      // active entries are queued block-wide (in `own`, free until the window loop) so the probe
-      // loads issue from as few waves as there are active entries, not from every wave
-      for (int i = tid; i < nec; i += BS) {
-        const int32_t nx = enext[i];
-        if (nx < hi && !hi_is_end) {
-          own[atomicAdd(&s_nq, 1)] = (typename C::own_t)i;
-        } else {
-          eoff[i] = nx < hi ? (int32_t)(eend[i] - epos[i]) : 0;
-          enext2[i] = nx < hi ? kNoRow : nx;
-        }
-      }
-      __syncthreads();
-      {
-        const int nq = s_nq;
-        for (int j = tid; j < nq; j += BS) {
-          const int i = own[j];
-          const int64_t p = epos[i];
-          int32_t nx2 = enext[i];
-          const int64_t stop = probe_stop64<RS, 8>(rowsA, p + 1, eend[i], hi, nx2);
-          eoff[i] = (int32_t)(stop - p);
-          enext2[i] = nx2;
-        }
-      }
-      __syncthreads();
-      if (tid == 0) s_nq = 0;
-#else
       for (int i = tid; i < nec; i += BS) {
         const int32_t nx = enext[i];
         const int64_t p = epos[i];
@@ -470,17 +368,18 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
             stop = end;
             nx2 = kNoRow;
           } else {
-            stop = probe_stop64<RS, 8>(rowsA, p + 1, end, hi, nx2);
+            const int32_t k = ecol[i];
+            const int32_t* blk = hub_blk(k);
+            stop = stop_search<8>(rowsA, p + 1, end, hi, blk, blk ? a.Acp[k] : 0, a.RB, nx2);
           }
         }
         eoff[i] = (int32_t)(stop - p);
         enext2[i] = nx2;
       }
       __syncthreads();
-#endif
       CBH_STAMP(2);
       block_scan_excl<BS>(eoff, nec, red);
-      for (int i = tid; i < nec; i += BS) qoff[i] = epos[i] - eoff[i];
+      for (int i = tid; i < nec; i += BS) epos[i] -= eoff[i];  // gather base of the entry's products
       const int P = eoff[nec];
       CBH_STAMP(3);
       int carry = -1;  // owner of the product just before the window
@@ -507,14 +406,10 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
           const int x0 = tid + u * BS;
           const int x = x0 < wn ? x0 : 0;
           const int i = own[x];
-          const int64_t q = qoff[i] + w0 + x;
+          const int64_t q = epos[i] + w0 + x;
           ow[u] = i;
-          if constexpr (PK) {
-            ld_rec(recA + q, r[u], av[u]);
-          } else {
-            r[u] = a.Air[q];
-            if constexpr (NUM) av[u] = reinterpret_cast<const val_t*>(a.Anum)[q];
-          }
+          r[u] = a.Air[q];
+          if constexpr (NUM) av[u] = reinterpret_cast<const val_t*>(a.Anum)[q];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -529,20 +424,10 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
           if (bitmap) {
             atomicOr(&words[d >> 5], 1u << (d & 31));
           } else if constexpr (NUM) {
-#if CBH_ABL & 2  // ablation build: gather only, no table update (keeps the loads alive)
-            if (r[u] == kNoRow - 1 && vv == val_t(12345)) bad |= 1 << 30;
-            continue;
-#endif
             uint32_t s = (uint32_t)(((uint64_t)d * scale) >> 32);
             bool ok = false;
             for (int probe = 0; probe < kPmax && s < (uint32_t)TA; ++probe, ++s) {
-#if CBH_RBC
-              const int32_t k0 = keys[s];
-              if (k0 != kEmpty && k0 != r[u]) continue;
-              const int32_t k = k0 == kEmpty ? atomicCAS(&keys[s], kEmpty, r[u]) : k0;
-#else
               const int32_t k = atomicCAS(&keys[s], kEmpty, r[u]);
-#endif
               if (k == kEmpty || k == r[u]) {
                 SR::lds_acc(&vals[s], vv);
                 ok = true;
@@ -568,10 +453,13 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         __syncthreads();
         CBH_STAMP(5);
       }
-      if (!bitmap && __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+      if (!bitmap && __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        for (int i = tid; i < nec; i += BS) epos[i] += eoff[i];  // back to the cursors
+        break;
+      }
       if (gstate) {  // this chunk's cursors after the sub-tile, into the other buffer
         int64_t* gn = par ? a.gcur0 : a.gcur1;
-        for (int i = tid; i < nec; i += BS) gn[go + (int64_t)ch * EMAX + i] = qoff[i] + eoff[i + 1];
+        for (int i = tid; i < nec; i += BS) gn[go + (int64_t)ch * EMAX + i] = epos[i] + eoff[i + 1];
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the stores land before the barrier
       }
       if (chunked) __syncthreads();  // entry state is reloaded by the next chunk
@@ -579,7 +467,6 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
     if (!bitmap && __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {  // table could not hold the sub-tile: halve the row range, redo
       __syncthreads();
       my_count = count_before;
-      vdirty = true;
       if (tw == 1) {
         if (tid == 0) atomicOr(&a.err[1], 1);
         return;
@@ -591,7 +478,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
     par ^= gstate ? 1 : 0;  // the cursors written during this sub-tile are now the committed ones
     if (!chunked)  // advance the cursors past the committed sub-tile
       for (int i = tid; i < (int)ne; i += BS) {
-        epos[i] = qoff[i] + eoff[i + 1];
+        epos[i] += eoff[i + 1];
         enext[i] = enext2[i];
       }
     CBH_STAMP(9);
@@ -601,11 +488,11 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
     } else if constexpr (NUM) {
       // rank commit. Slot s holding key x goes to (occupied slots before s) - (s - start of its
       // run) + (keys of its run smaller than x). Wave w owns the 64-aligned slots
-      // [w*SPW, (w+1)*SPW), one slot per lane per step; a lane reads the 8 slots on either side of
-      // its own at once, which gives the run's extent and the rank for every run of <= 17 slots
-      // without a dependent chain (runs crossing a 64-slot step included). Longer runs (clustered
-      // rows) walk LDS. Round 1's DPP-neighbour form walked LDS for every run crossing a step
-      // edge or longer than 5 slots: those serial walks were 30 % of the numeric kernel.
+      // [w*SPW, (w+1)*SPW); its occupied slots are queued in slot order (ballot + prefix
+      // popcount, into enext2: dead until the next sub-tile's entries pass) and committed 64 at
+      // a time, so the window reads run on full waves. A lane reads the kWin slots on either side
+      // of its slot at once, which gives the run's extent and the rank for every run of
+      // <= 2*kWin+1 slots without a dependent chain; longer runs (clustered rows) walk LDS.
       constexpr int SPW = ((TA + NW - 1) / NW + 63) / 64 * 64;
       const int sb = wid * SPW < TA ? wid * SPW : TA;
       const int se = sb + SPW < TA ? sb + SPW : TA;
@@ -626,16 +513,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         tot += rr;
       }
       const uint64_t lt = (1ull << lane) - 1ull;
-      // slot s (occupied, key, val) of the wave's occupied slots in slot order goes to
-      // base - (s - start of its run) + (keys of its run smaller than key)
       auto emit = [&](int s, int32_t key, acc_t val, int64_t base) {
-#if CBH_VCLR
-        vals[s] = SR::identity();  // only this lane reads vals[s]: the next sub-tile's clear skips vals
-#endif
-        // the kWin slots on either side (independent LDS reads, one latency): the run's extent
-        // around s and the keys of it smaller than key, branch-free while the run stays in the
-        // window (runs of <= 2*kWin+1 slots; the LDS walk below covers longer ones)
-        constexpr int kWin = CBH_KWIN;
         int32_t kl[kWin], kr[kWin];
 #pragma unroll
         for (int d = 0; d < kWin; ++d) {
@@ -669,25 +547,15 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         const int64_t pos = base - left + rank;
         if (pos >= out_end || pos >= a.ccap || pos < out_pos) {
           bad |= 1 << 5;
-        } else if ((CBH_ABL & 4) && key != kNoRow - 7) {  // ablation build: no stores
-          bad |= (key == kNoRow - 3 && val == acc_t(12345)) ? 1 << 29 : 0;
         } else {
           a.Cir[pos] = key;
           reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(val);
         }
       };
-#if CBH_CQ
-      // occupied slots are queued per wave (slot order, in enext2: dead until the next sub-tile's
-      // entries pass) and committed 64 at a time, so the window reads run on full waves instead of
-      // on the ~half of the lanes whose slot is occupied
       static_assert(NW * 128 * sizeof(int16_t) <= EMAX * sizeof(int32_t) && TA < 32768, "commit queue");
       int16_t* cq = reinterpret_cast<int16_t*>(enext2) + wid * 128;
       int qn = 0;  // queued slots (wave-uniform)
-#if CBH_ABL & 1  // ablation build: no commit loop
-      for (int s0 = se; s0 < se; s0 += 64) {
-#else
       for (int s0 = sb; s0 < se; s0 += 64) {
-#endif
         const int s = s0 + lane;
         const bool occ = s < se && keys[s] != kEmpty;
         const uint64_t mask = __ballot(occ);
@@ -709,22 +577,6 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         const int sq = cq[lane];
         emit(sq, keys[sq], vals[sq], o + lane);
       }
-#else
-#if CBH_ABL & 1  // ablation build: no commit loop
-      for (int s0 = se; s0 < se; s0 += 64) {
-#else
-      for (int s0 = sb; s0 < se; s0 += 64) {
-#endif
-        const int s = s0 + lane;
-        const bool in = s < se;
-        const int32_t key = in ? keys[s] : kEmpty;
-        const acc_t val = in ? vals[s] : SR::identity();
-        const bool occ = key != kEmpty;
-        const uint64_t mask = __ballot(occ);
-        if (occ) emit(s, key, val, o + __popcll(mask & lt));
-        o += __popcll(mask);
-      }
-#endif
       out_pos += tot;
     }
     lo = hi;
@@ -736,9 +588,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
     const int total = block_sum_int<NW>(my_count, red);
     if (tid == 0) a.cnt[task] = total;
   } else {
-#if !(CBH_ABL & 2)
     if (tid == 0 && out_pos != out_end) atomicAdd(&a.err[0], 1);
-#endif
   }
   if (bad) guard_fail(a.err, 31 - __clz(bad), c, bad, lo);
 #ifdef CBH_STAMPS
