@@ -728,6 +728,27 @@ __global__ void add_i64_kernel(const int64_t* __restrict__ x, const int64_t* __r
   if (i < n) o[i] = x[i] + y[i];
 }
 
+// numeric tasks split between the dense (bitmap-rank) and the hash kernels: wd / wh = the task's
+// output count in the kernel it goes to, 0 in the other
+__global__ void dense_split_kernel(const int64_t* __restrict__ tcnt, const int32_t* __restrict__ tlo,
+                                   const int32_t* __restrict__ thi, int64_t n, int64_t T, int64_t capd, int64_t nwb,
+                                   int64_t smallcap, int enable, int64_t* __restrict__ wd, int64_t* __restrict__ wh) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int64_t w = tcnt[t];
+  const bool d = enable && w > smallcap && dense_subtiles(w, (int64_t)thi[t] - tlo[t], T, capd, nwb) > 0;
+  wd[t] = d ? w : 0;
+  wh[t] = d ? 0 : w;
+}
+// CBH_DENSE=0 keeps every numeric task on the hash kernels (A/B switch)
+static bool kDenseEnabled() {
+  static int v = [] {
+    const char* e = std::getenv("CBH_DENSE");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v != 0;
+}
+
 // task-kernel configurations: T slots, BS threads, EMAX entries per chunk, U products per thread
 struct TSymSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 #ifndef CBH_SYM_U
@@ -805,6 +826,7 @@ static int launch_task_diag(cbh_ctx* ctx, const TaskArgs& a, const BinLists& bl,
       (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
       double tot = 0;
       for (int k = 0; k < 12; ++k) tot += (double)hs[k];
+      std::fprintf(stderr, "[cbh stamps]   chunk-subtiles=%llu overflows=%llu products=%llu\n", hs[13], hs[14], hs[15]);
       std::fprintf(stderr, "[cbh stamps]   wg=%llu cyc/wg=%.0f  setup %.1f%% clear %.1f%% entries %.1f%% scan %.1f%% own %.1f%% products %.1f%% | ovf-check %.1f%% cursor+count %.1f%% place %.1f%% end-sync %.1f%% | tail %.1f%%\n",
                    hs[12], tot / std::max(1ull, hs[12]), 100 * hs[0] / tot, 100 * hs[1] / tot, 100 * hs[2] / tot,
                    100 * hs[3] / tot, 100 * hs[4] / tot, 100 * hs[5] / tot, 100 * hs[8] / tot, 100 * hs[9] / tot,
@@ -999,8 +1021,24 @@ template <class SR>
 static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat* B, Plan& P, int64_t t0, int64_t t1,
                        int64_t cbase, int32_t* Cir, void* Cnum, int64_t* launches, int64_t ccap) {
   if (t1 <= t0) return CBH_OK;
-  BinLists bl;
-  CBH_TRY(make_bins(ctx, S, P.tcnt + t0, t1 - t0, t0, P.order, &bl, BinCaps{kSmallCap, kSmallCap}, P.tunits + t0));
+  // tasks whose sub-tiles fit a bitmap run the dense (bitmap-rank) kernel, the rest the hash
+  // kernels (task_kernel.h dense_subtiles: the same plan the kernel re-derives)
+  using CD = TaskCfg<SR, TNumLarge::T, TNumLarge::BS, TNumLarge::EMAX, TNumLarge::U, MODE_TDENSE>;
+  const int64_t nt = t1 - t0;
+  int64_t *wd, *wh;
+  CBH_TRY(S.get(&wd, nt));
+  CBH_TRY(S.get(&wh, nt));
+  hipLaunchKernelGGL(dense_split_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.tcnt + t0, P.tlo + t0,
+                     P.thi + t0, nt, (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSmallCap,
+                     kDenseEnabled() ? 1 : 0, wd, wh);
+  CBH_HIP(ctx, hipGetLastError());
+  BinLists bd, bl;
+  CBH_TRY(make_bins(ctx, S, wd, nt, t0, P.order, &bd, BinCaps{kSmallCap, kSmallCap}, P.tunits + t0));
+  const int64_t nd = bd.small_count + bd.mid_count + bd.large_count;
+  CBH_TRY(make_bins(ctx, S, wh, nt, t0, P.order + nd, &bl, BinCaps{kSmallCap, kSmallCap}, P.tunits + t0));
+  bl.small_first += nd;
+  bl.mid_first += nd;
+  bl.large_first += nd;
   TaskArgs a = task_args(A, B, P, ctx);
   a.twork = P.tcnt;
   a.toff = P.toff;
@@ -1010,12 +1048,19 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
   a.ccap = ccap;
   // algorithmic bytes: (s_i+s_v) * (nnz(B) + flops + nnz(C)) + pointers
   constexpr double eb = 4.0 + sizeof(typename SR::val_t);
+  const double nb_d = eb * bd.units[2] + 16.0 * bd.large_count;
   const double nb_l = eb * bl.units[2] + 16.0 * bl.large_count;
   const double nb_s = eb * (bl.units[0] + bl.units[1]) + 16.0 * (bl.small_count + bl.mid_count);
-  if (diag_enabled()) CBH_TRY((launch_task_diag<SR, TNumLarge, MODE_TNUM>(ctx, a, bl, "numeric")));
-  else CBH_TRY((launch_task<SR, TNumLarge, MODE_TNUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
+  if (diag_enabled()) {
+    CBH_TRY((launch_task_diag<SR, TNumLarge, MODE_TDENSE>(ctx, a, bd, "numeric dense")));
+    CBH_TRY((launch_task_diag<SR, TNumLarge, MODE_TNUM>(ctx, a, bl, "numeric hash")));
+  } else {
+    CBH_TRY((launch_task<SR, TNumLarge, MODE_TDENSE>(ctx, a, bd.large_first, bd.large_count, CBH_K_NUM_DENSE, nb_d)));
+    CBH_TRY((launch_task<SR, TNumLarge, MODE_TNUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
+  }
   CBH_TRY((launch_task<SR, TNumSmall, MODE_TNUM>(ctx, a, bl.small_first, bl.small_count + bl.mid_count,
                                                   CBH_K_NUM_SMALL, nb_s)));
+  if (launches) *launches += (bd.large_count > 0);
   if (launches) *launches += (bl.large_count > 0) + (bl.small_count + bl.mid_count > 0);
   return CBH_OK;
 }

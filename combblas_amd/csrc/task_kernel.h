@@ -33,10 +33,16 @@
 
 namespace cbh {
 
-enum : int { MODE_TSYM = 0, MODE_TNUM = 1 };
+enum : int { MODE_TSYM = 0, MODE_TNUM = 1, MODE_TDENSE = 2 };
 constexpr int32_t kNoRow = 0x7fffffff;
 constexpr int kFill8 = 4;  // numeric sub-tile: planned outputs, in eighths of the T home slots
 constexpr int kWin = 8;    // numeric commit: neighbour slots read on either side of an occupied slot
+// dense sub-tiles of one window keep their products in registers between the bitmap and the value
+// pass (else the value pass gathers them again)
+#ifndef CBH_DENSE_CARRY
+#define CBH_DENSE_CARRY 0
+#endif
+constexpr bool kDenseCarry = CBH_DENSE_CARRY != 0;
 
 // Diagnostic build only (-DCBH_STAMPS, libcombblas_hip_stamps.so): thread 0 of every workgroup
 // adds the s_memtime cycles of each kernel phase (delimited by block barriers) into g_stamps.
@@ -159,14 +165,62 @@ __device__ __forceinline__ int64_t stop_search(const int32_t* __restrict__ rows,
   return stop;
 }
 
+// Exclusive prefix sum of one int per thread over the block (thread order); total = block sum.
+// Uses red[0..NW); all threads must call.
+template <int BS>
+__device__ __forceinline__ int block_excl_sum(int v, int* red, int& total) {
+  constexpr int NW = BS / 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int s = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(s, d);
+    if (lane >= d) s += y;
+  }
+  __syncthreads();  // red may still be read by a previous user
+  if (lane == 63) red[wid] = s;
+  __syncthreads();
+  int wpre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const int r = red[w];
+    wpre += (w < wid) ? r : 0;
+    tot += r;
+  }
+  total = tot;
+  return wpre + s - v;
+}
+
+// Numeric task plan shared by the binning (host launch) and the kernel: a task runs DENSE when a
+// bitmap over each sub-tile's rows fits the NWB LDS words and the sub-tiles it then needs (at
+// most 15/16 of CAPD outputs each) are not more than 5/4 of the hash sub-tiles (T/2 outputs).
+// Returns the dense sub-tile count, or 0 when the task stays on the hash.
+__host__ __device__ inline int64_t dense_subtiles(int64_t work, int64_t span, int64_t T, int64_t capd, int64_t nwb) {
+  if (work <= 0 || span <= 0) return 0;
+  const int64_t cap = T / 2;
+  const int64_t R = (work + cap - 1) / cap;
+  const int64_t cd = capd * 15 / 16;
+  int64_t Rd = (work + cd - 1) / cd;
+  const int64_t Rw = (span + 32 * nwb - 1) / (32 * nwb);
+  Rd = Rd > Rw ? Rd : Rw;
+  return Rd <= R + R / 4 ? Rd : 0;
+}
+
 template <class SR, int T, int BS, int EMAX, int U, int MODE>
 struct TaskCfg {
-  static constexpr bool NUM = MODE == MODE_TNUM;
+  static constexpr bool NUM = MODE != MODE_TSYM;
+  static constexpr bool DENSE = MODE == MODE_TDENSE;
   using val_t = typename SR::val_t;
   using acc_t = typename SR::acc_t;
   static constexpr int TA = NUM ? T + kGuard : T;  // slots (symbolic: 32-bit words, keys or bitmap)
   static constexpr int NW = BS / 64;
   static constexpr int WIN = U * BS;
+  // dense numeric sub-tiles: CAPD outputs (keys + values at the front of the two tables); the
+  // rest of the key table holds the bitmap (NWB words), the rest of the value table the int16
+  // prefix popcounts of the words
+  static constexpr int CAPD = T / 2;
+  static constexpr int NWB = TA - CAPD;
+  static_assert(!NUM || (TA - CAPD) * sizeof(acc_t) >= 2 * (size_t)NWB, "dense prefix array fits");
   // owner map entries are entry indices (< EMAX): 16 bits leave LDS room for larger windows
   using own_t = int16_t;
   static_assert(EMAX < 32768, "owner map entries are 16-bit");
@@ -186,7 +240,7 @@ struct TaskCfg {
 };
 
 template <class SR, int T, int BS, int EMAX, int U, int MODE>
-__global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
+__global__ __launch_bounds__(BS, 2048 / BS) void task_kernel(TaskArgs a) {
   using C = TaskCfg<SR, T, BS, EMAX, U, MODE>;
   using val_t = typename C::val_t;
   using acc_t = typename C::acc_t;
@@ -234,25 +288,34 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
     return;
   }
   const int64_t span = (int64_t)thi - tlo;
-  // sub-tile plan (uniform in rows)
+  const bool chunked = ne > EMAX;
+  const int nchunks = chunked ? (int)((ne + EMAX - 1) / EMAX) : 1;
+  // sub-tile plan (uniform in rows). Numeric sub-tiles are DENSE when a bitmap over the
+  // sub-tile's rows fits LDS without more sub-tiles than the hash needs: distinct rows are marked
+  // in the bitmap first, its prefix popcounts then give every row its output rank directly, so
+  // values accumulate in row order and the commit is a straight copy (no hashing, no probing, no
+  // rank search). Sparse row ranges use the order-preserving hash.
   bool bitmap = false;
+  constexpr bool dense = C::DENSE;
   int64_t R;
   {
-    constexpr int64_t cap = NUM ? (int64_t)T * kFill8 / 8 : T / 2;  // numeric: outputs per sub-tile
+    constexpr int64_t cap = NUM ? (int64_t)T * kFill8 / 8 : T / 2;  // outputs (keys) per sub-tile
     R = (work + cap - 1) / cap;
-    if (!NUM) {
+    if constexpr (!NUM) {
       const int64_t Rb = (span + 32ll * T - 1) / (32ll * T);
       if (Rb <= R) {
         bitmap = true;
         R = Rb;
       }
+    } else if constexpr (dense) {  // the binning chose this kernel with the same plan
+      const int64_t Rd = dense_subtiles(work, span, T, C::CAPD, C::NWB);
+      const int64_t Rw = (span + 32ll * C::NWB - 1) / (32ll * C::NWB);
+      R = Rd > Rw ? Rd : Rw;
     }
     if (R > span) R = span;
     if (R < 1) R = 1;
   }
   const int64_t wnom = (span + R - 1) / R;
-  const bool chunked = ne > EMAX;
-  const int nchunks = chunked ? (int)((ne + EMAX - 1) / EMAX) : 1;
 
   // violated bounds guards are recorded in a register and reported once at the end: a guard_fail
   // (global atomics with return values) inside a hot loop makes the compiler drain vmcnt there
@@ -263,8 +326,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
     return h >= 0 ? a.htab + (int64_t)h * (a.nblk + 1) : nullptr;
   };
   // entry state of entries [first, first+cnt): cursor at the first row >= lo
-  const bool gstate = chunked;
-  const int64_t go = gstate ? a.goff[task] : 0;
+  const int64_t go = chunked ? a.goff[task] : 0;
   int par = 0;  // which HBM cursor buffer holds the committed cursors
   auto load_entries = [&](int64_t first, int cnt, int32_t lo, bool lo_is_start, bool from_state) {
     for (int i = tid; i < cnt; i += BS) {
@@ -309,15 +371,91 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
       }
       epos[i] = pos;
       eend[i] = cend;
-      if (gstate) a.gend[go + first + i] = cend;
+      if (chunked) a.gend[go + first + i] = cend;
       enext[i] = pos < cend ? rowsA[pos] : kNoRow;
     }
   };
+  // segment of every entry inside [lo, hi) (idle entries -- next row >= hi -- cost one LDS read),
+  // then the exclusive scan of the segment lengths; epos becomes the gather base (cursor - offset).
+  // Returns the sub-tile's product count P.
+  auto segments = [&](int nec, int32_t hi, bool hi_is_end) -> int {
+    for (int i = tid; i < nec; i += BS) {
+      const int32_t nx = enext[i];
+      const int64_t p = epos[i];
+      int64_t stop = p;
+      int32_t nx2 = nx;
+      if (nx < hi) {
+        const int64_t end = eend[i];
+        if (hi_is_end) {
+          stop = end;
+          nx2 = kNoRow;
+        } else {
+          const int32_t k = ecol[i];
+          const int32_t* blk = hub_blk(k);
+          stop = stop_search<8>(rowsA, p + 1, end, hi, blk, blk ? a.Acp[k] : 0, a.RB, nx2);
+        }
+      }
+      eoff[i] = (int32_t)(stop - p);
+      enext2[i] = nx2;
+    }
+    __syncthreads();
+    CBH_STAMP(2);
+    block_scan_excl<BS>(eoff, nec, red);
+    for (int i = tid; i < nec; i += BS) epos[i] -= eoff[i];
+    return eoff[nec];
+  };
+  // products of the sub-tile held in registers between the two dense passes (single window)
+  int32_t r[U];
+  val_t av[U];  // numeric: A value * B value (the product), once values are gathered
+  // One sweep over the windows of the current entry set: owner map, gather U products per
+  // thread (all loads in flight), then `upd(u)` for every product this thread holds.
+  auto sweep = [&](int nec, int P, bool with_vals, auto&& upd) {
+    int carry = -1;  // owner of the product just before the window
+    for (int w0 = 0; w0 < P; w0 += WIN) {
+      const int wn = (P - w0) < WIN ? (P - w0) : WIN;
+      for (int x = tid; x < WIN; x += BS) own[x] = (typename C::own_t)((x == 0) ? carry : -1);
+      __syncthreads();
+      for (int i = tid; i < nec; i += BS) {
+        const int s0 = eoff[i];
+        if (s0 >= w0 && s0 < w0 + wn && eoff[i + 1] > s0) own[s0 - w0] = (typename C::own_t)i;
+      }
+      __syncthreads();
+      block_max_scan<BS, WIN>(own, red);
+      carry = own[wn - 1];
+      CBH_STAMP(4);
+      if (__hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+      // branch-free gather: lanes past the window re-read product 0 and are masked afterwards
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int x0 = tid + u * BS;
+        const int x = x0 < wn ? x0 : 0;
+        const int i = own[x];
+        const int64_t q = epos[i] + w0 + x;
+        r[u] = a.Air[q];
+        if constexpr (NUM)
+          if (with_vals) av[u] = SR::multiply(reinterpret_cast<const val_t*>(a.Anum)[q], escale[i]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (tid + u * BS < wn) upd(u);
+      __syncthreads();
+      CBH_STAMP(5);
+    }
+  };
+  auto set_ovf = [&]() { __hip_atomic_store(&s_ovf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
 
   if (!chunked) {
     load_entries(0, (int)ne, tlo, (full & 1) != 0, false);
-    __syncthreads();
   }
+  uint32_t* dwords = words;  // dense: bitmap words past the CAPD keys; int16 prefix past CAPD vals
+  int16_t* dpre = nullptr;
+  if constexpr (NUM) {
+    dwords = reinterpret_cast<uint32_t*>(smem + C::o_keys + sizeof(int32_t) * C::CAPD);
+    dpre = reinterpret_cast<int16_t*>(smem + C::o_vals + sizeof(acc_t) * C::CAPD);
+    if (dense)  // dense accumulators start at the identity; every commit resets what it read
+      for (int s = tid; s < C::CAPD; s += BS) vals[s] = SR::identity();
+  }
+  __syncthreads();
   CBH_STAMP(0);
 
   int64_t out_pos = 0, out_end = 0;
@@ -334,9 +472,11 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
     const bool hi_is_end = hi == thi;  // entry ends are clamped to the task (load_entries)
     const uint32_t tw = (uint32_t)(hi - lo);
     const uint64_t scale = ((uint64_t)T << 32) / (uint64_t)tw;  // numeric order-preserving slot map
-    if (bitmap) {
-      const int nwords = (int)((tw + 31) >> 5);
-      for (int s = tid; s < nwords; s += BS) words[s] = 0u;
+    const int nwd = (int)((tw + 31) >> 5);
+    if (!NUM && bitmap) {
+      for (int s = tid; s < nwd; s += BS) words[s] = 0u;
+    } else if constexpr (dense) {
+      for (int s = tid; s < nwd; s += BS) dwords[s] = 0u;
     } else {
       for (int s = tid; s < TA; s += BS) {
         keys[s] = kEmpty;
@@ -348,6 +488,7 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
     __syncthreads();
     CBH_STAMP(1);
 
+    bool single = false;  // dense, one window, products kept in registers for the value pass
     for (int ch = 0; ch < nchunks; ++ch) {
       int nec = (int)ne;
       if (chunked) {
@@ -356,115 +497,146 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         load_entries(first, nec, lo, lo == tlo && (full & 1), lo != tlo);
         __syncthreads();
       }
-      // segment of every entry inside [lo, hi): idle entries (next row >= hi) cost one LDS read
-      for (int i = tid; i < nec; i += BS) {
-        const int32_t nx = enext[i];
-        const int64_t p = epos[i];
-        int64_t stop = p;
-        int32_t nx2 = nx;
-        if (nx < hi) {
-          const int64_t end = eend[i];
-          if (hi_is_end) {
-            stop = end;
-            nx2 = kNoRow;
-          } else {
-            const int32_t k = ecol[i];
-            const int32_t* blk = hub_blk(k);
-            stop = stop_search<8>(rowsA, p + 1, end, hi, blk, blk ? a.Acp[k] : 0, a.RB, nx2);
-          }
-        }
-        eoff[i] = (int32_t)(stop - p);
-        enext2[i] = nx2;
+      const int P = segments(nec, hi, hi_is_end);
+#ifdef CBH_STAMPS
+      if (tid == 0) {
+        atomicAdd(&g_stamps[13], 1ull);
+        atomicAdd(&g_stamps[15], (unsigned long long)P);
       }
-      __syncthreads();
-      CBH_STAMP(2);
-      block_scan_excl<BS>(eoff, nec, red);
-      for (int i = tid; i < nec; i += BS) epos[i] -= eoff[i];  // gather base of the entry's products
-      const int P = eoff[nec];
+#endif
       CBH_STAMP(3);
-      int carry = -1;  // owner of the product just before the window
-      for (int w0 = 0; w0 < P; w0 += WIN) {
-        const int wn = (P - w0) < WIN ? (P - w0) : WIN;
-        for (int x = tid; x < WIN; x += BS) own[x] = (typename C::own_t)((x == 0) ? carry : -1);
-        __syncthreads();
-        for (int i = tid; i < nec; i += BS) {
-          const int s0 = eoff[i];
-          if (s0 >= w0 && s0 < w0 + wn && eoff[i + 1] > s0) own[s0 - w0] = (typename C::own_t)i;
-        }
-        __syncthreads();
-        block_max_scan<BS, WIN>(own, red);
-        carry = own[wn - 1];
-        CBH_STAMP(4);
-        if (!bitmap && __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-        // gather U products per thread first (all loads in flight), then update the table
-        // (branch-free: lanes past the window re-read product 0 and are masked afterwards)
-        int32_t r[U];
-        int ow[U];
-        val_t av[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int x0 = tid + u * BS;
-          const int x = x0 < wn ? x0 : 0;
-          const int i = own[x];
-          const int64_t q = epos[i] + w0 + x;
-          ow[u] = i;
-          r[u] = a.Air[q];
-          if constexpr (NUM) av[u] = reinterpret_cast<const val_t*>(a.Anum)[q];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (tid + u * BS >= wn) continue;
-          val_t vv{};
-          if constexpr (NUM) vv = SR::multiply(av[u], escale[ow[u]]);
+      if (!NUM && bitmap) {
+        sweep(nec, P, false, [&](int u) {
+          const uint32_t d = (uint32_t)(r[u] - lo);
+          if (d >= tw) bad |= 1 << 8;
+          else atomicOr(&words[d >> 5], 1u << (d & 31));
+        });
+      } else if constexpr (dense) {
+        single = kDenseCarry && !chunked && P <= WIN;
+        sweep(nec, P, single, [&](int u) {
+          const uint32_t d = (uint32_t)(r[u] - lo);
+          if (d >= tw) bad |= 1 << 8;
+          else atomicOr(&dwords[d >> 5], 1u << (d & 31));
+        });
+      } else if constexpr (NUM) {
+        sweep(nec, P, true, [&](int u) {
+          const val_t vv = av[u];
           const uint32_t d = (uint32_t)(r[u] - lo);
           if (d >= tw) {
             bad |= 1 << 8;
-            continue;
+            return;
           }
-          if (bitmap) {
-            atomicOr(&words[d >> 5], 1u << (d & 31));
-          } else if constexpr (NUM) {
-            uint32_t s = (uint32_t)(((uint64_t)d * scale) >> 32);
-            bool ok = false;
-            for (int probe = 0; probe < kPmax && s < (uint32_t)TA; ++probe, ++s) {
-              const int32_t k = atomicCAS(&keys[s], kEmpty, r[u]);
-              if (k == kEmpty || k == r[u]) {
-                SR::lds_acc(&vals[s], vv);
-                ok = true;
-                break;
-              }
+          uint32_t s = (uint32_t)(((uint64_t)d * scale) >> 32);
+          bool ok = false;
+          for (int probe = 0; probe < kPmax && s < (uint32_t)TA; ++probe, ++s) {
+            const int32_t k = atomicCAS(&keys[s], kEmpty, r[u]);
+            if (k == kEmpty || k == r[u]) {
+              SR::lds_acc(&vals[s], vv);
+              ok = true;
+              break;
             }
-            if (!ok) __hip_atomic_store(&s_ovf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          } else {
-            constexpr int LG = __builtin_ctz(T);
-            uint32_t s = ((uint32_t)r[u] * 0x9E3779B1u) >> (32 - LG);
-            bool ok = false;
-            for (int probe = 0; probe < 2 * kPmax; ++probe, s = (s + 1) & (T - 1)) {
-              const int32_t k = atomicCAS(&keys[s], kEmpty, r[u]);
-              if (k == kEmpty) ++my_count;
-              if (k == kEmpty || k == r[u]) {
-                ok = true;
-                break;
-              }
-            }
-            if (!ok) __hip_atomic_store(&s_ovf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           }
-        }
-        __syncthreads();
-        CBH_STAMP(5);
+          if (!ok) set_ovf();
+        });
+      } else {
+        sweep(nec, P, false, [&](int u) {
+          const uint32_t d = (uint32_t)(r[u] - lo);
+          if (d >= tw) {
+            bad |= 1 << 8;
+            return;
+          }
+          constexpr int LG = __builtin_ctz(T);
+          uint32_t s = ((uint32_t)r[u] * 0x9E3779B1u) >> (32 - LG);
+          bool ok = false;
+          for (int probe = 0; probe < 2 * kPmax; ++probe, s = (s + 1) & (T - 1)) {
+            const int32_t k = atomicCAS(&keys[s], kEmpty, r[u]);
+            if (k == kEmpty) ++my_count;
+            if (k == kEmpty || k == r[u]) {
+              ok = true;
+              break;
+            }
+          }
+          if (!ok) set_ovf();
+        });
       }
-      if (!bitmap && __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+      if (__hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
         for (int i = tid; i < nec; i += BS) epos[i] += eoff[i];  // back to the cursors
         break;
       }
-      if (gstate) {  // this chunk's cursors after the sub-tile, into the other buffer
+      if (chunked) {  // this chunk's cursors after the sub-tile, into the other buffer
         int64_t* gn = par ? a.gcur0 : a.gcur1;
         for (int i = tid; i < nec; i += BS) gn[go + (int64_t)ch * EMAX + i] = epos[i] + eoff[i + 1];
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the stores land before the barrier
+        __syncthreads();  // entry state is reloaded by the next chunk
       }
-      if (chunked) __syncthreads();  // entry state is reloaded by the next chunk
     }
-    if (!bitmap && __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {  // table could not hold the sub-tile: halve the row range, redo
+    int dtotal = 0;
+    if constexpr (NUM) {
+      if (dense && !__hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        // output rank of every word's first row: exclusive scan of the bitmap's popcounts
+        constexpr int KW = (C::NWB + BS - 1) / BS;
+        int tsum = 0;
+        for (int k = 0; k < KW; ++k) {
+          const int x = tid * KW + k;
+          tsum += x < nwd ? __popc(dwords[x]) : 0;
+        }
+        int ex = block_excl_sum<BS>(tsum, red, dtotal);
+        for (int k = 0; k < KW; ++k) {
+          const int x = tid * KW + k;
+          if (x < nwd) {
+            dpre[x] = (int16_t)ex;
+            ex += __popc(dwords[x]);
+          }
+        }
+        if (dtotal > C::CAPD) {
+          if (tid == 0) set_ovf();
+        }
+        __syncthreads();
+      }
+      if (dense && !__hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        auto place = [&](int u) {
+          const val_t vv = av[u];
+          const uint32_t d = (uint32_t)(r[u] - lo);
+          if (d >= tw) return;
+          const uint32_t wv = dwords[d >> 5];
+          const int slot = dpre[d >> 5] + __popc(wv & ((1u << (d & 31)) - 1u));
+          keys[slot] = r[u];
+          SR::lds_acc(&vals[slot], vv);
+        };
+        if (single) {
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (tid + u * BS < (int)eoff[ne]) place(u);
+        } else {
+          // value pass over the same products again (second gather, mostly cache hits): the
+          // segments are known -- LDS (one chunk) or the two HBM cursor buffers (chunked)
+          for (int ch = 0; ch < nchunks; ++ch) {
+            int nec = (int)ne;
+            if (chunked) {
+              const int64_t first = (int64_t)ch * EMAX;
+              nec = (int)((ne - first) < EMAX ? (ne - first) : EMAX);
+              const int64_t* gc = par ? a.gcur1 : a.gcur0;
+              const int64_t* gn = par ? a.gcur0 : a.gcur1;
+              for (int i = tid; i < nec; i += BS) {
+                const int64_t pe = e0 + first + i;
+                escale[i] = reinterpret_cast<const val_t*>(a.Bnum)[pe];
+                const int64_t p0 = gc[go + first + i];
+                epos[i] = p0;
+                eoff[i] = (int32_t)(gn[go + first + i] - p0);
+              }
+              __syncthreads();
+              block_scan_excl<BS>(eoff, nec, red);
+              for (int i = tid; i < nec; i += BS) epos[i] -= eoff[i];
+            }
+            sweep(nec, eoff[nec], true, place);
+          }
+        }
+        __syncthreads();
+      }
+    }
+    if (__hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {  // table could not hold the sub-tile: halve the row range, redo
+      if (!chunked && dense)  // the value pass never ran: restore the cursors the bitmap pass moved
+        for (int i = tid; i < (int)ne; i += BS) epos[i] += eoff[i];
       __syncthreads();
       my_count = count_before;
       if (tw == 1) {
@@ -472,19 +644,35 @@ __global__ __launch_bounds__(BS) void task_kernel(TaskArgs a) {
         return;
       }
       w = (tw + 1) / 2;
+#ifdef CBH_STAMPS
+      if (tid == 0) atomicAdd(&g_stamps[14], 1ull);
+#endif
       continue;
     }
     CBH_STAMP(8);
-    par ^= gstate ? 1 : 0;  // the cursors written during this sub-tile are now the committed ones
+    par ^= chunked ? 1 : 0;  // the cursors written during this sub-tile are now the committed ones
     if (!chunked)  // advance the cursors past the committed sub-tile
       for (int i = tid; i < (int)ne; i += BS) {
         epos[i] += eoff[i + 1];
         enext[i] = enext2[i];
       }
     CBH_STAMP(9);
-    if (bitmap) {
-      const int nwords = (int)((tw + 31) >> 5);
-      for (int s = tid; s < nwords; s += BS) my_count += __popc(words[s]);
+    if (!NUM && bitmap) {
+      for (int s = tid; s < nwd; s += BS) my_count += __popc(words[s]);
+    } else if constexpr (dense) {
+      if constexpr (NUM) {  // outputs are already in row order: straight copy
+        for (int i = tid; i < dtotal; i += BS) {
+          const int64_t pos = out_pos + i;
+          if (pos >= out_end || pos >= a.ccap) {
+            bad |= 1 << 5;
+          } else {
+            a.Cir[pos] = keys[i];
+            reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(vals[i]);
+          }
+          vals[i] = SR::identity();
+        }
+        out_pos += dtotal;
+      }
     } else if constexpr (NUM) {
       // rank commit. Slot s holding key x goes to (occupied slots before s) - (s - start of its
       // run) + (keys of its run smaller than x). Wave w owns the 64-aligned slots

@@ -152,13 +152,14 @@ int cbh_ctx_enable_timing(cbh_ctx* ctx, int enable);
 /* Per-kernel-class totals accumulated while timing is enabled: HIP-event time of every launch,
  * launch count, and the ALGORITHMIC bytes those launches processed (SURVEY.md §8(d):
  * (s_i+s_v)*(nnz(B)+flops+nnz(C)) + column pointers; the symbolic pass counts row ids only).  */
-#define CBH_K_SYM_LARGE 0 /* tile_kernel<...,8192,512,512,MODE_SYM>  */
-#define CBH_K_SYM_SMALL 1 /* tile_kernel<...,512,128,256,MODE_SYM>   */
-#define CBH_K_NUM_LARGE 2 /* tile_kernel<SR,4096,512,512,MODE_NUM>   */
-#define CBH_K_NUM_SMALL 3 /* tile_kernel<SR,512,128,256,MODE_NUM>    */
+#define CBH_K_SYM_LARGE 0 /* task_kernel<...,8192,512,512,8,MODE_TSYM>   symbolic, work > 256   */
+#define CBH_K_SYM_SMALL 1 /* task_kernel<...,512,128,256,4,MODE_TSYM>    symbolic, work <= 256  */
+#define CBH_K_NUM_LARGE 2 /* task_kernel<SR,4096,512,512,8,MODE_TNUM>    numeric hash sub-tiles */
+#define CBH_K_NUM_SMALL 3 /* task_kernel<SR,512,128,256,4,MODE_TNUM>     numeric, <= 256 outputs */
 #define CBH_K_MERGE_SYM 4
 #define CBH_K_MERGE_NUM 5
-#define CBH_K_NKINDS 6
+#define CBH_K_NUM_DENSE 6 /* task_kernel<SR,4096,512,512,8,MODE_TDENSE>  numeric bitmap-rank    */
+#define CBH_K_NKINDS 7
 typedef struct cbh_kernel_stat {
   double ms;
   int64_t launches;
