@@ -371,7 +371,10 @@ __global__ __launch_bounds__(BS, 2048 / BS) void task_kernel(TaskArgs a) {
       }
       epos[i] = pos;
       eend[i] = cend;
-      if (chunked) a.gend[go + first + i] = cend;
+      if (chunked) {  // the first sub-tile's cursors are committed state too (dense value pass)
+        a.gend[go + first + i] = cend;
+        (par ? a.gcur1 : a.gcur0)[go + first + i] = pos;
+      }
       enext[i] = pos < cend ? rowsA[pos] : kNoRow;
     }
   };
