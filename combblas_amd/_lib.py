@@ -55,6 +55,16 @@ SIGNATURES = {
     "cbh_ctx_set_allocator": (ctypes.c_int, [ctypes.c_void_p, ALLOC_FN, FREE_FN, ctypes.c_void_p]),
     "cbh_ctx_set_phase_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "cbh_mat_upload": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cbh_dcsc), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_mat_upload_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cbh_dcsc), ctypes.c_int64,
+                                            ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_mat_value_bytes": (ctypes.c_int64, [ctypes.c_void_p]),
+    # user-semiring plans (the numeric launches are C++/HIP: include/combblas_hip/HipSpGEMMDevice.h)
+    "cbh_plan_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_plan_info": (ctypes.c_int, [ctypes.c_void_p, c_int64_p, c_int64_p]),
+    "cbh_plan_numeric": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint32,
+                                        ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]),
+    "cbh_plan_finish": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
+    "cbh_plan_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "cbh_mat_wrap_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cbh_dcsc), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_mat_info": (ctypes.c_int, [ctypes.c_void_p, c_int64_p, c_int64_p, c_int64_p, c_int64_p, ctypes.POINTER(ctypes.c_int)]),
     "cbh_mat_device_arrays": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_void_p)] * 4),

@@ -12,7 +12,7 @@
 //
 // Included once by spgemm.hip (one translation unit).
 #pragma once
-#include "task_kernel.h"
+#include "../../include/combblas_hip/device/task_kernel.h"
 
 namespace cbh {
 

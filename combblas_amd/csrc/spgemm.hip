@@ -22,8 +22,7 @@
 #include <vector>
 
 #include "../../include/combblas_hip.h"
-#include "semiring.h"
-#include "task_kernel.h"
+#include "../../include/combblas_hip/device/numeric.h"
 #include "apps.h"
 #include "convert.h"
 
@@ -67,6 +66,7 @@ struct cbh_ctx {
 struct cbh_mat {
   int64_t m = 0, n = 0, nnz = 0, nzc = 0;
   int dtype = CBH_F64;
+  int64_t vbytes = 8;  // bytes per value (dtype's size; CBH_OPAQUE: the caller's)
   int64_t* cp = nullptr;
   int64_t* jc = nullptr;
   int32_t* ir = nullptr;
@@ -417,7 +417,6 @@ __global__ __launch_bounds__(256) void checksum_kernel(const int64_t* __restrict
 //           8192-key hash, one tile; large: 512 threads, LDS bitmap of 12288 words = 393,216 rows
 //           per tile (heavy columns: <= 11 tiles at scale 22, exact, no hashing).
 // numeric : small (nnz <= 256) 512(+64)-slot table; large: 4096(+64) slots, tiles of <= 2048 outputs.
-constexpr int64_t kSmallCap = 256;
 constexpr int64_t kSymMidCap = 4096;
 struct SymSmall { static constexpr int T = 512, BS = 128, EMAX = 256; };
 struct SymMid { static constexpr int T = 8192, BS = 256, EMAX = 512; };
@@ -703,7 +702,6 @@ __global__ __launch_bounds__(256) void hub_fill_kernel(const int64_t* __restrict
 }
 
 // entries of every task that may run chunked (more than the smallest EMAX), else 0
-constexpr int64_t kChunkMin = 256;
 __global__ void chunk_count_kernel(const int32_t* __restrict__ tcol, const int64_t* __restrict__ Bcp, int64_t ntasks,
                                    int64_t emin, int64_t* __restrict__ cnt) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -749,22 +747,9 @@ static bool kDenseEnabled() {
   return v != 0;
 }
 
-// task-kernel configurations: T slots, BS threads, EMAX entries per chunk, U products per thread
-struct TSymSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
-#ifndef CBH_SYM_U
-#define CBH_SYM_U 8
-#endif
-#ifndef CBH_NUM_U
-#define CBH_NUM_U 8
-#endif
-struct TSymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512, U = CBH_SYM_U; };
-struct TNumSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
-struct TNumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512, U = CBH_NUM_U; };
-static_assert(kChunkMin <= TSymSmall::EMAX && kChunkMin <= TSymLarge::EMAX && kChunkMin <= TNumSmall::EMAX &&
-                  kChunkMin <= TNumLarge::EMAX,
-              "every chunked task needs HBM cursor state");
-// (measured at scale 22: a 1024-thread workgroup with an 8192-slot table, half the sub-tiles,
-// ran 28 % slower than two 512-thread workgroups per CU with 4096 slots)
+// task_kernel launch with optional HIP-event timing (kernel configurations: device/numeric.h;
+// measured at scale 22: a 1024-thread workgroup with an 8192-slot table, half the sub-tiles, ran
+// 28 % slower than two 512-thread workgroups per CU with 4096 slots)
 template <class SR, class CFG, int MODE>
 static int launch_task(cbh_ctx* ctx, const TaskArgs& args, int64_t first, int64_t count, int kind = -1,
                        double bytes = 0) {
@@ -774,23 +759,7 @@ static int launch_task(cbh_ctx* ctx, const TaskArgs& args, int64_t first, int64_
     e0 = next_event(ctx);
     if (e0 != (size_t)-1) (void)hipEventRecord(ctx->evpool[e0], ctx->stream);
   }
-  using C = TaskCfg<SR, CFG::T, CFG::BS, CFG::EMAX, CFG::U, MODE>;
-  auto kern = task_kernel<SR, CFG::T, CFG::BS, CFG::EMAX, CFG::U, MODE>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    CBH_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)C::bytes));
-    attr_set = true;
-  }
-  const int64_t kMaxGrid = 1ll << 30;
-  for (int64_t off = 0; off < count; off += kMaxGrid) {
-    const int64_t n = std::min(kMaxGrid, count - off);
-    TaskArgs b = args;
-    b.order = args.order + first + off;
-    b.norder = n;
-    hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(CFG::BS), C::bytes, ctx->stream, b);
-    CBH_HIP(ctx, hipGetLastError());
-  }
+  CBH_HIP(ctx, (launch_tasks<SR, CFG, MODE>(args, first, count, ctx->stream)));
   if (e0 != (size_t)-1) {
     const size_t e1 = next_event(ctx);
     if (e1 != (size_t)-1) {
@@ -1094,17 +1063,19 @@ static int dispatch_sr(cbh_ctx* ctx, cbh_semiring sr, int dtype, F&& f) {
                                   ", dtype=" + std::to_string(dtype) + ")");
 }
 
-static int new_mat(cbh_ctx* ctx, int64_t m, int64_t n, int64_t nnz, int64_t nzc, int dtype, cbh_mat** out) {
+static int new_mat(cbh_ctx* ctx, int64_t m, int64_t n, int64_t nnz, int64_t nzc, int dtype, cbh_mat** out,
+                   int64_t vbytes = 0) {
   cbh_mat* M = new cbh_mat;
   M->m = m;
   M->n = n;
   M->nnz = nnz;
   M->nzc = nzc;
   M->dtype = dtype;
+  M->vbytes = vbytes > 0 ? vbytes : (int64_t)dtype_size(dtype);
   int rc = dalloc(ctx, &M->cp, nzc + 1);
   if (rc == CBH_OK) rc = dalloc(ctx, &M->jc, nzc);
   if (rc == CBH_OK) rc = dalloc(ctx, &M->ir, nnz);
-  if (rc == CBH_OK) rc = dalloc(ctx, reinterpret_cast<char**>(&M->num), nnz * dtype_size(dtype));
+  if (rc == CBH_OK) rc = dalloc(ctx, reinterpret_cast<char**>(&M->num), nnz * M->vbytes);
   if (rc != CBH_OK) {
     cbh_mat_free(ctx, M);
     return rc;
@@ -1281,6 +1252,7 @@ int cbh_mat_wrap_device(cbh_ctx* ctx, const cbh_dcsc* d, cbh_dtype dtype, cbh_ma
   M->nnz = d->nnz;
   M->nzc = d->nzc;
   M->dtype = dtype;
+  M->vbytes = (int64_t)dtype_size(dtype);
   M->cp = const_cast<int64_t*>(d->cp);
   M->jc = const_cast<int64_t*>(d->jc);
   M->ir = const_cast<int32_t*>(d->ir);
@@ -1317,7 +1289,7 @@ int cbh_mat_copy_out(cbh_ctx* ctx, const cbh_mat* M, int64_t* cp, int64_t* jc, i
   if (cp) CBH_HIP(ctx, hipMemcpyAsync(cp, M->cp, sizeof(int64_t) * (M->nzc + 1), k, ctx->stream));
   if (jc && M->nzc) CBH_HIP(ctx, hipMemcpyAsync(jc, M->jc, sizeof(int64_t) * M->nzc, k, ctx->stream));
   if (ir && M->nnz) CBH_HIP(ctx, hipMemcpyAsync(ir, M->ir, sizeof(int32_t) * M->nnz, k, ctx->stream));
-  if (num && M->nnz) CBH_HIP(ctx, hipMemcpyAsync(num, M->num, dtype_size(M->dtype) * M->nnz, k, ctx->stream));
+  if (num && M->nnz) CBH_HIP(ctx, hipMemcpyAsync(num, M->num, M->vbytes * M->nnz, k, ctx->stream));
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return CBH_OK;
 }
@@ -1333,6 +1305,28 @@ int cbh_mat_free(cbh_ctx* ctx, cbh_mat* M) {
   delete M;
   return CBH_OK;
 }
+
+int cbh_mat_upload_bytes(cbh_ctx* ctx, const cbh_dcsc* h, int64_t value_bytes, cbh_mat** out) {
+  if (!ctx || !h || !out || value_bytes <= 0) return fail(ctx, CBH_E_ARG, "bad upload arguments");
+  if (h->nnz < 0 || h->nzc < 0 || h->m < 0 || h->n < 0) return fail(ctx, CBH_E_DIMMISMATCH, "negative sizes");
+  cbh_mat* M;
+  CBH_TRY(new_mat(ctx, h->m, h->n, h->nnz, h->nzc, CBH_OPAQUE, &M, value_bytes));
+  if (h->nzc > 0) {
+    CBH_HIP(ctx, hipMemcpyAsync(M->cp, h->cp, sizeof(int64_t) * (h->nzc + 1), hipMemcpyHostToDevice, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(M->jc, h->jc, sizeof(int64_t) * h->nzc, hipMemcpyHostToDevice, ctx->stream));
+  } else {
+    CBH_HIP(ctx, hipMemsetAsync(M->cp, 0, sizeof(int64_t), ctx->stream));
+  }
+  if (h->nnz > 0) {
+    CBH_HIP(ctx, hipMemcpyAsync(M->ir, h->ir, sizeof(int32_t) * h->nnz, hipMemcpyHostToDevice, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(M->num, h->num, value_bytes * h->nnz, hipMemcpyHostToDevice, ctx->stream));
+  }
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  *out = M;
+  return CBH_OK;
+}
+
+int64_t cbh_mat_value_bytes(const cbh_mat* M) { return M ? M->vbytes : 0; }
 
 int cbh_spgemm_symbolic(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, int64_t* flops, int64_t* nnzC,
                         int64_t* col_flops_dev, int64_t* col_nnz_dev) {
@@ -1528,6 +1522,143 @@ int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh
     }
     return CBH_OK;
   });
+}
+
+// ---------------------------------------------------------------------------- user-semiring plans
+// The semiring-independent half of cbh_spgemm (symbolic pass, task plan, binning, compaction);
+// the caller launches the numeric kernels of its own semiring in between (device/numeric.h).
+}  // extern "C"
+struct cbh_plan {
+  cbh_ctx* ctx = nullptr;
+  const cbh_mat* A = nullptr;
+  const cbh_mat* B = nullptr;
+  Scratch S;
+  Plan P;
+  int64_t* pos = nullptr;  // nonempty-column positions of C (compaction)
+  int64_t nzcC = 0;
+  explicit cbh_plan(cbh_ctx* c) : ctx(c), S(c) {}
+};
+extern "C" {
+
+int cbh_plan_create(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, cbh_plan** out) {
+  if (!ctx || !A || !B || !out) return fail(ctx, CBH_E_ARG, "null argument");
+  if (A == B) return fail(ctx, CBH_E_MATRIXALIAS, "A and B alias (ParFriends.h:172-179)");
+  if (A->n != B->m) return fail(ctx, CBH_E_DIMMISMATCH, "A.getncol() != B.getnrow()");
+  if (A->m > INT32_MAX) return fail(ctx, CBH_E_DIMMISMATCH, "local row count exceeds 32-bit row ids");
+  *out = nullptr;
+  cbh_plan* p = new cbh_plan(ctx);
+  p->A = A;
+  p->B = B;
+  if (A->nnz > 0 && B->nnz > 0) {
+    const int rc = run_symbolic(ctx, p->S, A, B, p->P);
+    if (rc != CBH_OK) {
+      delete p;
+      return rc;
+    }
+  }
+  *out = p;
+  return CBH_OK;
+}
+
+int cbh_plan_info(const cbh_plan* p, int64_t* flops, int64_t* nnzC) {
+  if (!p) return CBH_E_ARG;
+  if (flops) *flops = p->P.total_flops;
+  if (nnzC) *nnzC = p->P.total_nnz;
+  return CBH_OK;
+}
+
+int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t flags, cbh_mat** C,
+                     cbh_numeric_plan* out) {
+  if (!p || !C || !out || value_bytes <= 0) return fail(p ? p->ctx : nullptr, CBH_E_ARG, "bad plan arguments");
+  cbh_ctx* ctx = p->ctx;
+  Plan& P = p->P;
+  *C = nullptr;
+  std::memset(out, 0, sizeof(*out));
+  out->stream = ctx->stream;
+  if (P.ntasks == 0) {  // empty operand or product: an empty C (mtSpGEMM.h:224-227)
+    CBH_TRY(new_mat(ctx, p->A->m, p->B->n, 0, 0, dtype, C, value_bytes));
+    CBH_HIP(ctx, hipMemsetAsync((*C)->cp, 0, sizeof(int64_t), ctx->stream));
+    return CBH_OK;
+  }
+  int64_t* flag;
+  CBH_TRY(p->S.get(&flag, P.nzcB + 1));
+  CBH_TRY(p->S.get(&p->pos, P.nzcB + 1));
+  hipLaunchKernelGGL(nz_flag_kernel, dim3(blocks_for(P.nzcB + 1, 256)), dim3(256), 0, ctx->stream, P.nnz, P.nzcB + 1,
+                     flag);
+  CBH_TRY(exclusive_scan_i64(ctx, p->S, flag, p->pos, P.nzcB + 1));
+  CBH_HIP(ctx, hipMemcpyAsync(&p->nzcC, p->pos + P.nzcB, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  CBH_TRY(new_mat(ctx, p->A->m, p->B->n, P.total_nnz, P.nzcB, dtype, C, value_bytes));
+  // bins: dense (built-in, lock-free semirings only), then hash large / small
+  using CD = TaskCfg<PlusTimesD<double>, TNumLarge::T, TNumLarge::BS, TNumLarge::EMAX, TNumLarge::U, MODE_TDENSE>;
+  const int64_t nt = P.ntasks;
+  int64_t *wd, *wh;
+  CBH_TRY(p->S.get(&wd, nt));
+  CBH_TRY(p->S.get(&wh, nt));
+  hipLaunchKernelGGL(dense_split_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.tcnt, P.tlo, P.thi, nt,
+                     (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSmallCap,
+                     (kDenseEnabled() && !(flags & CBH_PLAN_NO_DENSE)) ? 1 : 0, wd, wh);
+  CBH_HIP(ctx, hipGetLastError());
+  BinLists bd, bl;
+  CBH_TRY(make_bins(ctx, p->S, wd, nt, 0, P.order, &bd, BinCaps{kSmallCap, kSmallCap}));
+  const int64_t nd = bd.small_count + bd.mid_count + bd.large_count;
+  CBH_TRY(make_bins(ctx, p->S, wh, nt, 0, P.order + nd, &bl, BinCaps{kSmallCap, kSmallCap}));
+  const cbh_mat* A = p->A;
+  const cbh_mat* B = p->B;
+  out->Acp = P.Adense;
+  out->Air = A->ir;
+  out->Anum = A->num;
+  out->Bcp = B->cp;
+  out->Bir = B->ir;
+  out->Bnum = B->num;
+  out->hidx = P.hidx;
+  out->htab = P.htab;
+  out->nblk = P.nblk;
+  out->RB = P.htab ? P.RB : 0;
+  out->tcol = P.tcol;
+  out->tlo = P.tlo;
+  out->thi = P.thi;
+  out->tfull = P.tfull;
+  out->tcnt = P.tcnt;
+  out->toff = P.toff;
+  out->goff = P.goff;
+  out->gcur0 = P.gcur0;
+  out->gcur1 = P.gcur1;
+  out->gend = P.gend;
+  out->err = ctx->d_err;
+  out->nnzA = A->nnz;
+  out->ncolA = A->n;
+  out->ntasks = P.ntasks;
+  out->order = P.order;
+  out->dense_first = bd.large_first;
+  out->dense_count = bd.large_count;
+  out->large_first = nd + bl.large_first;
+  out->large_count = bl.large_count;
+  out->small_first = nd + bl.small_first;
+  out->small_count = bl.small_count + bl.mid_count;
+  return CBH_OK;
+}
+
+int cbh_plan_finish(cbh_plan* p, cbh_mat* C, uint32_t flags) {
+  if (!p || !C) return fail(p ? p->ctx : nullptr, CBH_E_ARG, "bad plan arguments");
+  cbh_ctx* ctx = p->ctx;
+  Plan& P = p->P;
+  if (P.ntasks == 0) return CBH_OK;
+  if (flags & CBH_KEEP_EMPTY_COLS) {
+    CBH_HIP(ctx, hipMemcpyAsync(C->jc, p->B->jc, sizeof(int64_t) * P.nzcB, hipMemcpyDeviceToDevice, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(C->cp, P.Ccp, sizeof(int64_t) * (P.nzcB + 1), hipMemcpyDeviceToDevice, ctx->stream));
+  } else {
+    hipLaunchKernelGGL(compact_cols_kernel, dim3(blocks_for(P.nzcB, 256)), dim3(256), 0, ctx->stream, P.nnz, p->pos,
+                       p->B->jc, P.Ccp, P.nzcB, C->jc, C->cp);
+    C->nzc = p->nzcC;
+  }
+  CBH_HIP(ctx, hipGetLastError());
+  return check_err(ctx);
+}
+
+int cbh_plan_destroy(cbh_plan* p) {
+  delete p;
+  return CBH_OK;
 }
 
 int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* parts, cbh_mat** C) {
@@ -1974,7 +2105,7 @@ extern "C" int cbh_dcsc_to_tuples(cbh_ctx* ctx, const cbh_mat* M, int32_t* rows,
   if (!ctx || !M || (M->nnz > 0 && (!rows || !cols || !vals))) return fail(ctx, CBH_E_ARG, "bad dcsc_to_tuples arguments");
   if (M->nnz == 0) return CBH_OK;
   CBH_HIP(ctx, hipMemcpyAsync(rows, M->ir, sizeof(int32_t) * M->nnz, hipMemcpyDeviceToDevice, ctx->stream));
-  CBH_HIP(ctx, hipMemcpyAsync(vals, M->num, dtype_size(M->dtype) * M->nnz, hipMemcpyDeviceToDevice, ctx->stream));
+  CBH_HIP(ctx, hipMemcpyAsync(vals, M->num, M->vbytes * M->nnz, hipMemcpyDeviceToDevice, ctx->stream));
   hipLaunchKernelGGL(expand_cols_kernel, dim3(blocks_for(M->nzc, 4)), dim3(256), 0, ctx->stream, M->jc, M->cp, M->nzc,
                      cols);
   CBH_HIP(ctx, hipGetLastError());

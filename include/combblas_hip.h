@@ -57,11 +57,12 @@ typedef enum cbh_semiring {
 } cbh_semiring;
 
 typedef enum cbh_dtype {
-  CBH_F64 = 0,  /* double  */
-  CBH_I64 = 1,  /* int64_t */
-  CBH_BOOL = 2, /* bool, one byte per value */
-  CBH_F32 = 3,  /* float   */
-  CBH_I32 = 4   /* int32_t */
+  CBH_F64 = 0,   /* double  */
+  CBH_I64 = 1,   /* int64_t */
+  CBH_BOOL = 2,  /* bool, one byte per value */
+  CBH_F32 = 3,   /* float   */
+  CBH_I32 = 4,   /* int32_t */
+  CBH_OPAQUE = 5 /* a user value type of a fixed byte size (cbh_mat_upload_bytes; user semirings) */
 } cbh_dtype;
 
 /* cbh_spgemm flags */
@@ -100,6 +101,10 @@ int cbh_ctx_set_phase_budget(cbh_ctx* ctx, int64_t bytes);
 
 /* Copy a host DCSC into a new device matrix (SpParHelper::BCastMatrix receive side / upload). */
 int cbh_mat_upload(cbh_ctx* ctx, const cbh_dcsc* host, cbh_dtype dtype, cbh_mat** out);
+/* Copy a host DCSC whose values are an opaque type of value_bytes bytes (a user semiring's NT). */
+int cbh_mat_upload_bytes(cbh_ctx* ctx, const cbh_dcsc* host, int64_t value_bytes, cbh_mat** out);
+/* Bytes per value of a matrix (any dtype). */
+int64_t cbh_mat_value_bytes(const cbh_mat* mat);
 /* Wrap device arrays without copying. The caller keeps them alive until cbh_mat_free. */
 int cbh_mat_wrap_device(cbh_ctx* ctx, const cbh_dcsc* dev, cbh_dtype dtype, cbh_mat** out);
 /* Sizes (host pointers, any may be NULL). */
@@ -167,6 +172,41 @@ typedef struct cbh_kernel_stat {
 } cbh_kernel_stat;
 int cbh_kernel_stats(cbh_ctx* ctx, int kind, cbh_kernel_stat* out);
 int cbh_kernel_stats_reset(cbh_ctx* ctx);
+
+/* ---------------------------------------------------------------- user semirings
+ * LocalHybridSpGEMM<SR,NTO>(SpDCCols<IT,NT1>, SpDCCols<IT,NT2>) for a semiring the library was
+ * not built with (Semirings.h:143-255 contract; NT1 != NT2 promotion). The library runs what
+ * does not depend on the semiring -- the symbolic pass (estimateFLOP + estimateNNZ_Hash), the
+ * task plan, the binning, C's allocation and column compaction -- and the caller launches the
+ * numeric kernels instantiated for its semiring from the header-only device code
+ * (include/combblas_hip/HipSpGEMMDevice.h -> device/numeric.h: cbh::run_numeric_plan<SR>) on
+ * the plan's stream, between cbh_plan_numeric and cbh_plan_finish.                          */
+typedef struct cbh_plan cbh_plan;
+typedef struct cbh_numeric_plan {
+  const int64_t* Acp; const int32_t* Air; const void* Anum;  /* A: dense column pointers, rows, values */
+  const int64_t* Bcp; const int32_t* Bir; const void* Bnum;  /* B: DCSC pointers, rows, values         */
+  const int32_t* hidx; const int32_t* htab; int64_t nblk; int32_t RB; /* hub row-block table      */
+  const int32_t* tcol; const int32_t* tlo; const int32_t* thi; const uint8_t* tfull; /* tasks    */
+  const int64_t* tcnt; const int64_t* toff;                  /* outputs per task, output offsets  */
+  const int64_t* goff; int64_t* gcur0; int64_t* gcur1; int64_t* gend; /* chunked-task cursors    */
+  int* err;                                                  /* device consistency flags          */
+  int64_t nnzA, ncolA, ntasks;
+  const int32_t* order;                                      /* task ids in launch order          */
+  int64_t dense_first, dense_count, large_first, large_count, small_first, small_count;
+  void* stream;                                              /* hipStream_t of the context        */
+} cbh_numeric_plan;
+#define CBH_PLAN_NO_DENSE 0x1u /* bin every task for the hash kernels (locked / user semirings) */
+/* Symbolic pass of C = A*B (A and B values may differ in type); the plan owns its scratch. */
+int cbh_plan_create(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, cbh_plan** plan);
+int cbh_plan_info(const cbh_plan* plan, int64_t* flops, int64_t* nnzC);
+/* Allocate C (value_bytes per value, CBH_OPAQUE unless it matches a built-in dtype the caller
+ * names in dtype) and bin the tasks; fills the launch description. */
+int cbh_plan_numeric(cbh_plan* plan, cbh_dtype dtype, int64_t value_bytes, uint32_t flags, cbh_mat** C,
+                     cbh_numeric_plan* out);
+/* After the caller's numeric launches: C's column pointers / ids (CBH_KEEP_EMPTY_COLS honoured)
+ * and the device-side consistency checks. */
+int cbh_plan_finish(cbh_plan* plan, cbh_mat* C, uint32_t flags);
+int cbh_plan_destroy(cbh_plan* plan);
 
 /* ---------------------------------------------------------------- callers around the hot path
  * (device kernels in combblas_amd/csrc/apps.h)                           */

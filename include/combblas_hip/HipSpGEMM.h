@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstring>
 #include <limits>
+#include <memory>
 #include <tuple>
 #include <type_traits>
 #include <vector>
@@ -36,13 +37,20 @@
 namespace combblas_hip {
 
 // ------------------------------------------------------------------ type/semiring mapping
+inline cbh_ctx* context();
+
+// value type -> dtype code (CBH_OPAQUE for any other trivially copyable type: user semirings)
 template <class NT>
-struct dtype_of;
+struct dtype_of { static constexpr cbh_dtype value = CBH_OPAQUE; };
 template <> struct dtype_of<double> { static constexpr cbh_dtype value = CBH_F64; };
 template <> struct dtype_of<int64_t> { static constexpr cbh_dtype value = CBH_I64; };
 template <> struct dtype_of<float> { static constexpr cbh_dtype value = CBH_F32; };
 template <> struct dtype_of<int32_t> { static constexpr cbh_dtype value = CBH_I32; };
 template <> struct dtype_of<bool> { static constexpr cbh_dtype value = CBH_BOOL; };
+
+inline int upload_dcsc(const cbh_dcsc& h, cbh_dtype dt, int64_t vbytes, cbh_mat** out) {
+  return dt == CBH_OPAQUE ? cbh_mat_upload_bytes(context(), &h, vbytes, out) : cbh_mat_upload(context(), &h, dt, out);
+}
 
 template <class SR>
 struct semiring_traits;  // specialize: static constexpr cbh_semiring code
@@ -106,8 +114,9 @@ cbh_mat* upload(const combblas::SpDCCols<IT, NT>& A) {
   h.ir = ir.data();
   h.num = num.data();
   if (h.m > std::numeric_limits<int32_t>::max()) die(context(), CBH_E_DIMMISMATCH, "local rows exceed int32");
+  static_assert(std::is_trivially_copyable<NT>::value, "device values must be trivially copyable");
   cbh_mat* out = nullptr;
-  int rc = cbh_mat_upload(context(), &h, dtype_of<NT>::value, &out);
+  int rc = upload_dcsc(h, dtype_of<NT>::value, (int64_t)sizeof(NT), &out);
   if (rc != CBH_OK) die(context(), rc, "cbh_mat_upload");
   return out;
 }
@@ -119,9 +128,10 @@ cbh_mat* upload(const combblas::SpTuples<IT, NT>& T) {
   h.m = T.getnrow();
   h.n = T.getncol();
   h.nnz = T.getnnz();
+  if (h.m > std::numeric_limits<int32_t>::max()) die(context(), CBH_E_DIMMISMATCH, "local rows exceed int32");
   std::vector<int64_t> cp(1, 0), jc;
   std::vector<int32_t> ir(h.nnz);
-  std::vector<NT> num(h.nnz);
+  std::unique_ptr<NT[]> num(new NT[h.nnz > 0 ? h.nnz : 1]);  // not std::vector: vector<bool> has no data()
   for (int64_t i = 0; i < h.nnz; ++i) {
     const IT c = T.colindex(i);
     if (jc.empty() || jc.back() != c) {
@@ -136,9 +146,9 @@ cbh_mat* upload(const combblas::SpTuples<IT, NT>& T) {
   h.cp = cp.data();
   h.jc = jc.data();
   h.ir = ir.data();
-  h.num = reinterpret_cast<const void*>(num.data());
+  h.num = reinterpret_cast<const void*>(num.get());
   cbh_mat* out = nullptr;
-  int rc = cbh_mat_upload(context(), &h, dtype_of<NT>::value, &out);
+  int rc = upload_dcsc(h, dtype_of<NT>::value, (int64_t)sizeof(NT), &out);
   if (rc != CBH_OK) die(context(), rc, "cbh_mat_upload");
   return out;
 }
@@ -150,8 +160,8 @@ combblas::SpTuples<IT, NT>* download_tuples(cbh_mat* C) {
   cbh_mat_info(C, &m, &n, &nnz, &nzc, nullptr);
   std::vector<int64_t> cp(nzc + 1), jc(nzc);
   std::vector<int32_t> ir(nnz);
-  std::vector<NT> num(nnz);
-  int rc = cbh_mat_copy_out(context(), C, cp.data(), jc.data(), ir.data(), reinterpret_cast<void*>(num.data()), 0);
+  std::unique_ptr<NT[]> num(new NT[nnz > 0 ? nnz : 1]);
+  int rc = cbh_mat_copy_out(context(), C, cp.data(), jc.data(), ir.data(), reinterpret_cast<void*>(num.get()), 0);
   if (rc != CBH_OK) die(context(), rc, "cbh_mat_copy_out");
   if (nnz == 0) return new combblas::SpTuples<IT, NT>(0, (IT)m, (IT)n);
   auto* tuples = static_cast<std::tuple<IT, IT, NT>*>(::operator new(sizeof(std::tuple<IT, IT, NT>) * nnz));
@@ -203,7 +213,14 @@ combblas::SpTuples<IT, NT>* MultiwayMerge(std::vector<combblas::SpTuples<IT, NT>
                                           bool delarrs = false) {
   const int nlists = (int)lists.size();
   if (nlists == 0) return new combblas::SpTuples<IT, NT>(0, mdim, ndim);
-  if (nlists == 1 && delarrs) return lists[0];  // MultiwayMerge.h:422-425 steals the input
+  if (nlists == 1) {
+    if (delarrs) return lists[0];  // MultiwayMerge.h:422-425 steals the input
+    // MultiwayMerge.h:426-438: a copy of the one list, no dimension check (pure data movement)
+    const int64_t nnz = lists[0]->getnnz();
+    auto* t = new std::tuple<IT, IT, NT>[nnz];
+    for (int64_t i = 0; i < nnz; ++i) t[i] = lists[0]->tuples[i];
+    return new combblas::SpTuples<IT, NT>(nnz, mdim, ndim, t, false);
+  }
   for (int i = 0; i < nlists; ++i)
     if (mdim != lists[i]->getnrow() || ndim != lists[i]->getncol()) {
       std::fprintf(stderr, "Dimensions of SpTuples do not match on multiwayMerge()\n");

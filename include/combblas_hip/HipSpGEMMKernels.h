@@ -1,0 +1,114 @@
+// HipSpGEMMKernels.h -- device half of HipSpGEMMDevice.h: compile ONE translation unit with
+// hipcc that includes "CombBLAS/CombBLAS.h", this header and the semiring definitions, and
+// instantiates the gfx950 kernels of each semiring the application routes to the device:
+//
+//   COMBBLAS_HIP_DEVICE_KERNELS(SR, IT, NT1, NT2, NTO)
+//
+// (the same arguments as COMBBLAS_HIP_INSTANTIATE_DEVICE in the host translation units). Only
+// this definition of combblas_hip::DeviceLocalSpGEMM runs here: the reference drivers stay in
+// the host translation units, built by the application's own compiler.
+#pragma once
+
+#include "HipSpGEMMDevice.h"
+#include "device/numeric.h"
+
+namespace combblas_hip {
+
+// reference semiring type -> device functor
+template <class SR, class NT1, class NT2, class NTO>
+struct device_semiring {
+  using type = cbh::UserSRD<SR, NT1, NT2, NTO>;
+};
+template <class T1, class T2, class NT1, class NT2, class NTO>
+struct device_semiring<combblas::PlusTimesSRing<T1, T2>, NT1, NT2, NTO> {
+  using type = typename std::conditional<std::is_same<NT1, NTO>::value && std::is_same<NT2, NTO>::value,
+                                         cbh::PlusTimesD<NTO>, cbh::PlusTimesPromoteD<NT1, NT2, NTO>>::type;
+};
+
+// SelectMaxSRing / MinPlusSRing with NT1 != NT2: the reference's functions are host-only, so the
+// device functor restates them (Semirings.h:165-187, 235-255) in T_promote = NTO.
+template <class NT1, class NT2, class NTO>
+struct SelectMaxPromoteD {
+  using a_t = NT1;
+  using b_t = NT2;
+  using val_t = NTO;
+  using acc_t = NTO;
+  static constexpr bool kLocked = true;
+  static __device__ __forceinline__ NTO multiply(NT1 a, NT2 b) { return static_cast<NTO>(a) * static_cast<NTO>(b); }
+  static __device__ __forceinline__ NTO add(NTO a, NTO b) { return a < b ? b : a; }
+  static __device__ __forceinline__ NTO identity() { return NTO(); }
+  static __device__ __forceinline__ NTO finalize(NTO a) { return a; }
+};
+template <class NT1, class NT2, class NTO>
+struct MinPlusPromoteD {
+  using a_t = NT1;
+  using b_t = NT2;
+  using val_t = NTO;
+  using acc_t = NTO;
+  static constexpr bool kLocked = true;
+  static __device__ __forceinline__ NTO multiply(NT1 a, NT2 b) {
+    const NTO x = static_cast<NTO>(a), y = static_cast<NTO>(b), inf = std::numeric_limits<NTO>::max();
+    return (x == inf || y == inf) ? inf : x + y;
+  }
+  static __device__ __forceinline__ NTO add(NTO a, NTO b) { return b < a ? b : a; }
+  static __device__ __forceinline__ NTO identity() { return NTO(); }
+  static __device__ __forceinline__ NTO finalize(NTO a) { return a; }
+};
+template <class T1, class T2, class NT1, class NT2, class NTO>
+struct device_semiring<combblas::SelectMaxSRing<T1, T2>, NT1, NT2, NTO> {
+  using type = SelectMaxPromoteD<NT1, NT2, NTO>;
+};
+template <class T1, class T2, class NT1, class NT2, class NTO>
+struct device_semiring<combblas::MinPlusSRing<T1, T2>, NT1, NT2, NTO> {
+  using type = MinPlusPromoteD<NT1, NT2, NTO>;
+};
+
+// C = A*B on the device for any (SR, NT1, NT2, NTO): library plan + caller-instantiated kernels.
+template <class SR, class NTO, class IT, class NT1, class NT2>
+combblas::SpTuples<IT, NTO>* DeviceLocalSpGEMM(const combblas::SpDCCols<IT, NT1>& A,
+                                               const combblas::SpDCCols<IT, NT2>& B, bool clearA, bool clearB) {
+  using DSR = typename device_semiring<SR, NT1, NT2, NTO>::type;
+  static_assert(std::is_trivially_copyable<NTO>::value, "device values must be trivially copyable");
+  const IT mdim = A.getnrow(), ndim = B.getncol();
+  combblas::SpTuples<IT, NTO>* out;
+  if (A.isZero() || B.isZero()) {
+    out = new combblas::SpTuples<IT, NTO>(0, mdim, ndim);  // mtSpGEMM.h:224-227
+  } else {
+    cbh_ctx* ctx = context();
+    MatGuard a, b, c;
+    a.m = upload(A);
+    b.m = upload(B);
+    cbh_plan* plan = nullptr;
+    int rc = cbh_plan_create(ctx, a.m, b.m, &plan);
+    if (rc != CBH_OK) die(ctx, rc, "cbh_plan_create");
+    cbh_numeric_plan np;
+    rc = cbh_plan_numeric(plan, dtype_of<NTO>::value, (int64_t)sizeof(NTO),
+                          cbh::sr_locked<DSR>::value ? CBH_PLAN_NO_DENSE : 0u, &c.m, &np);
+    if (rc != CBH_OK) die(ctx, rc, "cbh_plan_numeric");
+    const int64_t *cp, *jc;
+    const int32_t* ir;
+    const void* num;
+    cbh_mat_device_arrays(c.m, &cp, &jc, &ir, &num);
+    int64_t nnzC = 0;
+    cbh_mat_info(c.m, nullptr, nullptr, &nnzC, nullptr, nullptr);
+    const hipError_t e = cbh::run_numeric_plan<DSR>(np, const_cast<int32_t*>(ir), const_cast<void*>(num), nnzC);
+    if (e != hipSuccess) {
+      std::fprintf(stderr, "combblas_hip: numeric launch failed: %s\n", hipGetErrorString(e));
+      MPI_Abort(MPI_COMM_WORLD, CBH_E_HIP);
+    }
+    rc = cbh_plan_finish(plan, c.m, 0);
+    if (rc != CBH_OK) die(ctx, rc, "cbh_plan_finish");
+    cbh_plan_destroy(plan);
+    out = download_tuples<IT, NTO>(c.m);
+  }
+  if (clearA) delete const_cast<combblas::SpDCCols<IT, NT1>*>(&A);
+  if (clearB) delete const_cast<combblas::SpDCCols<IT, NT2>*>(&B);
+  return out;
+}
+
+}  // namespace combblas_hip
+
+
+#define COMBBLAS_HIP_DEVICE_KERNELS(SR, IT, NT1, NT2, NTO)                                                   \
+  template combblas::SpTuples<IT, NTO>* combblas_hip::DeviceLocalSpGEMM<SR, NTO, IT, NT1, NT2>(            \
+      const combblas::SpDCCols<IT, NT1>&, const combblas::SpDCCols<IT, NT2>&, bool, bool);

@@ -1,0 +1,120 @@
+// numeric.h -- host-side launch of the numeric SpGEMM kernels for one semiring, shared by the
+// library (built-in semirings, combblas_amd/csrc/spgemm.hip) and by user translation units that
+// instantiate the kernels for their own semiring (combblas_hip/HipSpGEMMDevice.h). Compile with
+// hipcc. The symbolic pass, the task plan and its binning stay in libcombblas_hip.so; they reach
+// this code as a cbh_numeric_plan (include/combblas_hip.h, cbh_plan_numeric).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "../../combblas_hip.h"
+#include "task_kernel.h"
+
+namespace cbh {
+
+// task-kernel configurations: T slots, BS threads, EMAX entries per chunk, U products per thread
+struct TSymSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
+struct TSymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512, U = 8; };
+struct TNumSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
+struct TNumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512, U = 8; };
+// wider accumulators (user value types) keep the large table within ~50 KB of LDS
+template <class SR>
+struct TNumLargeFor {
+  static constexpr int bytes = (int)(sizeof(int32_t) + sizeof(typename SR::acc_t));
+  static constexpr int T = bytes <= 12 ? 4096 : (bytes <= 24 ? 2048 : (bytes <= 48 ? 1024 : 512));
+  static constexpr int BS = 512, EMAX = 512, U = 8;
+};
+template <class SR>
+struct TNumSmallFor {
+  static constexpr int bytes = (int)(sizeof(int32_t) + sizeof(typename SR::acc_t));
+  static constexpr int T = bytes <= 48 ? 512 : 256;
+  static constexpr int BS = 128, EMAX = 256, U = 4;
+};
+constexpr int64_t kChunkMin = 256;  // tasks with more B entries than this keep cursors in HBM
+constexpr int64_t kSmallCap = 256;  // numeric tasks with <= kSmallCap outputs run the small kernel
+static_assert(kChunkMin <= TSymSmall::EMAX && kChunkMin <= TSymLarge::EMAX && kChunkMin <= TNumSmall::EMAX &&
+                  kChunkMin <= TNumLarge::EMAX,
+              "every chunked task needs HBM cursor state");
+
+// Launches task_kernel<SR, CFG, MODE> over order[first, first+count) on `stream` (grid slices of
+// at most 2^30 workgroups). The dynamic-LDS attribute is set once per instantiation.
+template <class SR, class CFG, int MODE>
+hipError_t launch_tasks(const TaskArgs& args, int64_t first, int64_t count, hipStream_t stream) {
+  if (count <= 0) return hipSuccess;
+  using C = TaskCfg<SR, CFG::T, CFG::BS, CFG::EMAX, CFG::U, MODE>;
+  auto kern = task_kernel<SR, CFG::T, CFG::BS, CFG::EMAX, CFG::U, MODE>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::bytes);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int64_t kMaxGrid = 1ll << 30;
+  for (int64_t off = 0; off < count; off += kMaxGrid) {
+    const int64_t n = std::min(kMaxGrid, count - off);
+    TaskArgs b = args;
+    b.order = args.order + first + off;
+    b.norder = n;
+    hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(CFG::BS), C::bytes, stream, b);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// Kernel arguments of the numeric pass from the library's plan; C's entries go to Cir/Cnum at
+// toff[task] - cbase.
+inline TaskArgs numeric_args(const cbh_numeric_plan& p, int64_t cbase, int32_t* Cir, void* Cnum, int64_t ccap) {
+  TaskArgs a{};
+  a.Acp = p.Acp;
+  a.Air = p.Air;
+  a.Anum = p.Anum;
+  a.Bcp = p.Bcp;
+  a.Bir = p.Bir;
+  a.Bnum = p.Bnum;
+  a.order = p.order;
+  a.hidx = p.hidx;
+  a.htab = p.htab;
+  a.nblk = p.nblk;
+  a.RB = p.RB;
+  a.tcol = p.tcol;
+  a.tlo = p.tlo;
+  a.thi = p.thi;
+  a.tfull = p.tfull;
+  a.twork = p.tcnt;
+  a.toff = p.toff;
+  a.cbase = cbase;
+  a.Cir = Cir;
+  a.Cnum = Cnum;
+  a.ccap = ccap;
+  a.err = p.err;
+  a.nnzA = p.nnzA;
+  a.ncolA = p.ncolA;
+  a.ntasks = p.ntasks;
+  a.goff = p.goff;
+  a.gcur0 = p.gcur0;
+  a.gcur1 = p.gcur1;
+  a.gend = p.gend;
+  return a;
+}
+
+// The numeric pass of a plan for semiring SR: dense tasks (if the plan binned any: built-in,
+// lock-free semirings only), hash tasks of the large and the small kernel, all on the plan's
+// stream. C is the matrix cbh_plan_numeric allocated.
+template <class SR>
+hipError_t run_numeric_plan(const cbh_numeric_plan& p, int32_t* Cir, void* Cnum, int64_t ccap) {
+  const TaskArgs a = numeric_args(p, 0, Cir, Cnum, ccap);
+  hipStream_t s = reinterpret_cast<hipStream_t>(p.stream);
+  hipError_t e = hipSuccess;
+  if constexpr (!sr_locked<SR>::value) {
+    e = launch_tasks<SR, TNumLarge, MODE_TDENSE>(a, p.dense_first, p.dense_count, s);
+    if (e != hipSuccess) return e;
+  }
+  e = launch_tasks<SR, TNumLargeFor<SR>, MODE_TNUM>(a, p.large_first, p.large_count, s);
+  if (e != hipSuccess) return e;
+  return launch_tasks<SR, TNumSmallFor<SR>, MODE_TNUM>(a, p.small_first, p.small_count, s);
+}
+
+}  // namespace cbh

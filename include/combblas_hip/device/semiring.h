@@ -6,14 +6,32 @@
 //                (the reference's SR::id() is not always one: SelectMaxSRing::id() is -1).
 //   lds_acc()    atomic "acc = add(acc, v)" on an LDS slot (ds_add_f64 / ds_max_i64 / ...).
 // val_t is the element type in HBM; acc_t the LDS accumulator type (bool widens to u32
-// so it can use ds_or_b32).
+// so it can use ds_or_b32). Optional members: a_t / b_t (A's and B's value types when they
+// differ from val_t -- the reference's NT1 / NT2 -> T_promote), kLocked (the kernels accumulate
+// under a per-slot lock with SR::add instead of SR::lds_acc: any trivially copyable value type,
+// e.g. a user semiring's struct; the first product of a slot is stored as is, every later one is
+// folded in with add(new, old) -- the reference's hash-branch order, mtSpGEMM.h:401-416).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <limits>
+#include <type_traits>
 
 namespace cbh {
+
+template <class SR, class = void>
+struct sr_a_type { using type = typename SR::val_t; };
+template <class SR>
+struct sr_a_type<SR, std::void_t<typename SR::a_t>> { using type = typename SR::a_t; };
+template <class SR, class = void>
+struct sr_b_type { using type = typename SR::val_t; };
+template <class SR>
+struct sr_b_type<SR, std::void_t<typename SR::b_t>> { using type = typename SR::b_t; };
+template <class SR, class = void>
+struct sr_locked : std::false_type {};
+template <class SR>
+struct sr_locked<SR, std::void_t<decltype(SR::kLocked)>> : std::integral_constant<bool, SR::kLocked> {};
 
 template <class T>
 struct PlusTimesD {  // PlusTimesSRing<T,T>, Semirings.h:212-232
@@ -113,6 +131,37 @@ struct OrAndD {  // boolean OR-AND: PlusTimesSRing<bool,bool> / KTipsSR (Release
     if (v) atomicOr(p, 1u);
   }
   static __device__ __forceinline__ val_t finalize(acc_t a) { return (uint8_t)(a != 0); }
+};
+
+// PlusTimesSRing<T1,T2> with T1 != T2 (Semirings.h:212-232): multiply in T_promote = TO.
+template <class T1, class T2, class TO>
+struct PlusTimesPromoteD {
+  using a_t = T1;
+  using b_t = T2;
+  using val_t = TO;
+  using acc_t = TO;
+  static __device__ __forceinline__ acc_t identity() { return PlusTimesD<TO>::identity(); }
+  static __device__ __forceinline__ TO multiply(T1 a, T2 b) { return static_cast<TO>(a) * static_cast<TO>(b); }
+  static __device__ __forceinline__ TO add(TO a, TO b) { return a + b; }
+  static __device__ __forceinline__ void lds_acc(acc_t* p, TO v) { PlusTimesD<TO>::lds_acc(p, v); }
+  static __device__ __forceinline__ val_t finalize(acc_t a) { return a; }
+};
+
+// A user semiring with the reference's static-functor contract (Semirings.h:143-255; e.g.
+// ReleaseTests/KTipsTest.cpp:12-20, Applications/SegTestApp/SegTest.cpp:35-61) whose add and
+// multiply are callable on the device (__host__ __device__). Accumulated under the slot lock.
+template <class USR, class NT1, class NT2, class NTO>
+struct UserSRD {
+  using a_t = NT1;
+  using b_t = NT2;
+  using val_t = NTO;
+  using acc_t = NTO;
+  static constexpr bool kLocked = true;
+  static_assert(std::is_trivially_copyable<NTO>::value, "device values must be trivially copyable");
+  static __device__ __forceinline__ NTO multiply(const NT1& a, const NT2& b) { return USR::multiply(a, b); }
+  static __device__ __forceinline__ NTO add(const NTO& x, const NTO& y) { return USR::add(x, y); }
+  static __device__ __forceinline__ acc_t identity() { return acc_t(); }  // never read: first product is stored
+  static __device__ __forceinline__ val_t finalize(const acc_t& a) { return a; }
 };
 
 }  // namespace cbh

@@ -165,6 +165,42 @@ __device__ __forceinline__ int64_t stop_search(const int32_t* __restrict__ rows,
   return stop;
 }
 
+// Slot update of a locked semiring (sr_locked): the key word doubles as the slot's lock (bit 31;
+// rows are < 2^31 - 1). Claims an empty slot with the lock held and stores the first product,
+// or, if the slot holds row r, takes the lock and folds v in with SR::add(v, old) (new value
+// first, as the reference's hash branch, mtSpGEMM.h:408). Returns false if the slot belongs to
+// another row. SIMT-safe: every loop iteration makes ONE acquire attempt per lane and a lane that
+// acquires releases in the same iteration, so no lane ever waits on a lock held by a lane of its
+// own wave that the divergent branch order has not run yet.
+constexpr uint32_t kLockBit = 0x80000000u;
+template <class SR>
+__device__ __forceinline__ bool locked_insert(int32_t* key, typename SR::acc_t* val, int32_t r,
+                                              const typename SR::val_t& v) {
+  const int32_t locked = (int32_t)((uint32_t)r | kLockBit);
+  bool done = false, mine = true;
+  while (!done) {
+    int32_t k = kEmpty;
+    if (__hip_atomic_compare_exchange_strong(key, &k, locked, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP)) {
+      *val = v;  // first product of the slot
+      __hip_atomic_store(key, r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      done = true;
+    } else if ((int32_t)((uint32_t)k & ~kLockBit) != r) {
+      mine = false;  // another row's slot: probe on
+      done = true;
+    } else {
+      int32_t e = r;
+      if (__hip_atomic_compare_exchange_strong(key, &e, locked, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        *val = SR::add(v, *val);
+        __hip_atomic_store(key, r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        done = true;
+      }
+    }
+  }
+  return mine;
+}
+
 // Exclusive prefix sum of one int per thread over the block (thread order); total = block sum.
 // Uses red[0..NW); all threads must call.
 template <int BS>
@@ -212,6 +248,8 @@ struct TaskCfg {
   static constexpr bool DENSE = MODE == MODE_TDENSE;
   using val_t = typename SR::val_t;
   using acc_t = typename SR::acc_t;
+  using a_t = typename sr_a_type<SR>::type;  // A's values (NT1)
+  using b_t = typename sr_b_type<SR>::type;  // B's values (NT2)
   static constexpr int TA = NUM ? T + kGuard : T;  // slots (symbolic: 32-bit words, keys or bitmap)
   static constexpr int NW = BS / 64;
   static constexpr int WIN = U * BS;
@@ -220,7 +258,7 @@ struct TaskCfg {
   // prefix popcounts of the words
   static constexpr int CAPD = T / 2;
   static constexpr int NWB = TA - CAPD;
-  static_assert(!NUM || (TA - CAPD) * sizeof(acc_t) >= 2 * (size_t)NWB, "dense prefix array fits");
+  static_assert(!DENSE || (TA - CAPD) * sizeof(acc_t) >= 2 * (size_t)NWB, "dense prefix array fits");
   // owner map entries are entry indices (< EMAX): 16 bits leave LDS room for larger windows
   using own_t = int16_t;
   static_assert(EMAX < 32768, "owner map entries are 16-bit");
@@ -230,7 +268,7 @@ struct TaskCfg {
   static constexpr size_t o_pos = al(o_vals + (NUM ? sizeof(acc_t) * TA : 0));
   static constexpr size_t o_end = al(o_pos + sizeof(int64_t) * EMAX);
   static constexpr size_t o_scale = al(o_end + sizeof(int64_t) * EMAX);
-  static constexpr size_t o_next = al(o_scale + (NUM ? sizeof(val_t) * EMAX : 0));
+  static constexpr size_t o_next = al(o_scale + (NUM ? sizeof(b_t) * EMAX : 0));
   static constexpr size_t o_next2 = al(o_next + sizeof(int32_t) * EMAX);
   static constexpr size_t o_col = al(o_next2 + sizeof(int32_t) * EMAX);
   static constexpr size_t o_off = al(o_col + sizeof(int32_t) * EMAX);
@@ -240,11 +278,16 @@ struct TaskCfg {
 };
 
 template <class SR, int T, int BS, int EMAX, int U, int MODE>
-__global__ __launch_bounds__(BS, 2048 / BS) void task_kernel(TaskArgs a) {
+// 512-thread groups: two per CU (LDS-bound), so 4 waves per SIMD -> <= 128 VGPRs
+__global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(TaskArgs a) {
   using C = TaskCfg<SR, T, BS, EMAX, U, MODE>;
   using val_t = typename C::val_t;
   using acc_t = typename C::acc_t;
+  using a_t = typename C::a_t;
+  using b_t = typename C::b_t;
   constexpr bool NUM = C::NUM;
+  constexpr bool LOCKED = sr_locked<SR>::value;
+  static_assert(!(LOCKED && C::DENSE), "locked (user-semiring) accumulation runs on the hash kernels");
   constexpr int TA = C::TA, NW = C::NW, WIN = C::WIN;
   static_assert((T & (T - 1)) == 0, "table size must be a power of two");
 
@@ -256,7 +299,7 @@ __global__ __launch_bounds__(BS, 2048 / BS) void task_kernel(TaskArgs a) {
   // it holds cursor - exclusive offset (the gather base of the entry's products)
   int64_t* epos = reinterpret_cast<int64_t*>(smem + C::o_pos);
   int64_t* eend = reinterpret_cast<int64_t*>(smem + C::o_end);    // end of the A column in the task
-  val_t* escale = reinterpret_cast<val_t*>(smem + C::o_scale);    // B value
+  b_t* escale = reinterpret_cast<b_t*>(smem + C::o_scale);        // B value
   int32_t* enext = reinterpret_cast<int32_t*>(smem + C::o_next);  // row at the cursor (kNoRow: done)
   int32_t* enext2 = reinterpret_cast<int32_t*>(smem + C::o_next2);  // row at the sub-tile's stop
   int32_t* ecol = reinterpret_cast<int32_t*>(smem + C::o_col);    // A column id
@@ -332,7 +375,7 @@ __global__ __launch_bounds__(BS, 2048 / BS) void task_kernel(TaskArgs a) {
     for (int i = tid; i < cnt; i += BS) {
       const int64_t p = e0 + first + i;
       const int32_t k = a.Bir[p];
-      if constexpr (NUM) escale[i] = reinterpret_cast<const val_t*>(a.Bnum)[p];
+      if constexpr (NUM) escale[i] = reinterpret_cast<const b_t*>(a.Bnum)[p];
       if (k < 0 || k >= a.ncolA) {
         bad |= 1 << 1;
         ecol[i] = 0;
@@ -436,7 +479,7 @@ __global__ __launch_bounds__(BS, 2048 / BS) void task_kernel(TaskArgs a) {
         const int64_t q = epos[i] + w0 + x;
         r[u] = a.Air[q];
         if constexpr (NUM)
-          if (with_vals) av[u] = SR::multiply(reinterpret_cast<const val_t*>(a.Anum)[q], escale[i]);
+          if (with_vals) av[u] = SR::multiply(reinterpret_cast<const a_t*>(a.Anum)[q], escale[i]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -455,7 +498,7 @@ __global__ __launch_bounds__(BS, 2048 / BS) void task_kernel(TaskArgs a) {
   if constexpr (NUM) {
     dwords = reinterpret_cast<uint32_t*>(smem + C::o_keys + sizeof(int32_t) * C::CAPD);
     dpre = reinterpret_cast<int16_t*>(smem + C::o_vals + sizeof(acc_t) * C::CAPD);
-    if (dense)  // dense accumulators start at the identity; every commit resets what it read
+    if constexpr (dense)  // dense accumulators start at the identity; every commit resets what it read
       for (int s = tid; s < C::CAPD; s += BS) vals[s] = SR::identity();
   }
   __syncthreads();
@@ -483,7 +526,7 @@ __global__ __launch_bounds__(BS, 2048 / BS) void task_kernel(TaskArgs a) {
     } else {
       for (int s = tid; s < TA; s += BS) {
         keys[s] = kEmpty;
-        if constexpr (NUM) vals[s] = SR::identity();
+        if constexpr (NUM && !LOCKED) vals[s] = SR::identity();
       }
     }
     if (tid == 0) __hip_atomic_store(&s_ovf, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -531,12 +574,20 @@ __global__ __launch_bounds__(BS, 2048 / BS) void task_kernel(TaskArgs a) {
           }
           uint32_t s = (uint32_t)(((uint64_t)d * scale) >> 32);
           bool ok = false;
-          for (int probe = 0; probe < kPmax && s < (uint32_t)TA; ++probe, ++s) {
-            const int32_t k = atomicCAS(&keys[s], kEmpty, r[u]);
-            if (k == kEmpty || k == r[u]) {
-              SR::lds_acc(&vals[s], vv);
-              ok = true;
-              break;
+          if constexpr (LOCKED) {
+            for (int probe = 0; probe < kPmax && s < (uint32_t)TA; ++probe, ++s)
+              if (locked_insert<SR>(&keys[s], &vals[s], r[u], vv)) {
+                ok = true;
+                break;
+              }
+          } else {
+            for (int probe = 0; probe < kPmax && s < (uint32_t)TA; ++probe, ++s) {
+              const int32_t k = atomicCAS(&keys[s], kEmpty, r[u]);
+              if (k == kEmpty || k == r[u]) {
+                SR::lds_acc(&vals[s], vv);
+                ok = true;
+                break;
+              }
             }
           }
           if (!ok) set_ovf();
@@ -574,7 +625,7 @@ __global__ __launch_bounds__(BS, 2048 / BS) void task_kernel(TaskArgs a) {
       }
     }
     int dtotal = 0;
-    if constexpr (NUM) {
+    if constexpr (NUM && dense) {
       if (dense && !__hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
         // output rank of every word's first row: exclusive scan of the bitmap's popcounts
         constexpr int KW = (C::NWB + BS - 1) / BS;
@@ -622,7 +673,7 @@ __global__ __launch_bounds__(BS, 2048 / BS) void task_kernel(TaskArgs a) {
               const int64_t* gn = par ? a.gcur0 : a.gcur1;
               for (int i = tid; i < nec; i += BS) {
                 const int64_t pe = e0 + first + i;
-                escale[i] = reinterpret_cast<const val_t*>(a.Bnum)[pe];
+                escale[i] = reinterpret_cast<const b_t*>(a.Bnum)[pe];
                 const int64_t p0 = gc[go + first + i];
                 epos[i] = p0;
                 eoff[i] = (int32_t)(gn[go + first + i] - p0);

@@ -1,11 +1,19 @@
 // Drop-in integration test (built by `make -C oracle ref` into oracle/_ref/dropin_harness; it
-// compiles the reference's headers, so its binary lives with the other reference builds).
+// compiles the reference's headers, so its binary lives with the other reference builds). This
+// translation unit is built with g++, as the reference is; the device kernels of the
+// test-defined semirings are instantiated in dropin_kernels.hip (hipcc).
 //
-// The reference's UNCHANGED Mult_AnXBn_Synch (ParFriends.h:1004-1108) is instantiated twice on the
-// same R-MAT input: once for PlusTimesSRing<double,double> / SelectMaxSRing<int64_t,int64_t>,
-// which COMBBLAS_HIP_INSTANTIATE routes to the gfx950 kernels through the C-ABI, and once for
-// value-identical local semirings that are not specialized (stock OpenMP LocalHybridSpGEMM).
-// The two DCSC results must match exactly (structure, row order and values).
+// The reference's UNCHANGED Mult_AnXBn_Synch (ParFriends.h:1004-1108) runs twice per case on the
+// same R-MAT input: once for a semiring routed to the gfx950 kernels, once for a value-identical
+// semiring that is not specialized (the stock OpenMP LocalHybridSpGEMM). The two DCSC results
+// must match exactly (structure, row order and values).
+//   built-in semirings (COMBBLAS_HIP_INSTANTIATE, library kernels through the C-ABI):
+//     PlusTimesSRing<double,double>, SelectMaxSRing<int64_t,int64_t>
+//   header-instantiated (COMBBLAS_HIP_INSTANTIATE_DEVICE, HipSpGEMMDevice.h):
+//     KTipsDev    -- test-defined bool OR-AND with the KTipsSR contract (KTipsTest.cpp:12-20)
+//     MinMaxSR    -- test-defined semiring over a two-field struct, int64 inputs (NT != NTO, as
+//                    SegTest.cpp:165-171's KmerIntersect<int64_t, CommonKmers>)
+//     PlusTimesSRing<double,int64_t> -- promotion NT1 != NT2 -> T_promote = double
 //   dropin_harness <scale>      -> prints "DROPIN <case> OK nnz=..." lines, exit 0 on success
 #include <mpi.h>
 
@@ -14,19 +22,16 @@
 #include <memory>
 
 #include "CombBLAS/CombBLAS.h"
-#include "combblas_hip/HipSpGEMM.h"
+#include "combblas_hip/HipSpGEMMDevice.h"
 
 using namespace combblas;
 
 double cblas_alltoalltime, cblas_allgathertime, cblas_mergeconttime, cblas_transvectime, cblas_localspmvtime;
 MTRand GlobalMT(123);
 
-typedef PlusTimesSRing<double, double> PTDD;
-typedef SelectMaxSRing<int64_t, int64_t> SMLL;
-COMBBLAS_HIP_INSTANTIATE(PTDD, int64_t, double)
-COMBBLAS_HIP_INSTANTIATE(SMLL, int64_t, int64_t)
+#include "dropin_semirings.h"
 
-// value-identical semirings that stay on the stock CPU path
+// the value-identical stock semirings of the built-in cases
 template <class T>
 struct CpuPlusTimes {
   static T id() { return 0; }
@@ -45,6 +50,23 @@ struct CpuSelectMax {
   static T multiply(const T& a, const T& b) { return a * b; }
   static void axpy(T a, const T& x, T& y) { y = std::max(y, a * x); }
 };
+struct CpuPlusTimesDI {  // PlusTimesSRing<double,int64_t> on the stock path
+  static double id() { return 0; }
+  static bool returnedSAID() { return false; }
+  static MPI_Op mpi_op() { return MPI_SUM; }
+  static double add(const double& a, const double& b) { return a + b; }
+  static double multiply(const double& a, const int64_t& b) { return a * static_cast<double>(b); }
+  static void axpy(double a, const int64_t& x, double& y) { y += a * x; }
+};
+
+typedef PlusTimesSRing<double, double> PTDD;
+typedef SelectMaxSRing<int64_t, int64_t> SMLL;
+typedef PlusTimesSRing<double, int64_t> PTDI;
+COMBBLAS_HIP_INSTANTIATE(PTDD, int64_t, double)
+COMBBLAS_HIP_INSTANTIATE(SMLL, int64_t, int64_t)
+COMBBLAS_HIP_INSTANTIATE_DEVICE(KTipsDev, int64_t, bool, bool, bool)
+COMBBLAS_HIP_INSTANTIATE_DEVICE(MinMaxDev, int64_t, int64_t, int64_t, MinMax)
+COMBBLAS_HIP_INSTANTIATE_DEVICE(PTDI, int64_t, double, int64_t, double)
 
 template <class NT>
 static bool same(const SpDCCols<int64_t, NT>& x, const SpDCCols<int64_t, NT>& y) {
@@ -60,19 +82,29 @@ static bool same(const SpDCCols<int64_t, NT>& x, const SpDCCols<int64_t, NT>& y)
   return true;
 }
 
-template <class NT, class SRH, class SRC>
-static int run_case(const char* name, SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>>& G) {
-  typedef SpDCCols<int64_t, NT> DER;
-  SpParMat<int64_t, NT, DER> A(G);
-  SpParMat<int64_t, NT, DER> B(G);
+// value = f(row, col, value) on the local block (1 rank: local ids are global), as TC.cpp:72-87 edits L
+template <class F>
+static void set_values(SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>>& M, F f) {
+  for (auto colit = M.seq().begcol(); colit != M.seq().endcol(); ++colit)
+    for (auto nzit = M.seq().begnz(colit); nzit != M.seq().endnz(colit); ++nzit)
+      nzit.value() = f(nzit.rowid(), colit.colid(), nzit.value());
+}
+
+template <class NTO, class SRH, class SRC, class NA, class NB>
+static int run_case(const char* name, SpParMat<int64_t, NA, SpDCCols<int64_t, NA>>& A,
+                    SpParMat<int64_t, NB, SpDCCols<int64_t, NB>>& B) {
+  typedef SpDCCols<int64_t, NTO> DER;
+  std::fprintf(stderr, "case %s: device\n", name);
   double t0 = MPI_Wtime();
-  SpParMat<int64_t, NT, DER> Ch = Mult_AnXBn_Synch<SRH, NT, DER>(A, B);  // device path
+  SpParMat<int64_t, NTO, DER> Ch = Mult_AnXBn_Synch<SRH, NTO, DER>(A, B);  // device path
   double t1 = MPI_Wtime();
-  SpParMat<int64_t, NT, DER> Cc = Mult_AnXBn_Synch<SRC, NT, DER>(A, B);  // stock reference path
+  std::fprintf(stderr, "case %s: stock\n", name);
+  SpParMat<int64_t, NTO, DER> Cc = Mult_AnXBn_Synch<SRC, NTO, DER>(A, B);  // stock reference path
   double t2 = MPI_Wtime();
   bool ok = same(Ch.seq(), Cc.seq());
   std::printf("DROPIN %s %s nnz=%lld hip_s=%.3f cpu_s=%.3f\n", name, ok ? "OK" : "MISMATCH", (long long)Ch.getnnz(),
               t1 - t0, t2 - t1);
+  std::fflush(stdout);
   return ok ? 0 : 1;
 }
 
@@ -84,10 +116,21 @@ int main(int argc, char** argv) {
     double init[4] = {.57, .19, .19, .05};
     DistEdgeList<int64_t>* DEL = new DistEdgeList<int64_t>();
     DEL->GenGraph500Data(init, scale, 16, true, true);
-    SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>> G(*DEL, false);
+    typedef SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>> PMatI;
+    PMatI G(*DEL, false);
     delete DEL;
-    bad += run_case<double, PlusTimesSRing<double, double>, CpuPlusTimes<double>>("PSpGEMM<PlusTimes<double>>", G);
-    bad += run_case<int64_t, SelectMaxSRing<int64_t, int64_t>, CpuSelectMax<int64_t>>("PSpGEMM<SelectMax<int64>>", G);
+    SpParMat<int64_t, double, SpDCCols<int64_t, double>> Ad(G), Bd(G);
+    bad += run_case<double, PTDD, CpuPlusTimes<double>>("PSpGEMM<PlusTimes<double>>", Ad, Bd);
+    PMatI Ai(G), Bi(G);
+    bad += run_case<int64_t, SMLL, CpuSelectMax<int64_t>>("PSpGEMM<SelectMax<int64>>", Ai, Bi);
+    SpParMat<int64_t, bool, SpDCCols<int64_t, bool>> Ab(G), Bb(G);
+    bad += run_case<bool, KTipsDev, KTipsCpu>("PSpGEMM<user KTipsSR bool>", Ab, Bb);
+    // values that differ per entry (multiplicities alone make most products equal)
+    PMatI Av(G), Bv(G);
+    set_values(Av, [](int64_t r, int64_t c, int64_t x) { return x * ((r * 7919 + c * 31) % 23 - 11); });
+    set_values(Bv, [](int64_t r, int64_t c, int64_t x) { return x * ((r * 104729 + c * 17) % 19 - 9); });
+    bad += run_case<MinMax, MinMaxDev, MinMaxCpu>("PSpGEMM<user struct MinMax, int64 -> struct>", Av, Bv);
+    bad += run_case<double, PTDI, CpuPlusTimesDI>("PSpGEMM<PlusTimes<double,int64> promotion>", Ad, Bi);
   }
   MPI_Finalize();
   return bad ? 1 : 0;

@@ -1,0 +1,61 @@
+// Test-defined semirings of the drop-in harness, shared by the g++ translation unit that runs the
+// reference drivers (dropin_harness.cpp) and the hipcc one that instantiates their device
+// kernels (dropin_kernels.hip). add/multiply are callable on the device (CBH_HD).
+#pragma once
+#include <mpi.h>
+
+#include <cstdint>
+#include <ostream>
+
+#ifdef __HIP__
+#define CBH_HD __host__ __device__
+#else
+#define CBH_HD
+#endif
+
+// KTipsSR with device-callable add/multiply (ReleaseTests/KTipsTest.cpp:12-20)
+struct KTipsDev {
+  static bool id() { return false; }
+  static bool returnedSAID() { return false; }
+  static MPI_Op mpi_op() { return MPI_LOR; }
+  CBH_HD static bool add(const bool& a, const bool& b) { return a || b; }
+  CBH_HD static bool multiply(const bool& a, const bool& b) { return a && b; }
+  static void axpy(bool a, const bool& x, bool& y) { y = add(y, multiply(a, x)); }
+};
+struct KTipsCpu {  // the same semiring on the stock path
+  static bool id() { return false; }
+  static bool returnedSAID() { return false; }
+  static MPI_Op mpi_op() { return MPI_LOR; }
+  static bool add(const bool& a, const bool& b) { return a || b; }
+  static bool multiply(const bool& a, const bool& b) { return a && b; }
+  static void axpy(bool a, const bool& x, bool& y) { y = add(y, multiply(a, x)); }
+};
+
+// a two-field struct value: (smallest, largest) product reaching each output
+struct MinMax {
+  int64_t lo = 0, hi = 0;
+  bool operator==(const MinMax& o) const { return lo == o.lo && hi == o.hi; }
+  friend std::ostream& operator<<(std::ostream& os, const MinMax& m) { return os << "(" << m.lo << "," << m.hi << ")"; }
+};
+struct MinMaxDev {
+  static MinMax id() { return MinMax(); }
+  static bool returnedSAID() { return false; }
+  CBH_HD static MinMax add(const MinMax& a, const MinMax& b) {
+    MinMax r;
+    r.lo = a.lo < b.lo ? a.lo : b.lo;
+    r.hi = a.hi > b.hi ? a.hi : b.hi;
+    return r;
+  }
+  CBH_HD static MinMax multiply(const int64_t& a, const int64_t& b) {
+    MinMax r;
+    r.lo = r.hi = a * b - 3 * a + b;  // not symmetric in (a, b): catches swapped operands
+    return r;
+  }
+};
+struct MinMaxCpu {
+  static MinMax id() { return MinMax(); }
+  static bool returnedSAID() { return false; }
+  static MinMax add(const MinMax& a, const MinMax& b) { return MinMaxDev::add(a, b); }
+  static MinMax multiply(const int64_t& a, const int64_t& b) { return MinMaxDev::multiply(a, b); }
+};
+
