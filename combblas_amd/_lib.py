@@ -58,6 +58,9 @@ SIGNATURES = {
     "cbh_mat_upload_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cbh_dcsc), ctypes.c_int64,
                                             ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_mat_value_bytes": (ctypes.c_int64, [ctypes.c_void_p]),
+    "cbh_mat_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                      ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_mat_clone": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
     # user-semiring plans (the numeric launches are C++/HIP: include/combblas_hip/HipSpGEMMDevice.h)
     "cbh_plan_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_plan_info": (ctypes.c_int, [ctypes.c_void_p, c_int64_p, c_int64_p]),

@@ -1328,6 +1328,30 @@ int cbh_mat_upload_bytes(cbh_ctx* ctx, const cbh_dcsc* h, int64_t value_bytes, c
 
 int64_t cbh_mat_value_bytes(const cbh_mat* M) { return M ? M->vbytes : 0; }
 
+int cbh_mat_create(cbh_ctx* ctx, int64_t m, int64_t n, int64_t nnz, int64_t nzc, cbh_dtype dtype, int64_t value_bytes,
+                   cbh_mat** out) {
+  if (!ctx || !out || m < 0 || n < 0 || nnz < 0 || nzc < 0) return fail(ctx, CBH_E_ARG, "bad create arguments");
+  const int64_t vb = dtype == CBH_OPAQUE ? value_bytes : (int64_t)dtype_size(dtype);
+  if (vb <= 0) return fail(ctx, CBH_E_ARG, "unknown value size");
+  CBH_TRY(new_mat(ctx, m, n, nnz, nzc, dtype, out, vb));
+  if (nzc == 0) CBH_HIP(ctx, hipMemsetAsync((*out)->cp, 0, sizeof(int64_t), ctx->stream));
+  return CBH_OK;
+}
+
+int cbh_mat_clone(cbh_ctx* ctx, const cbh_mat* S, cbh_mat** out) {
+  if (!ctx || !S || !out) return fail(ctx, CBH_E_ARG, "bad clone arguments");
+  cbh_mat* M;
+  CBH_TRY(new_mat(ctx, S->m, S->n, S->nnz, S->nzc, S->dtype, &M, S->vbytes));
+  CBH_HIP(ctx, hipMemcpyAsync(M->cp, S->cp, sizeof(int64_t) * (S->nzc + 1), hipMemcpyDeviceToDevice, ctx->stream));
+  if (S->nzc) CBH_HIP(ctx, hipMemcpyAsync(M->jc, S->jc, sizeof(int64_t) * S->nzc, hipMemcpyDeviceToDevice, ctx->stream));
+  if (S->nnz) {
+    CBH_HIP(ctx, hipMemcpyAsync(M->ir, S->ir, sizeof(int32_t) * S->nnz, hipMemcpyDeviceToDevice, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(M->num, S->num, S->vbytes * S->nnz, hipMemcpyDeviceToDevice, ctx->stream));
+  }
+  *out = M;
+  return CBH_OK;
+}
+
 int cbh_spgemm_symbolic(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, int64_t* flops, int64_t* nnzC,
                         int64_t* col_flops_dev, int64_t* col_nnz_dev) {
   CBH_TRY(validate_pair(ctx, A, B));

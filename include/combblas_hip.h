@@ -103,6 +103,12 @@ int cbh_ctx_set_phase_budget(cbh_ctx* ctx, int64_t bytes);
 int cbh_mat_upload(cbh_ctx* ctx, const cbh_dcsc* host, cbh_dtype dtype, cbh_mat** out);
 /* Copy a host DCSC whose values are an opaque type of value_bytes bytes (a user semiring's NT). */
 int cbh_mat_upload_bytes(cbh_ctx* ctx, const cbh_dcsc* host, int64_t value_bytes, cbh_mat** out);
+/* An uninitialised device matrix of the given sizes (the receive side of a broadcast,
+ * SpDCCols::Create(essentials), SpDCCols.cpp:787-795); value_bytes is used for CBH_OPAQUE. */
+int cbh_mat_create(cbh_ctx* ctx, int64_t m, int64_t n, int64_t nnz, int64_t nzc, cbh_dtype dtype,
+                   int64_t value_bytes, cbh_mat** out);
+/* A device copy of a matrix (SpDCCols copy constructor, SpDCCols.cpp:214-226). */
+int cbh_mat_clone(cbh_ctx* ctx, const cbh_mat* src, cbh_mat** out);
 /* Bytes per value of a matrix (any dtype). */
 int64_t cbh_mat_value_bytes(const cbh_mat* mat);
 /* Wrap device arrays without copying. The caller keeps them alive until cbh_mat_free. */

@@ -1,0 +1,287 @@
+// SpParMatDev.h -- device-resident distributed SpGEMM behind the reference's own API.
+//
+//   typedef combblas::SpParMat<int64_t, double, combblas_hip::SpDCColsDev<int64_t, double>> DMat;
+//   DMat A = combblas_hip::to_device(Ahost), B = combblas_hip::to_device(Bhost);
+//   DMat C = combblas::PSpGEMM<combblas::PlusTimesSRing<double, double>>(A, B);   // SpParMat.h:454-467
+//   auto Ch = combblas_hip::to_host(C);
+//
+// SpDCColsDev<IT,NT> is a DER (the local-block type parameter of SpParMat, like SpDCCols) whose
+// Dcsc arrays live in HBM (a cbh_mat). For SpParMats over it, the overload of
+// combblas::Mult_AnXBn_Synch below is more specialized than the reference's generic one
+// (ParFriends.h:1004-1108), so the reference's PSpGEMM (and any code that calls
+// Mult_AnXBn_Synch<SR, NUO, UDERO>) runs the same 2D SUMMA with every block kept in HBM:
+//   GetSetSizes      host MPI_Allgather of the 4 essentials per rank (scalars; SpParHelper.cpp:797-808)
+//   BCastMatrix      cp / jc / ir / num broadcast DEVICE TO DEVICE on the row (A) and column (B)
+//                    communicators with RCCL (ncclBroadcast over xGMI; SpParHelper.cpp:581-599)
+//   local multiply   cbh_spgemm (LocalHybridSpGEMM, mtSpGEMM.h:212-460)
+//   MultiwayMerge    cbh_merge of the stage partials on the device (MultiwayMerge.h:411-526)
+// -- no host copy of any block, partial or result. The RCCL communicators mirror the
+// reference's MPI ones (CommGrid.cpp:37-75: world, row and column splits): one ncclComm per MPI
+// communicator, bootstrapped by an MPI_Bcast of the ncclUniqueId from the communicator's rank 0.
+// COMBBLAS_HIP_COMM=mpi selects a host-staged MPI_Bcast transport instead (test rehearsal of
+// several ranks sharing one GPU, which RCCL does not allow).
+//
+// Link: libcombblas_hip.so, librccl.so (/opt/rocm/lib), libamdhip64.so, MPI.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <vector>
+
+#include "HipSpGEMM.h"
+
+namespace combblas_hip {
+
+// ------------------------------------------------------------------ the device-resident block
+template <class IT, class NT>
+class SpDCColsDev {
+ public:
+  typedef IT LocalIT;
+  typedef NT LocalNT;
+  static const int esscount = 4;  // nnz, m, n, nzc (SpDCCols.h esscount, SpDCCols.cpp:787-795)
+
+  SpDCColsDev() { mat_ = make_empty(0, 0); }
+  SpDCColsDev(IT m, IT n) { mat_ = make_empty(m, n); }
+  explicit SpDCColsDev(cbh_mat* m) : mat_(m) {}  // takes ownership
+  explicit SpDCColsDev(const combblas::SpDCCols<IT, NT>& host) { mat_ = upload(host); }
+  SpDCColsDev(const SpDCColsDev& o) {  // deep copy, as SpDCCols's (SpDCCols.cpp:214-226)
+    int rc = cbh_mat_clone(context(), o.mat_, &mat_);
+    if (rc != CBH_OK) die(context(), rc, "cbh_mat_clone");
+  }
+  SpDCColsDev& operator=(const SpDCColsDev& o) {
+    if (this != &o) {
+      cbh_mat* m = nullptr;
+      int rc = cbh_mat_clone(context(), o.mat_, &m);
+      if (rc != CBH_OK) die(context(), rc, "cbh_mat_clone");
+      reset(m);
+    }
+    return *this;
+  }
+  ~SpDCColsDev() { reset(nullptr); }
+
+  IT getnrow() const { return (IT)info(0); }
+  IT getncol() const { return (IT)info(1); }
+  IT getnnz() const { return (IT)info(2); }
+  IT getnzc() const { return (IT)info(3); }
+  bool isZero() const { return getnnz() == 0; }
+  // SpDCCols::GetEssentials (SpDCCols.cpp:46): {nnz, m, n, nzc}
+  std::vector<IT> GetEssentials() const { return {getnnz(), getnrow(), getncol(), getnzc()}; }
+
+  cbh_mat* mat() const { return mat_; }
+  void reset(cbh_mat* m) {
+    if (mat_) cbh_mat_free(context(), mat_);
+    mat_ = m;
+  }
+  cbh_mat* release() {
+    cbh_mat* m = mat_;
+    mat_ = nullptr;
+    return m;
+  }
+  // one download of the whole block (the only device -> host copy of the path)
+  combblas::SpDCCols<IT, NT>* to_host() const {
+    combblas::SpTuples<IT, NT>* t = download_tuples<IT, NT>(mat_);
+    auto* d = new combblas::SpDCCols<IT, NT>(*t, false);
+    delete t;
+    return d;
+  }
+
+ private:
+  static cbh_mat* make_empty(IT m, IT n) {
+    cbh_mat* out = nullptr;
+    int rc = cbh_mat_create(context(), m, n, 0, 0, dtype_of<NT>::value, (int64_t)sizeof(NT), &out);
+    if (rc != CBH_OK) die(context(), rc, "cbh_mat_create");
+    return out;
+  }
+  int64_t info(int k) const {
+    int64_t v[4] = {0, 0, 0, 0};
+    cbh_mat_info(mat_, &v[0], &v[1], &v[2], &v[3], nullptr);
+    return v[k];
+  }
+  cbh_mat* mat_ = nullptr;
+};
+
+// ------------------------------------------------------------------ RCCL communicators of a grid
+inline bool use_mpi_transport() {
+  static const bool v = [] {
+    const char* e = std::getenv("COMBBLAS_HIP_COMM");
+    return e && std::strcmp(e, "mpi") == 0;
+  }();
+  return v;
+}
+
+inline void rccl_check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) {
+    std::fprintf(stderr, "combblas_hip: %s failed: %s\n", what, ncclGetErrorString(r));
+    MPI_Abort(MPI_COMM_WORLD, CBH_E_HIP);
+  }
+}
+
+// ncclComm_t mirroring one MPI communicator (ncclUniqueId from its rank 0 over MPI_Bcast).
+inline ncclComm_t rccl_comm_for(MPI_Comm comm) {
+  static std::map<MPI_Comm, ncclComm_t> cache;
+  auto it = cache.find(comm);
+  if (it != cache.end()) return it->second;
+  int rank = 0, size = 1;
+  MPI_Comm_rank(comm, &rank);
+  MPI_Comm_size(comm, &size);
+  ncclUniqueId id;
+  if (rank == 0) rccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  MPI_Bcast(&id, (int)sizeof(id), MPI_BYTE, 0, comm);
+  context();  // the context selects this rank's device
+  ncclComm_t c;
+  rccl_check(ncclCommInitRank(&c, size, id, rank), "ncclCommInitRank");
+  cache[comm] = c;
+  return c;
+}
+
+// SpParHelper::BCastMatrix (SpParHelper.cpp:581-599) on device blocks: non-root ranks allocate
+// from the essentials {nnz, m, n, nzc} (SpDCCols::Create), then cp, jc, ir and the values are
+// broadcast device to device on the context stream.
+template <class IT, class NT>
+void BCastMatrix(MPI_Comm comm, SpDCColsDev<IT, NT>& M, const std::vector<IT>& ess, int root) {
+  int rank = 0;
+  MPI_Comm_rank(comm, &rank);
+  cbh_ctx* ctx = context();
+  if (rank != root) {
+    cbh_mat* m = nullptr;
+    int rc = cbh_mat_create(ctx, ess[1], ess[2], ess[0], ess[3], dtype_of<NT>::value, (int64_t)sizeof(NT), &m);
+    if (rc != CBH_OK) die(ctx, rc, "cbh_mat_create");
+    M.reset(m);
+  }
+  const int64_t *cp, *jc;
+  const int32_t* ir;
+  const void* num;
+  cbh_mat_device_arrays(M.mat(), &cp, &jc, &ir, &num);
+  const int64_t nnz = ess[0], nzc = ess[3];
+  struct Piece {
+    void* p;
+    size_t bytes;
+  } pieces[4] = {{const_cast<int64_t*>(cp), sizeof(int64_t) * (size_t)(nzc + 1)},
+                 {const_cast<int64_t*>(jc), sizeof(int64_t) * (size_t)nzc},
+                 {const_cast<int32_t*>(ir), sizeof(int32_t) * (size_t)nnz},
+                 {const_cast<void*>(num), sizeof(NT) * (size_t)nnz}};
+  hipStream_t s = reinterpret_cast<hipStream_t>(cbh_ctx_stream(ctx));
+  if (use_mpi_transport()) {  // host-staged rehearsal transport
+    for (const Piece& x : pieces) {
+      if (!x.bytes) continue;
+      std::vector<char> h(x.bytes);
+      if (rank == root) {
+        (void)hipMemcpyAsync(h.data(), x.p, x.bytes, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+      }
+      MPI_Bcast(h.data(), (int)x.bytes, MPI_BYTE, root, comm);
+      if (rank != root) {
+        (void)hipMemcpyAsync(x.p, h.data(), x.bytes, hipMemcpyHostToDevice, s);
+        (void)hipStreamSynchronize(s);
+      }
+    }
+    return;
+  }
+  ncclComm_t nc = rccl_comm_for(comm);
+  rccl_check(ncclGroupStart(), "ncclGroupStart");
+  for (const Piece& x : pieces)
+    if (x.bytes) rccl_check(ncclBroadcast(x.p, x.p, x.bytes, ncclUint8, root, nc, s), "ncclBroadcast");
+  rccl_check(ncclGroupEnd(), "ncclGroupEnd");
+}
+
+// SpParHelper::GetSetSizes (SpParHelper.cpp:797-808): essentials of every rank of comm1d
+template <class IT, class NT>
+std::vector<std::vector<IT>> GetSetSizes(const SpDCColsDev<IT, NT>& M, MPI_Comm comm1d) {
+  int size = 1;
+  MPI_Comm_size(comm1d, &size);
+  std::vector<IT> mine = M.GetEssentials(), all(4 * (size_t)size);
+  MPI_Allgather(mine.data(), 4 * (int)sizeof(IT), MPI_BYTE, all.data(), 4 * (int)sizeof(IT), MPI_BYTE, comm1d);
+  std::vector<std::vector<IT>> out(size);
+  for (int r = 0; r < size; ++r) out[r].assign(all.begin() + 4 * r, all.begin() + 4 * r + 4);
+  return out;
+}
+
+// the built-in semiring code of SR (semiring_traits in HipSpGEMM.h)
+template <class SR, class NUO, class NU1, class NU2>
+cbh_mat* local_multiply(const cbh_mat* A, const cbh_mat* B) {
+  static_assert(std::is_same<NU1, NUO>::value && std::is_same<NU2, NUO>::value,
+                "device-resident SUMMA: built-in semirings over one value type");
+  cbh_mat* C = nullptr;
+  int rc = cbh_spgemm(context(), semiring_traits<SR>::code, A, B, CBH_SORTED_ROWS, &C);
+  if (rc != CBH_OK) die(context(), rc, "cbh_spgemm");
+  return C;
+}
+
+// SpParMat<.., SpDCCols> <-> SpParMat<.., SpDCColsDev>: one upload / download of the local block
+template <class IT, class NT>
+combblas::SpParMat<IT, NT, SpDCColsDev<IT, NT>> to_device(combblas::SpParMat<IT, NT, combblas::SpDCCols<IT, NT>>& A) {
+  return combblas::SpParMat<IT, NT, SpDCColsDev<IT, NT>>(new SpDCColsDev<IT, NT>(A.seq()), A.getcommgrid());
+}
+template <class IT, class NT>
+combblas::SpParMat<IT, NT, combblas::SpDCCols<IT, NT>> to_host(combblas::SpParMat<IT, NT, SpDCColsDev<IT, NT>>& A) {
+  return combblas::SpParMat<IT, NT, combblas::SpDCCols<IT, NT>>(A.seq().to_host(), A.getcommgrid());
+}
+
+}  // namespace combblas_hip
+
+namespace combblas {
+
+// (equal value types: promote.h's promote_trait<T, T> already gives T)
+template <class IT, class NT1, class NT2>
+struct promote_trait<combblas_hip::SpDCColsDev<IT, NT1>, combblas_hip::SpDCColsDev<IT, NT2>,
+                     typename std::enable_if<!std::is_same<NT1, NT2>::value>::type> {
+  typedef combblas_hip::SpDCColsDev<IT, typename promote_trait<NT1, NT2>::T_promote> T_promote;
+};
+
+// Mult_AnXBn_Synch (ParFriends.h:1004-1108) for device-resident operands: the same SUMMA stage
+// loop, sizes exchanged on the host, blocks broadcast and multiplied in HBM, partials merged on
+// the device, C returned device-resident.
+template <typename SR, typename NUO, typename UDERO, typename IU, typename NU1, typename NU2>
+SpParMat<IU, NUO, UDERO> Mult_AnXBn_Synch(SpParMat<IU, NU1, combblas_hip::SpDCColsDev<IU, NU1>>& A,
+                                          SpParMat<IU, NU2, combblas_hip::SpDCColsDev<IU, NU2>>& B,
+                                          bool clearA = false, bool clearB = false) {
+  static_assert(std::is_same<UDERO, combblas_hip::SpDCColsDev<IU, NUO>>::value,
+                "device-resident operands give a device-resident product");
+  typedef combblas_hip::SpDCColsDev<IU, NU1> DA;
+  typedef combblas_hip::SpDCColsDev<IU, NU2> DB;
+  if (!CheckSpGEMMCompliance(A, B)) return SpParMat<IU, NUO, UDERO>();
+  int stages, dummy;
+  std::shared_ptr<CommGrid> GridC = ProductGrid(A.getcommgrid().get(), B.getcommgrid().get(), stages, dummy, dummy);
+  const IU C_m = A.seq().getnrow(), C_n = B.seq().getncol();
+  auto Asizes = combblas_hip::GetSetSizes(A.seq(), A.getcommgrid()->GetRowWorld());
+  auto Bsizes = combblas_hip::GetSetSizes(B.seq(), B.getcommgrid()->GetColWorld());
+  const int Aself = A.getcommgrid()->GetRankInProcRow();
+  const int Bself = B.getcommgrid()->GetRankInProcCol();
+  std::vector<cbh_mat*> tomerge;
+  for (int i = 0; i < stages; ++i) {
+    DA Arecv;
+    DB Brecv;
+    DA& Ai = (i == Aself) ? A.seq() : Arecv;
+    DB& Bi = (i == Bself) ? B.seq() : Brecv;
+    combblas_hip::BCastMatrix(GridC->GetRowWorld(), Ai, Asizes[i], i);
+    combblas_hip::BCastMatrix(GridC->GetColWorld(), Bi, Bsizes[i], i);
+    cbh_mat* Ci = combblas_hip::local_multiply<SR, NUO, NU1, NU2>(Ai.mat(), Bi.mat());
+    int64_t nnz = 0;
+    cbh_mat_info(Ci, nullptr, nullptr, &nnz, nullptr, nullptr);
+    if (nnz > 0) tomerge.push_back(Ci);  // `if(!C_cont->isZero()) tomerge.push_back`
+    else cbh_mat_free(combblas_hip::context(), Ci);
+  }  // received blocks are freed at the end of their stage (the reference's clearA/clearB = i != self)
+  if (clearA) A.seq() = DA();
+  if (clearB) B.seq() = DB();
+  cbh_mat* C = nullptr;
+  if (tomerge.empty()) {
+    int rc = cbh_mat_create(combblas_hip::context(), C_m, C_n, 0, 0, combblas_hip::dtype_of<NUO>::value,
+                            (int64_t)sizeof(NUO), &C);
+    if (rc != CBH_OK) combblas_hip::die(combblas_hip::context(), rc, "cbh_mat_create");
+  } else if (tomerge.size() == 1) {
+    C = tomerge[0];  // one partial: it is the product (no copy round trip)
+  } else {
+    int rc = cbh_merge(combblas_hip::context(), combblas_hip::semiring_traits<SR>::code, (int)tomerge.size(),
+                       tomerge.data(), &C);
+    if (rc != CBH_OK) combblas_hip::die(combblas_hip::context(), rc, "cbh_merge");
+    for (cbh_mat* p : tomerge) cbh_mat_free(combblas_hip::context(), p);
+  }
+  return SpParMat<IU, NUO, UDERO>(new UDERO(C), GridC);
+}
+
+}  // namespace combblas
