@@ -4,9 +4,10 @@
 //   densify_cp     A's DCSC -> dense column pointers        [Dcsc::ConstructAux/FillColInds, dcsc.cpp:983-1010,1282-1344]
 //   flop_kernel    flop_j, rmin_j, rmax_j per column of B    [estimateFLOP, mtSpGEMM.h:1057-1134]
 //   bin_*          columns binned by flop (symbolic) / nnz (numeric), large bins ordered by size
-//   tile_kernel<SYM>  exact nnz per column                   [estimateNNZ_Hash, mtSpGEMM.h:806-933]
-//   hipcub scan    column offsets of C                        [prefixsum, mtSpGEMM.h:23-70]
-//   tile_kernel<NUM>  values, rows ascending per column      [LocalHybridSpGEMM loop, mtSpGEMM.h:289-441]
+//   task_kernel<TSYM>  exact nnz per task (row range of a column)  [estimateNNZ_Hash, mtSpGEMM.h:806-933]
+//   hipcub scan    task / column offsets of C                  [prefixsum, mtSpGEMM.h:23-70]
+//   task_kernel<TNUM|TDENSE>  values, rows ascending           [LocalHybridSpGEMM loop, mtSpGEMM.h:289-441]
+//   cbh_merge      task_kernel in merge mode                   [MultiwayMerge, MultiwayMerge.h:411-526]
 //   compact_cols   drop empty columns -> DCSC of C            [SpDCCols(SpTuples), SpDCCols.cpp:109-183]
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -412,18 +413,6 @@ __global__ __launch_bounds__(256) void checksum_kernel(const int64_t* __restrict
   }
 }
 
-// ============================================================================ kernel configurations
-// symbolic: small (flop <= 256): 128 threads, 512-key hash; mid (flop <= 4096): 256 threads,
-//           8192-key hash, one tile; large: 512 threads, LDS bitmap of 12288 words = 393,216 rows
-//           per tile (heavy columns: <= 11 tiles at scale 22, exact, no hashing).
-// numeric : small (nnz <= 256) 512(+64)-slot table; large: 4096(+64) slots, tiles of <= 2048 outputs.
-constexpr int64_t kSymMidCap = 4096;
-struct SymSmall { static constexpr int T = 512, BS = 128, EMAX = 256; };
-struct SymMid { static constexpr int T = 8192, BS = 256, EMAX = 512; };
-struct SymBmp { static constexpr int T = 12288, BS = 512, EMAX = 512; };
-struct NumSmall { static constexpr int T = 512, BS = 128, EMAX = 256; };
-struct NumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512; };
-
 static size_t next_event(cbh_ctx* ctx) {
   if (ctx->evused == ctx->evpool.size()) {
     hipEvent_t e;
@@ -445,45 +434,6 @@ static void flush_records(cbh_ctx* ctx) {
   }
   ctx->recs.clear();
   ctx->evused = 0;
-}
-
-template <class SR, class CFG, int MODE>
-static int launch_tile(cbh_ctx* ctx, const TileArgs& args, int64_t first, int64_t count, int kind = -1,
-                       double bytes = 0) {
-  if (count <= 0) return CBH_OK;
-  size_t e0 = (size_t)-1;
-  if (ctx->timing && kind >= 0) {
-    e0 = next_event(ctx);
-    if (e0 != (size_t)-1) (void)hipEventRecord(ctx->evpool[e0], ctx->stream);
-  }
-  using C = TileCfg<SR, CFG::T, CFG::BS, CFG::EMAX, MODE>;
-  auto kern = tile_kernel<SR, CFG::T, CFG::BS, CFG::EMAX, MODE>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    CBH_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)C::bytes));
-    attr_set = true;
-  }
-  TileArgs a = args;
-  a.cols = args.cols + first;
-  // grid.x limit is 2^31-1; launch in slices for safety
-  const int64_t kMaxGrid = 1ll << 30;
-  for (int64_t off = 0; off < count; off += kMaxGrid) {
-    const int64_t n = std::min(kMaxGrid, count - off);
-    TileArgs b = a;
-    b.cols = a.cols + off;
-    b.ncols = n;
-    hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(CFG::BS), C::bytes, ctx->stream, b);
-    CBH_HIP(ctx, hipGetLastError());
-  }
-  if (e0 != (size_t)-1) {
-    const size_t e1 = next_event(ctx);
-    if (e1 != (size_t)-1) {
-      (void)hipEventRecord(ctx->evpool[e1], ctx->stream);
-      ctx->recs.push_back({kind, e0, e1, bytes});
-    }
-  }
-  return CBH_OK;
 }
 
 // Bins the items [0, n) (column slots or tasks) by work; writes item ids + col0 into `ids`.
@@ -542,29 +492,6 @@ static bool diag_enabled() {
   }();
   return v != 0;
 }
-template <class SR, class CFG, int MODE>
-static int launch_large_diag(cbh_ctx* ctx, const TileArgs& a, const BinLists& bl, const char* what) {
-  int64_t first = bl.large_first;
-  for (int lg = kSub - 1; lg >= 0; --lg) {
-    const int64_t n = bl.sub_count[lg];
-    if (!n) continue;
-    hipEvent_t e0, e1;
-    (void)hipEventCreate(&e0);
-    (void)hipEventCreate(&e1);
-    (void)hipEventRecord(e0, ctx->stream);
-    CBH_TRY((launch_tile<SR, CFG, MODE>(ctx, a, first, n)));
-    (void)hipEventRecord(e1, ctx->stream);
-    (void)hipEventSynchronize(e1);
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, e0, e1);
-    std::fprintf(stderr, "[cbh diag] %s work 2^%d: %lld cols, %.3f ms\n", what, lg, (long long)n, ms);
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    first += n;
-  }
-  return CBH_OK;
-}
-
 static int exclusive_scan_i64(cbh_ctx* ctx, Scratch& S, const int64_t* in, int64_t* out, int64_t n) {
   size_t tmp = 0;
   CBH_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)n, ctx->stream));
@@ -711,6 +638,10 @@ __global__ void chunk_count_kernel(const int32_t* __restrict__ tcol, const int64
   cnt[t] = ne > emin ? ne : 0;
 }
 
+__global__ void iota_scaled_kernel(int64_t* __restrict__ x, int64_t n, int64_t k) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = i * k;
+}
 __global__ void gather_i64_kernel(const int64_t* __restrict__ src, const int64_t* __restrict__ idx, int64_t n,
                                   int64_t* __restrict__ dst) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -750,7 +681,7 @@ static bool kDenseEnabled() {
 // task_kernel launch with optional HIP-event timing (kernel configurations: device/numeric.h;
 // measured at scale 22: a 1024-thread workgroup with an 8192-slot table, half the sub-tiles, ran
 // 28 % slower than two 512-thread workgroups per CU with 4096 slots)
-template <class SR, class CFG, int MODE>
+template <class SR, class CFG, int MODE, bool MERGE = false>
 static int launch_task(cbh_ctx* ctx, const TaskArgs& args, int64_t first, int64_t count, int kind = -1,
                        double bytes = 0) {
   if (count <= 0) return CBH_OK;
@@ -759,7 +690,7 @@ static int launch_task(cbh_ctx* ctx, const TaskArgs& args, int64_t first, int64_
     e0 = next_event(ctx);
     if (e0 != (size_t)-1) (void)hipEventRecord(ctx->evpool[e0], ctx->stream);
   }
-  CBH_HIP(ctx, (launch_tasks<SR, CFG, MODE>(args, first, count, ctx->stream)));
+  CBH_HIP(ctx, (launch_tasks<SR, CFG, MODE, MERGE>(args, first, count, ctx->stream)));
   if (e0 != (size_t)-1) {
     const size_t e1 = next_event(ctx);
     if (e1 != (size_t)-1) {
@@ -1734,28 +1665,22 @@ int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* p
     CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
     CBH_TRY(check_err(ctx));  // column ids outside [0, n): stop before they index anything
     if (ncols == 0) return empty_result(ctx, P0->m, n, dtype, C);
-    int64_t *jcC, *seg_start, *seg_len, *work, *nnz, *Ccp;
-    int32_t *rmin, *rmax, *cols;
+    int64_t *jcC, *seg_start, *seg_len, *work, *Ccp;
+    int32_t *rmin, *rmax;
     CBH_TRY(S.get(&jcC, ncols));
     CBH_TRY(S.get(&seg_start, ncols * nlists));
     CBH_TRY(S.get(&seg_len, ncols * nlists));
     CBH_TRY(S.get(&work, ncols + 1));
-    CBH_TRY(S.get(&nnz, ncols + 1));
     CBH_TRY(S.get(&Ccp, ncols + 1));
     CBH_TRY(S.get(&rmin, ncols));
     CBH_TRY(S.get(&rmax, ncols));
-    CBH_TRY(S.get(&cols, ncols));
     hipLaunchKernelGGL(union_cols_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, flag, idx, n, jcC);
     CBH_HIP(ctx, hipMemsetAsync(seg_len, 0, sizeof(int64_t) * ncols * nlists, ctx->stream));
     CBH_HIP(ctx, hipMemsetAsync(seg_start, 0, sizeof(int64_t) * ncols * nlists, ctx->stream));
     ListRows lr;
     std::memset(&lr, 0, sizeof(lr));
-    TileArgs a;
-    std::memset(&a, 0, sizeof(a));
     for (int l = 0; l < nlists; ++l) {
       lr.ir[l] = parts[l]->ir;
-      a.lir[l] = parts[l]->ir;
-      a.lnum[l] = parts[l]->num;
       if (parts[l]->nzc)
         hipLaunchKernelGGL(merge_seg_kernel, dim3(blocks_for(parts[l]->nzc, 256)), dim3(256), 0, ctx->stream,
                            parts[l]->jc, parts[l]->cp, parts[l]->nzc, idx, l, nlists, seg_start, seg_len);
@@ -1763,44 +1688,97 @@ int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* p
     hipLaunchKernelGGL(merge_work_kernel, dim3(blocks_for(ncols, 256)), dim3(256), 0, ctx->stream, seg_start, seg_len,
                        nlists, lr, ncols, work, rmin, rmax);
     CBH_HIP(ctx, hipGetLastError());
-    a.seg_start = seg_start;
-    a.seg_len = seg_len;
-    a.nlists = nlists;
-    a.nnzA = INT64_MAX;
-    a.ncolA = INT64_MAX;
-    a.nnzB = INT64_MAX;
-    a.ccap = INT64_MAX;
-    a.nslots = ncols;
-    a.cols = cols;
-    a.rmin = rmin;
-    a.rmax = rmax;
-    a.err = ctx->d_err;
-    // symbolic
-    CBH_HIP(ctx, hipMemsetAsync(nnz, 0, sizeof(int64_t) * (ncols + 1), ctx->stream));
-    BinLists bl;
-    CBH_TRY(make_bins(ctx, S, work, ncols, 0, cols, &bl, BinCaps{kSmallCap, kSymMidCap}));
-    a.work = work;
-    a.nnz_out = nnz;
-    CBH_TRY((launch_tile<SR, SymBmp, MODE_SYM_BMP_MRG>(ctx, a, bl.large_first, bl.large_count, CBH_K_MERGE_SYM)));
-    CBH_TRY((launch_tile<SR, SymMid, MODE_SYM_MRG>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_MERGE_SYM)));
-    CBH_TRY((launch_tile<SR, SymSmall, MODE_SYM_MRG>(ctx, a, bl.small_first, bl.small_count, CBH_K_MERGE_SYM)));
-    CBH_TRY(exclusive_scan_i64(ctx, S, nnz, Ccp, ncols + 1));
+    // task-parallel merge: every union column becomes row-range tasks of ~kTaskFlops list
+    // entries (as the SpGEMM's columns), symbolic -> scan -> numeric on the task kernels in
+    // merge mode (entries = the lists' segments of the column; task_kernel.h MERGE)
+    const int32_t RB = (int32_t)std::max<int64_t>(1, (P0->m + kRowBlocks - 1) / kRowBlocks);
+    int64_t *bcp, *scnt, *tstart;
+    CBH_TRY(S.get(&bcp, ncols + 1));
+    CBH_TRY(S.get(&scnt, ncols + 1));
+    CBH_TRY(S.get(&tstart, ncols + 1));
+    hipLaunchKernelGGL(iota_scaled_kernel, dim3(blocks_for(ncols + 1, 256)), dim3(256), 0, ctx->stream, bcp, ncols + 1,
+                       (int64_t)nlists);
+    hipLaunchKernelGGL(task_count_kernel, dim3(blocks_for(ncols, 256)), dim3(256), 0, ctx->stream, work, rmin, rmax,
+                       ncols, task_flops(), RB, scnt);
+    CBH_HIP(ctx, hipMemsetAsync(scnt + ncols, 0, sizeof(int64_t), ctx->stream));
+    CBH_TRY(exclusive_scan_i64(ctx, S, scnt, tstart, ncols + 1));
+    int64_t ntasks = 0;
+    CBH_HIP(ctx, hipMemcpyAsync(&ntasks, tstart + ncols, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ntasks > INT32_MAX) return fail(ctx, CBH_E_INTERNAL, "more than 2^31 merge tasks");
+    const int64_t nt = std::max<int64_t>(ntasks, 1);
+    int32_t *tcol, *tlo, *thi, *order;
+    uint8_t* tfull;
+    int64_t *twork, *tunits, *tcnt, *toff;
+    CBH_TRY(S.get(&tcol, nt));
+    CBH_TRY(S.get(&tlo, nt));
+    CBH_TRY(S.get(&thi, nt));
+    CBH_TRY(S.get(&tfull, nt));
+    CBH_TRY(S.get(&twork, nt));
+    CBH_TRY(S.get(&tunits, nt));
+    CBH_TRY(S.get(&tcnt, nt + 1));
+    CBH_TRY(S.get(&toff, nt + 1));
+    CBH_TRY(S.get(&order, nt));
+    hipLaunchKernelGGL(task_fill_kernel, dim3(blocks_for(ncols, 4)), dim3(256), 0, ctx->stream, tstart, work, rmin, rmax,
+                       bcp, ncols, RB, tcol, tlo, thi, tfull, twork, tunits);
+    CBH_HIP(ctx, hipGetLastError());
+    CBH_HIP(ctx, hipMemsetAsync(tcnt, 0, sizeof(int64_t) * (nt + 1), ctx->stream));
+    TaskArgs ta;
+    std::memset(&ta, 0, sizeof(ta));
+    ta.Bcp = bcp;
+    ta.tcol = tcol;
+    ta.tlo = tlo;
+    ta.thi = thi;
+    ta.tfull = tfull;
+    ta.err = ctx->d_err;
+    ta.nnzA = INT64_MAX;
+    ta.ncolA = INT64_MAX;
+    ta.ntasks = ntasks;
+    ta.ccap = INT64_MAX;
+    ta.mstart = seg_start;
+    ta.mlen = seg_len;
+    ta.nl = nlists;
+    for (int l = 0; l < nlists; ++l) {
+      ta.lir[l] = parts[l]->ir;
+      ta.lnum[l] = parts[l]->num;
+    }
+    // symbolic: distinct rows per task
+    BinLists bs;
+    CBH_TRY(make_bins(ctx, S, twork, ntasks, 0, order, &bs, BinCaps{kSmallCap, kSmallCap}, tunits));
+    ta.order = order;
+    ta.twork = twork;
+    ta.cnt = tcnt;
+    using Dummy = PlusTimesD<int64_t>;
+    CBH_TRY((launch_task<Dummy, TSymLarge, MODE_TSYM, true>(ctx, ta, bs.large_first, bs.large_count, CBH_K_MERGE_SYM,
+                                                             4.0 * bs.units[2])));
+    CBH_TRY((launch_task<Dummy, TSymSmall, MODE_TSYM, true>(ctx, ta, bs.small_first, bs.small_count + bs.mid_count,
+                                                             CBH_K_MERGE_SYM, 4.0 * (bs.units[0] + bs.units[1]))));
+    CBH_TRY(exclusive_scan_i64(ctx, S, tcnt, toff, ntasks + 1));
+    hipLaunchKernelGGL(gather_i64_kernel, dim3(blocks_for(ncols + 1, 256)), dim3(256), 0, ctx->stream, toff, tstart,
+                       ncols + 1, Ccp);
+    hipLaunchKernelGGL(add_i64_kernel, dim3(blocks_for(ntasks, 256)), dim3(256), 0, ctx->stream, tunits, tcnt, ntasks,
+                       tunits);
     int64_t total = 0;
     CBH_HIP(ctx, hipMemcpyAsync(&total, Ccp + ncols, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
     CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
     CBH_TRY(check_err(ctx));
     cbh_mat* out;
-    CBH_TRY(new_mat(ctx, P0->m, n, total, ncols, dtype, &out));
-    int rc = make_bins(ctx, S, nnz, ncols, 0, cols, &bl, BinCaps{kSmallCap, kSmallCap});
+    CBH_TRY(new_mat(ctx, P0->m, n, total, ncols, dtype, &out, P0->vbytes));
+    BinLists bl;
+    int rc = make_bins(ctx, S, tcnt, ntasks, 0, order, &bl, BinCaps{kSmallCap, kSmallCap}, tunits);
     if (rc == CBH_OK) {
-      a.work = nnz;
-      a.Ccp = Ccp;
-      a.cbase = 0;
-      a.Cir = out->ir;
-      a.Cnum = out->num;
-      rc = launch_tile<SR, NumLarge, MODE_NUM_MRG>(ctx, a, bl.large_first, bl.large_count, CBH_K_MERGE_NUM);
+      ta.twork = tcnt;
+      ta.cnt = nullptr;
+      ta.toff = toff;
+      ta.cbase = 0;
+      ta.Cir = out->ir;
+      ta.Cnum = out->num;
+      constexpr double eb = 4.0 + sizeof(typename SR::val_t);  // entries read + outputs written
+      rc = launch_task<SR, TNumLargeFor<SR>, MODE_TNUM, true>(ctx, ta, bl.large_first, bl.large_count, CBH_K_MERGE_NUM,
+                                                               eb * bl.units[2]);
       if (rc == CBH_OK)
-        rc = launch_tile<SR, NumSmall, MODE_NUM_MRG>(ctx, a, bl.small_first, bl.small_count, CBH_K_MERGE_NUM);
+        rc = launch_task<SR, TNumSmallFor<SR>, MODE_TNUM, true>(ctx, ta, bl.small_first, bl.small_count + bl.mid_count,
+                                                                 CBH_K_MERGE_NUM, eb * (bl.units[0] + bl.units[1]));
     }
     if (rc == CBH_OK) {
       (void)hipMemcpyAsync(out->jc, jcC, sizeof(int64_t) * ncols, hipMemcpyDeviceToDevice, ctx->stream);

@@ -1,0 +1,154 @@
+// block_ops.h -- workgroup-level building blocks of the gfx950 SpGEMM kernels (task_kernel.h,
+// combblas_amd/csrc/apps.h): device-side bounds-guard reporting, block scans (sum, exclusive,
+// prefix-max for the owner map), row-sorted lower bounds, and the table constants.
+//
+// Numeric tables use an ORDER-PRESERVING slot map (slot = (row-lo)*T/(hi-lo)) with forward linear
+// probing that never wraps (kGuard slots past T): keys end up globally sorted once each run of
+// occupied slots is sorted (proof in DESIGN.md §3.3), replacing the per-column std::sort
+// (mtSpGEMM.h:434). A sub-tile whose probes exceed kPmax (clustered rows) or run off the table
+// is retried with half the row range.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "semiring.h"
+
+namespace cbh {
+
+constexpr int32_t kEmpty = -1;
+constexpr int kGuard = 64;  // numeric tables: extra slots past T (probing never wraps)
+constexpr int kPmax = 64;   // probe limit before the tile is split in half
+
+constexpr int kMaxLists = 16;
+
+// Records a violated bounds guard instead of faulting: err[2] = count, err[3] |= 1<<site, and the
+// first failure's context in err[4..15].
+__device__ __forceinline__ void guard_fail(int* err, int site, int64_t v0 = 0, int64_t v1 = 0, int64_t v2 = 0,
+                                           int64_t v3 = 0, int64_t v4 = 0, int64_t v5 = 0) {
+  atomicAdd(&err[2], 1);
+  atomicOr(&err[3], 1 << site);
+  if (atomicCAS(&err[4], 0, site) == 0) {
+    err[5] = (int)v0;
+    err[6] = (int)v1;
+    err[7] = (int)v2;
+    err[8] = (int)v3;
+    err[9] = (int)v4;
+    err[10] = (int)v5;
+    err[11] = (int)blockIdx.x;
+    err[12] = (int)threadIdx.x;
+  }
+}
+
+template <int NW>
+__device__ __forceinline__ int block_sum_int(int v, int* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  int t = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) t += red[w];
+  return t;
+}
+
+// In-place exclusive scan of x[0..n) (LDS), x[n] = total. All threads must call.
+template <int BS>
+__device__ __forceinline__ void block_scan_excl(int32_t* x, int n, int* red) {
+  constexpr int NW = BS / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int carry = 0;
+  for (int base = 0; base < n; base += BS) {
+    const int i = base + tid;
+    const int v = i < n ? x[i] : 0;
+    int s = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      int y = __shfl_up(s, d);
+      if (lane >= d) s += y;
+    }
+    if (lane == 63) red[wid] = s;
+    __syncthreads();
+    int wpre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const int r = red[w];
+      wpre += (w < wid) ? r : 0;
+      tot += r;
+    }
+    if (i < n) x[i] = carry + wpre + s - v;
+    carry += tot;
+    __syncthreads();
+  }
+  if (tid == 0) x[n] = carry;
+  __syncthreads();
+}
+
+// In-place inclusive prefix-max of own[0..WIN) (LDS); each thread owns E = WIN/BS contiguous slots.
+template <int BS, int WIN, class OT = int32_t>
+__device__ __forceinline__ void block_max_scan(OT* own, int* red) {
+  constexpr int E = WIN / BS, NW = BS / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int v[E];
+  int m = -1;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int x = own[tid * E + e];
+    m = x > m ? x : m;
+    v[e] = m;
+  }
+  int s = m;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(s, d);
+    if (lane >= d) s = y > s ? y : s;
+  }
+  if (lane == 63) red[wid] = s;
+  int ex = __shfl_up(s, 1);
+  if (lane == 0) ex = -1;
+  __syncthreads();
+  int wpre = -1;
+#pragma unroll
+  for (int w = 0; w < NW; ++w)
+    if (w < wid) wpre = red[w] > wpre ? red[w] : wpre;
+  const int carry = ex > wpre ? ex : wpre;
+#pragma unroll
+  for (int e = 0; e < E; ++e) own[tid * E + e] = (OT)(v[e] > carry ? v[e] : carry);
+  __syncthreads();
+}
+
+// first q in [lo, hi) with p[q] >= key (p sorted ascending); global memory.
+__device__ __forceinline__ int lower_bound_rows(const int32_t* __restrict__ p, int lo, int hi, int64_t key) {
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((int64_t)p[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+// Galloping lower bound from `lo`: the next tile's segment usually ends a few entries later,
+// so probe lo, lo+1, lo+3, lo+7, ... (same cache line) before bisecting.
+__device__ __forceinline__ int gallop_rows(const int32_t* __restrict__ p, int lo, int hi, int64_t key) {
+  if (lo >= hi || (int64_t)p[lo] >= key) return lo;
+  int step = 1, prev = lo;
+  while (true) {
+    const int nx = lo + step;
+    if (nx >= hi) return lower_bound_rows(p, prev + 1, hi, key);
+    if ((int64_t)p[nx] >= key) return lower_bound_rows(p, prev + 1, nx, key);
+    prev = nx;
+    step <<= 1;
+  }
+}
+// first i in [0, n] with x[i] >= key (x sorted); LDS.
+__device__ __forceinline__ int lower_bound_lds(const int32_t* x, int n, int key) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (x[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+}  // namespace cbh

@@ -39,11 +39,11 @@ static_assert(kChunkMin <= TSymSmall::EMAX && kChunkMin <= TSymLarge::EMAX && kC
 
 // Launches task_kernel<SR, CFG, MODE> over order[first, first+count) on `stream` (grid slices of
 // at most 2^30 workgroups). The dynamic-LDS attribute is set once per instantiation.
-template <class SR, class CFG, int MODE>
+template <class SR, class CFG, int MODE, bool MERGE = false>
 hipError_t launch_tasks(const TaskArgs& args, int64_t first, int64_t count, hipStream_t stream) {
   if (count <= 0) return hipSuccess;
   using C = TaskCfg<SR, CFG::T, CFG::BS, CFG::EMAX, CFG::U, MODE>;
-  auto kern = task_kernel<SR, CFG::T, CFG::BS, CFG::EMAX, CFG::U, MODE>;
+  auto kern = task_kernel<SR, CFG::T, CFG::BS, CFG::EMAX, CFG::U, MODE, MERGE>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),

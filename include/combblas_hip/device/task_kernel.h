@@ -1,9 +1,9 @@
-// gfx950 SpGEMM kernels, TASK-PARALLEL form (the SpGEMM hot path; merges still use tile_kernel.h).
+// gfx950 SpGEMM kernels, TASK-PARALLEL form (the SpGEMM hot path; merges still use block_ops.h).
 //
 // A task is one row range [lo, hi) of one output column j (one nonzero column of B). Heavy
 // columns are cut into tasks of about kTaskFlops products, so the heaviest column of R-MAT
 // scale 22 (15.7 M products, 752 K outputs) spreads over hundreds of workgroups instead of one
-// (the per-column row-tile loop of tile_kernel.h was tail-bound). R-MAT rows are scrambled
+// (the per-column row-tile loop of block_ops.h was tail-bound). R-MAT rows are scrambled
 // (uniform), so equal-width row ranges carry equal work.
 //
 // Inside a task the range is processed in SUB-TILES that fit one LDS table, one after another.
@@ -29,7 +29,7 @@
 // Columns with more than EMAX entries are processed in entry chunks whose cursors live in HBM
 // between sub-tiles (double-buffered, so that a retried sub-tile restarts from committed ones).
 #pragma once
-#include "tile_kernel.h"
+#include "block_ops.h"
 
 namespace cbh {
 
@@ -98,6 +98,13 @@ struct TaskArgs {
   int64_t* gcur0;
   int64_t* gcur1;
   int64_t* gend;
+  // merge mode (MultiwayMerge of k partial lists): entry l of output column slot c is list l's
+  // segment [mstart[c*nl+l], +mlen[c*nl+l]) of lir[l] / lnum[l]; no multiply
+  const int64_t* mstart;
+  const int64_t* mlen;
+  int nl;
+  const int32_t* lir[kMaxLists];
+  const void* lnum[kMaxLists];
 };
 
 // first q in [lo, hi) with rows[q] >= key (rows sorted); global memory, 64-bit positions.
@@ -277,7 +284,11 @@ struct TaskCfg {
   static constexpr size_t bytes = al(o_red + sizeof(int32_t) * (2 * NW + 4));
 };
 
-template <class SR, int T, int BS, int EMAX, int U, int MODE>
+// MERGE: the entries of a task are the k lists' segments of its output column (MultiwayMerge,
+// MultiwayMerge.h:411-526); rows and values are addressed through list 0's arrays plus a
+// per-list element offset (all device allocations share one address space, 256-byte aligned),
+// so the sub-tile machinery above runs unchanged and the "product" is the list value itself.
+template <class SR, int T, int BS, int EMAX, int U, int MODE, bool MERGE = false>
 // 512-thread groups: two per CU (LDS-bound), so 4 waves per SIMD -> <= 128 VGPRs
 __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(TaskArgs a) {
   using C = TaskCfg<SR, T, BS, EMAX, U, MODE>;
@@ -307,9 +318,12 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
   typename C::own_t* own = reinterpret_cast<typename C::own_t*>(smem + C::o_own);
   int32_t* red = reinterpret_cast<int32_t*>(smem + C::o_red);
   __shared__ int32_t s_ovf;  // overflow flag of the current sub-tile (LDS; read after barriers)
+  __shared__ int64_t s_vdelta[kMaxLists];  // merge: list l's value index - row index (elements)
+  static_assert(!MERGE || EMAX >= kMaxLists, "merge entries fit one chunk");
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int32_t* __restrict__ rowsA = a.Air;
+  const int32_t* __restrict__ rowsA = MERGE ? a.lir[0] : a.Air;
+  const val_t* __restrict__ valsA = reinterpret_cast<const val_t*>(MERGE ? a.lnum[0] : a.Anum);
 #ifdef CBH_STAMPS
   uint64_t st_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t t_prev_ = __builtin_amdgcn_s_memtime();
@@ -321,8 +335,8 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
     return;
   }
   const int32_t c = a.tcol[task];
-  const int64_t e0 = a.Bcp[c];
-  const int64_t ne = a.Bcp[c + 1] - e0;
+  const int64_t e0 = MERGE ? 0 : a.Bcp[c];
+  const int64_t ne = MERGE ? a.nl : a.Bcp[c + 1] - e0;
   const int64_t work = a.twork[task];
   const int32_t tlo = a.tlo[task], thi = a.thi[task];
   const uint8_t full = a.tfull[task];
@@ -372,6 +386,23 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
   const int64_t go = chunked ? a.goff[task] : 0;
   int par = 0;  // which HBM cursor buffer holds the committed cursors
   auto load_entries = [&](int64_t first, int cnt, int32_t lo, bool lo_is_start, bool from_state) {
+    if constexpr (MERGE) {  // entry i = list i; positions are list 0-relative row indices
+      for (int i = tid; i < cnt; i += BS) {
+        const int64_t rdelta = (int64_t)(a.lir[i] - a.lir[0]);
+        s_vdelta[i] = (int64_t)(reinterpret_cast<const val_t*>(a.lnum[i]) - valsA) - rdelta;
+        ecol[i] = i;
+        const int64_t base = a.mstart[(int64_t)c * a.nl + i] + rdelta;
+        const int64_t end = base + a.mlen[(int64_t)c * a.nl + i];
+        int64_t cend = end;
+        if (!(full & 2) && base < end) cend = lb_rows64(rowsA, base, end, thi);
+        int64_t pos = base;
+        if (!lo_is_start && base < cend) pos = lb_rows64(rowsA, base, cend, lo);
+        epos[i] = pos;
+        eend[i] = cend;
+        enext[i] = pos < cend ? rowsA[pos] : kNoRow;
+      }
+      return;
+    }
     for (int i = tid; i < cnt; i += BS) {
       const int64_t p = e0 + first + i;
       const int32_t k = a.Bir[p];
@@ -437,7 +468,7 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
           nx2 = kNoRow;
         } else {
           const int32_t k = ecol[i];
-          const int32_t* blk = hub_blk(k);
+          const int32_t* blk = MERGE ? nullptr : hub_blk(k);
           stop = stop_search<8>(rowsA, p + 1, end, hi, blk, blk ? a.Acp[k] : 0, a.RB, nx2);
         }
       }
@@ -477,9 +508,12 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
         const int x = x0 < wn ? x0 : 0;
         const int i = own[x];
         const int64_t q = epos[i] + w0 + x;
-        r[u] = a.Air[q];
-        if constexpr (NUM)
+        r[u] = rowsA[q];
+        if constexpr (NUM && MERGE) {
+          if (with_vals) av[u] = valsA[q + s_vdelta[i]];
+        } else if constexpr (NUM) {
           if (with_vals) av[u] = SR::multiply(reinterpret_cast<const a_t*>(a.Anum)[q], escale[i]);
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
