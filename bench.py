@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-cols-frac", type=float, default=1.0 / 64, help="column sample of the CPU baseline")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--no-merge", action="store_true", help="skip the MultiwayMerge measurement (N=1)")
+    p.add_argument("--merge-cols-frac", type=float, default=1.0 / 16, help="B column block of the merge sample")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on a node; gloo only for rehearsals")
     p.add_argument("--share-gpu", action="store_true", help="rehearsal: every rank on cuda:0 (needs gloo)")
     return p.parse_args()
@@ -117,6 +119,65 @@ def cpu_baseline(scale, ef, frac):
     return {"value": round(2 * flops / dt / 1e9, 6), "unit": "GFLOP/s", "cores": cores, "kind": "port",
             "sample": sample + f": {flops} flops, median of 3 after 1 warm-up = {dt:.3f} s (oracle restatement), "
                                f"nnzC {C.nnz}"}
+
+
+def host_block(A, c0, c1, r0, r1):
+    """A(r0:r1, c0:c1) of a HostDcsc with the same dimensions (entries outside are dropped)"""
+    import combblas_amd as cb
+
+    cols = np.repeat(A.jc, np.diff(A.cp))
+    keep = (cols >= c0) & (cols < c1) & (A.ir >= r0) & (A.ir < r1)
+    c = cols[keep]
+    jc, counts = np.unique(c, return_counts=True)
+    return cb.HostDcsc(A.m, A.n, jc, np.concatenate([[0], np.cumsum(counts)]), A.ir[keep], A.num[keep])
+
+
+def merge_measurement(A, frac, steps):
+    """MultiwayMerge (MultiwayMerge.h:411-526) of two SUMMA-stage partials on one GPU, as a 2-stage
+    SUMMA would produce them: the inner dimension split in halves, P_s = A(:, K_s) * A(K_s, J) for a
+    block J of B's columns, then C(:, J) = P_1 + P_2 by cbh_merge. Timed with HIP events on the
+    library stream (merge_sym + merge_num kernels), checked against the unsplit product."""
+    import combblas_amd as cb
+
+    ctx = cb.Context(0)  # torch-allocated: the check compares device tensors
+    n = A.n
+    J = max(1, int(n * frac))
+    h = n // 2
+    B = host_block(A, 0, J, 0, n)
+    dA = [cb.SpDCCols.from_host(ctx, host_block(A, 0, h, 0, n)), cb.SpDCCols.from_host(ctx, host_block(A, h, n, 0, n))]
+    dB = [cb.SpDCCols.from_host(ctx, host_block(B, 0, J, 0, h)), cb.SpDCCols.from_host(ctx, host_block(B, 0, J, h, n))]
+    P = [cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dA[i], dB[i]) for i in range(2)]
+    for x in dA + dB:
+        x.free()
+    ctx.synchronize()
+    ctx.reset_kernel_stats()
+    ctx.enable_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        M = cb.MultiwayMerge(cb.PlusTimesSRing, P, A.m, A.n)
+        M.free()
+    ctx.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    ctx.enable_timing(False)
+    ks = ctx.kernel_stats()
+    M = cb.MultiwayMerge(cb.PlusTimesSRing, P, A.m, A.n)
+    full = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, cb.SpDCCols.from_host(ctx, A), cb.SpDCCols.from_host(ctx, B))
+    ok = M.nnz == full.nnz and bool((M.tensors()[2] == full.tensors()[2]).all().item()) and \
+        bool((M.tensors()[3] == full.tensors()[3]).all().item())
+    kms = (ks["merge_sym"]["ms"] + ks["merge_num"]["ms"]) / steps
+    num_ms = ks["merge_num"]["ms"] / max(ks["merge_num"]["launches"], 1) * (ks["merge_num"]["launches"] / steps)
+    alg = ks["merge_num"]["alg_bytes"] / steps  # (s_i+s_v) * (entries read + outputs written)
+    out = {"sample": f"C(:, 0:{J}) = P1 + P2, inner dimension split at {h} (2-stage SUMMA partials)",
+           "nnz_partials": [P[0].nnz, P[1].nnz], "nnz_merged": M.nnz, "matches_unsplit_product": ok,
+           "merge_ms": round(kms, 3), "merge_num_ms": round(num_ms, 3), "wall_ms": round(wall * 1e3, 3),
+           "roofline": {"bound": "hbm", "achieved": round(alg / (num_ms / 1e3) / 1e9, 2) if num_ms > 0 else 0.0,
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(alg / (num_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if num_ms > 0 else 0.0,
+                        "alg_bytes_per_merge": round(alg)}}
+    for x in P + [M, full]:
+        x.free()
+    ctx.close()
+    return out
 
 
 def grid_shape(world):
@@ -313,6 +374,11 @@ def main():
         check["ok"] = bool((known is None or int(nnz_all) == known) and vsum == float(closed_sum)
                            and (dg is None or gold is None or str(dg) == gold))
 
+    merge = None
+    if world == 1 and not args.no_merge:
+        del dA, dB
+        ctx.close()  # releases the phase workspace before the merge sample allocates its own
+        merge = merge_measurement(cb.rmat(args.scale, args.edgefactor, dtype=np.float64), args.merge_cols_frac, 3)
     if rank == 0:
         base = None
         if world == 1 and not args.no_cpu_baseline:
@@ -326,7 +392,7 @@ def main():
                        "edgefactor": args.edgefactor, "nnzA": nnzA, "flops": int(flops), "nnzC": int(nnzC),
                        "phases": st["phases"], "parallelism": parallelism,
                        "kernel_ms": {n: round(v["ms"] / max(args.steps, 1), 3) for n, v in ks.items()}},
-            "roofline": roofline, "cpu_baseline": base, "check": check,
+            "roofline": roofline, "cpu_baseline": base, "check": check, "merge": merge,
         }
         print(json.dumps(out), flush=True)
     barrier()

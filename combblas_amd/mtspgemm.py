@@ -76,8 +76,9 @@ def MultiwayMerge(SR: Semiring, lists, mdim=0, ndim=0, delarrs=False) -> SpDCCol
         if (mdim or ndim) and (L.m != mdim or L.n != ndim):
             raise _lib.CombBLASHipError(3002, "Dimensions of SpTuples do not match on multiwayMerge()")
     cur = list(lists)
+    first = True
     # the kernel merges up to 16 lists at once; larger fan-in is merged hierarchically
-    while len(cur) > 1 or cur is lists:
+    while len(cur) > 1 or first:
         nxt = []
         for i in range(0, len(cur), 16):
             grp = cur[i:i + 16]
@@ -85,9 +86,10 @@ def MultiwayMerge(SR: Semiring, lists, mdim=0, ndim=0, delarrs=False) -> SpDCCol
             h = ctypes.c_void_p()
             check(lib().cbh_merge(ctx.h, SR.code, len(grp), arr, ctypes.byref(h)), ctx.h)
             nxt.append(SpDCCols(ctx, h))
-        if cur is not lists:
+        if not first:  # intermediate results of the hierarchy (the inputs are the caller's)
             for g in cur:
                 g.free()
+        first = False
         cur = nxt
     if delarrs:
         for L in lists:
