@@ -34,7 +34,15 @@ sys.path.insert(0, HERE)
 METRIC = "semiring GFLOP/s for R-MAT A² SpGEMM at 1/2/4/8 GPUs; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
 DOMINANT = "num_large"
-DOMINANT_KERNEL = "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 8, 1>"
+DOMINANT_KERNEL = "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 8, 1, false>"
+
+
+_T0 = time.perf_counter()
+
+
+def log(msg):
+    """stage progress on stderr (the JSON line alone goes to stdout)"""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
 def parse():
@@ -76,6 +84,7 @@ def cpu_baseline(scale, ef, frac):
             cmd = [ref, "slice", str(scale), str(ef), "0", str(n), "3", "pt_f64", str(stride)]
             if ranks > 1:
                 cmd = [mpirun, "-np", str(ranks)] + cmd
+            log(f"CPU baseline layout {ranks} rank(s) x {thr} threads")
             try:
                 r = subprocess.run(cmd, env=env, cwd="/tmp", capture_output=True, text=True, timeout=600)
                 line = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -160,6 +169,7 @@ def merge_measurement(A, frac, steps):
     wall = (time.perf_counter() - t0) / steps
     ctx.enable_timing(False)
     ks = ctx.kernel_stats()
+    log(f"{args.steps} timed step(s): {(t1 - t0) / max(args.steps, 1) * 1e3:.1f} ms/step")
     M = cb.MultiwayMerge(cb.PlusTimesSRing, P, A.m, A.n)
     full = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, cb.SpDCCols.from_host(ctx, A), cb.SpDCCols.from_host(ctx, B))
     ok = M.nnz == full.nnz and bool((M.tensors()[2] == full.tensors()[2]).all().item()) and \
@@ -254,6 +264,7 @@ def main():
         return t.item()
 
     SR = cb.PlusTimesSRing
+    log(f"generating R-MAT scale {args.scale}")
     A = cb.rmat(args.scale, args.edgefactor, dtype=np.float64)
     nnzA = A.nnz
     closed_sum = product_value_sum(A)
@@ -320,6 +331,7 @@ def main():
             run()
             return acc["nnz"], acc["sum"], None
 
+    log(f"{args.warmup} warm-up step(s)")
     for _ in range(args.warmup):
         st = step()
     ctx.synchronize()
@@ -336,6 +348,7 @@ def main():
     t1 = time.perf_counter()
     ctx.enable_timing(False)
     ks = ctx.kernel_stats()
+    log(f"{args.steps} timed step(s): {(t1 - t0) / max(args.steps, 1) * 1e3:.1f} ms/step")
 
     my_s = (t1 - t0) / max(args.steps, 1)
     step_s = allreduce(my_s, dist.ReduceOp.MAX if world > 1 else None)
@@ -363,6 +376,7 @@ def main():
 
     check = None
     if not args.no_verify:
+        log("verification product (checksums)")
         nz, vs, dg = verify()
         nnz_all = allreduce(float(nz), dist.ReduceOp.SUM if world > 1 else None)
         vsum = allreduce(vs, dist.ReduceOp.SUM if world > 1 else None)
@@ -378,10 +392,12 @@ def main():
     if world == 1 and not args.no_merge:
         del dA, dB
         ctx.close()  # releases the phase workspace before the merge sample allocates its own
+        log("MultiwayMerge sample")
         merge = merge_measurement(cb.rmat(args.scale, args.edgefactor, dtype=np.float64), args.merge_cols_frac, 3)
     if rank == 0:
         base = None
         if world == 1 and not args.no_cpu_baseline:
+            log("CPU baseline (reference harness on a column sample)")
             base = cpu_baseline(args.scale, args.edgefactor, args.cpu_cols_frac)
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps,

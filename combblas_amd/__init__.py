@@ -7,7 +7,7 @@ kernels' entry points without the library raises.
 from .semirings import MinPlusSRing, OrAndSRing, PlusTimesSRing, SelectMaxSRing  # noqa: F401
 from .spdccols import Context, HostDcsc, SpDCCols  # noqa: F401
 from .mtspgemm import (EstimateLocalFLOP, LocalHybridSpGEMM, LocalSpGEMM, LocalSpGEMMHash,  # noqa: F401
-                       MultiwayMerge, PhasedSpGEMM, estimateFLOPandNNZ)
+                       MultiwayMerge, PhasedSpGEMM, SpGEMMPlan, estimateFLOPandNNZ)
 from .rmat import rmat, rmat_edges  # noqa: F401
 
 __all__ = ["Context", "HostDcsc", "SpDCCols", "PlusTimesSRing", "SelectMaxSRing", "MinPlusSRing", "OrAndSRing",

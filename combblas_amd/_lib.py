@@ -51,6 +51,7 @@ SIGNATURES = {
     "cbh_ctx_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "cbh_ctx_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
     "cbh_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbh_ctx_trim": (ctypes.c_int, [ctypes.c_void_p]),
     "cbh_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "cbh_ctx_set_allocator": (ctypes.c_int, [ctypes.c_void_p, ALLOC_FN, FREE_FN, ctypes.c_void_p]),
     "cbh_ctx_set_phase_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
@@ -68,6 +69,9 @@ SIGNATURES = {
                                         ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]),
     "cbh_plan_finish": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
     "cbh_plan_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbh_plan_col_nnz": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "cbh_plan_spgemm_slots": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                                             ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_mat_wrap_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cbh_dcsc), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_mat_info": (ctypes.c_int, [ctypes.c_void_p, c_int64_p, c_int64_p, c_int64_p, c_int64_p, ctypes.POINTER(ctypes.c_int)]),
     "cbh_mat_device_arrays": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_void_p)] * 4),

@@ -64,6 +64,13 @@ class HipBackend:
         return MultiwayMerge(SR, blocks, m, n)
 
     @staticmethod
+    def plan(A: SpDCCols, B: SpDCCols):
+        """one symbolic pass of A*B for a phase loop: .col_nnz(), .multiply(SR, c0, c1), .close()"""
+        from .mtspgemm import SpGEMMPlan
+
+        return SpGEMMPlan(A, B)
+
+    @staticmethod
     def col_nnz(A: SpDCCols, B: SpDCCols):
         """exact nnz of A*B per nonzero column slot of B (device int64, length B.nzc)"""
         if A.nnz == 0 or B.nnz == 0:

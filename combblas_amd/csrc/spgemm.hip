@@ -56,6 +56,9 @@ struct cbh_ctx {
   std::multimap<size_t, void*> cache;
   std::unordered_map<void*, size_t> live;
   size_t cached_bytes = 0;
+  size_t cache_cap = size_t(64) << 30;  // CBH_CACHE_CAP_GB; above it the cache is released
+  bool poison = false;  // CBH_ALLOC_POISON=1: freed blocks are filled with 0xFF and never reused
+  std::vector<void*> quarantine;
   std::vector<hipEvent_t> evpool;
   size_t evused = 0;
   std::vector<Rec> recs;
@@ -110,7 +113,11 @@ static int fail(cbh_ctx* ctx, int code, const std::string& msg) {
 // (hipMallocAsync's default pool, used before, handed overlapping blocks to live allocations on
 // repeated phased products in processes where torch had not initialised HIP first.)
 // Sizes are rounded to 512 B (< 1 MiB) or 2 MiB; a cached block is reused for a request of at
-// least half its size. On OOM the cache is released (after a stream sync) and the request retried.
+// least half its size. On OOM the cache is released (after a stream sync) and the request retried;
+// it is also released when it grows past cache_cap, and on cbh_ctx_trim.
+// Debug mode CBH_ALLOC_POISON=1 (read at cbh_ctx_create): a freed block is overwritten with 0xFF
+// on the stream and quarantined until the context is destroyed, so a use after free reads NaN /
+// -1 row ids instead of a later allocation's data (tests/test_allocator_gpu.py).
 static size_t alloc_class(size_t bytes) {
   return bytes < (size_t(1) << 20) ? (bytes + 511) & ~size_t(511) : (bytes + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
 }
@@ -119,6 +126,8 @@ static void release_cache(cbh_ctx* ctx) {
   for (auto& kv : ctx->cache) (void)hipFree(kv.second);
   ctx->cache.clear();
   ctx->cached_bytes = 0;
+  for (void* q : ctx->quarantine) (void)hipFree(q);
+  ctx->quarantine.clear();
 }
 template <class T>
 static int dalloc(cbh_ctx* ctx, T** p, size_t count) {
@@ -163,9 +172,16 @@ static void dfree(cbh_ctx* ctx, void* p) {
   }
   auto it = ctx->live.find(p);
   if (it == ctx->live.end()) return;  // not ours (wrapped device arrays are never freed here)
+  if (ctx->poison) {
+    (void)hipMemsetAsync(p, 0xFF, it->second, ctx->stream);
+    ctx->quarantine.push_back(p);
+    ctx->live.erase(it);
+    return;
+  }
   ctx->cache.emplace(it->second, p);
   ctx->cached_bytes += it->second;
   ctx->live.erase(it);
+  if (ctx->cached_bytes > ctx->cache_cap) release_cache(ctx);
 }
 
 // RAII holder for scratch allocations of one call.
@@ -314,13 +330,21 @@ __global__ void nz_flag_kernel(const int64_t* __restrict__ nnz, int64_t n, int64
 
 __global__ void compact_cols_kernel(const int64_t* __restrict__ nnz, const int64_t* __restrict__ pos,
                                     const int64_t* __restrict__ Bjc, const int64_t* __restrict__ Ccp, int64_t n,
-                                    int64_t* __restrict__ jc, int64_t* __restrict__ cp) {
+                                    int64_t* __restrict__ jc, int64_t* __restrict__ cp, int64_t base = 0) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n && nnz[i] > 0) {
     jc[pos[i]] = Bjc[i];
-    cp[pos[i]] = Ccp[i];
+    cp[pos[i]] = Ccp[i] - base;
   }
-  if (i == n - 1) cp[pos[n]] = Ccp[n];
+  if (i == n - 1) cp[pos[n]] = Ccp[n] - base;
+}
+
+// CBH_KEEP_EMPTY_COLS form of a slot range: every slot kept, offsets rebased
+__global__ void keep_cols_kernel(const int64_t* __restrict__ Bjc, const int64_t* __restrict__ Ccp, int64_t n,
+                                 int64_t base, int64_t* __restrict__ jc, int64_t* __restrict__ cp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) jc[i] = Bjc[i];
+  if (i <= n) cp[i] = Ccp[i] - base;
 }
 
 __global__ void widen_i32_kernel(const int32_t* __restrict__ f, int64_t* __restrict__ o, int64_t k) {
@@ -1056,6 +1080,8 @@ int cbh_ctx_create(int device, cbh_ctx** out) {
     return CBH_E_HIP;
   }
   c->own_stream = true;
+  if (const char* v = std::getenv("CBH_ALLOC_POISON")) c->poison = std::atoi(v) != 0;
+  if (const char* v = std::getenv("CBH_CACHE_CAP_GB")) c->cache_cap = size_t(std::atof(v) * double(size_t(1) << 30));
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) {
       delete c;
@@ -1105,6 +1131,18 @@ void* cbh_ctx_stream(cbh_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->s
 int cbh_ctx_synchronize(cbh_ctx* ctx) {
   if (!ctx) return CBH_E_ARG;
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return CBH_OK;
+}
+
+int cbh_ctx_trim(cbh_ctx* ctx) {
+  if (!ctx) return CBH_E_ARG;
+  release_cache(ctx);
+  if (ctx->ws) {
+    (void)hipFree(ctx->ws);
+    ctx->ws = nullptr;
+    ctx->ws_bytes = 0;
+  }
+  CBH_HIP(ctx, hipGetLastError());
   return CBH_OK;
 }
 
@@ -1614,6 +1652,70 @@ int cbh_plan_finish(cbh_plan* p, cbh_mat* C, uint32_t flags) {
 int cbh_plan_destroy(cbh_plan* p) {
   delete p;
   return CBH_OK;
+}
+
+int cbh_plan_col_nnz(const cbh_plan* p, int64_t* col_nnz_dev) {
+  if (!p || !col_nnz_dev) return fail(p ? p->ctx : nullptr, CBH_E_ARG, "bad plan arguments");
+  cbh_ctx* ctx = p->ctx;
+  const int64_t n = p->B->nzc;
+  if (n == 0) return CBH_OK;
+  if (p->P.ntasks == 0) CBH_HIP(ctx, hipMemsetAsync(col_nnz_dev, 0, sizeof(int64_t) * n, ctx->stream));
+  else CBH_HIP(ctx, hipMemcpyAsync(col_nnz_dev, p->P.nnz, sizeof(int64_t) * n, hipMemcpyDeviceToDevice, ctx->stream));
+  return CBH_OK;
+}
+
+int cbh_plan_spgemm_slots(cbh_plan* p, cbh_semiring sr, int64_t s0, int64_t s1, uint32_t flags, cbh_mat** C) {
+  if (!p || !C) return fail(p ? p->ctx : nullptr, CBH_E_ARG, "bad plan arguments");
+  cbh_ctx* ctx = p->ctx;
+  const cbh_mat* A = p->A;
+  const cbh_mat* B = p->B;
+  *C = nullptr;
+  if (s0 < 0 || s1 < s0 || s1 > B->nzc) return fail(ctx, CBH_E_ARG, "slot range outside B's nonzero columns");
+  if (A->dtype != B->dtype) return fail(ctx, CBH_E_ARG, "A and B dtypes differ");
+  Plan& P = p->P;
+  if (P.ntasks == 0 || s1 == s0) return empty_result(ctx, A->m, B->n, A->dtype, C);
+  return dispatch_sr(ctx, sr, A->dtype, [&](auto srv) -> int {
+    using SR = decltype(srv);
+    Scratch S(ctx);
+    const int64_t n = s1 - s0;
+    int64_t h[4];
+    CBH_HIP(ctx, hipMemcpyAsync(&h[0], P.tstart + s0, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(&h[1], P.tstart + s1, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(&h[2], P.Ccp + s0, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(&h[3], P.Ccp + s1, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    const bool keep = (flags & CBH_KEEP_EMPTY_COLS) != 0;
+    int64_t nzcC = n;
+    int64_t* pos = nullptr;
+    if (!keep) {
+      int64_t* flag;
+      CBH_TRY(S.get(&flag, n + 1));
+      CBH_TRY(S.get(&pos, n + 1));
+      hipLaunchKernelGGL(nz_flag_kernel, dim3(blocks_for(n + 1, 256)), dim3(256), 0, ctx->stream, P.nnz + s0, n + 1,
+                         flag);
+      CBH_TRY(exclusive_scan_i64(ctx, S, flag, pos, n + 1));
+      CBH_HIP(ctx, hipMemcpyAsync(&nzcC, pos + n, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    }
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const int64_t nnz = h[3] - h[2];
+    cbh_mat* out;
+    CBH_TRY(new_mat(ctx, A->m, B->n, nnz, nzcC, A->dtype, &out));
+    int rc = run_numeric<SR>(ctx, S, A, B, P, h[0], h[1], h[2], out->ir, out->num, nullptr, nnz);
+    if (rc == CBH_OK) {
+      if (keep)
+        hipLaunchKernelGGL(keep_cols_kernel, dim3(blocks_for(n + 1, 256)), dim3(256), 0, ctx->stream, B->jc + s0,
+                           P.Ccp + s0, n, h[2], out->jc, out->cp);
+      else
+        hipLaunchKernelGGL(compact_cols_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, P.nnz + s0, pos,
+                           B->jc + s0, P.Ccp + s0, n, out->jc, out->cp, h[2]);
+      rc = check_err(ctx);
+    }
+    if (rc != CBH_OK) {
+      cbh_mat_free(ctx, out);
+      return rc;
+    }
+    *C = out;
+    return CBH_OK;
+  });
 }
 
 int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* parts, cbh_mat** C) {

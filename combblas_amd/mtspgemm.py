@@ -62,6 +62,63 @@ def estimateFLOPandNNZ(A: SpDCCols, B: SpDCCols, per_column=False):
     return (f.value, z.value, cf, cz) if per_column else (f.value, z.value)
 
 
+class SpGEMMPlan:
+    """The symbolic pass of C = A*B kept for a phase loop (cbh_plan_create): the exact nnz of every
+    nonzero column of B, and C = A * B(:, c0:c1) per phase without re-running the symbolic pass --
+    the phased drivers (MemEfficientSpGEMM, ParFriends.h:449-730, and its 3D form) multiply each
+    stage pair once per phase on a column slice of B. A and B must stay alive until close()."""
+
+    def __init__(self, A: SpDCCols, B: SpDCCols):
+        if A.ctx is not B.ctx:
+            raise ValueError("A and B live in different contexts")
+        self.ctx, self.A, self.B = A.ctx, A, B
+        h = ctypes.c_void_p()
+        check(lib().cbh_plan_create(A.ctx.h, A.h, B.h, ctypes.byref(h)), A.ctx.h)
+        self.h = h
+        self._jc = None
+
+    def col_nnz(self):
+        """exact nnz of A*B per nonzero column slot of B (device int64 tensor, length B.nzc)"""
+        import torch
+
+        out = torch.empty(self.B.nzc, dtype=torch.int64, device=self.ctx.tdevice)
+        check(lib().cbh_plan_col_nnz(self.h, ctypes.c_void_p(out.data_ptr())), self.ctx.h)
+        return out
+
+    def info(self):
+        f, z = ctypes.c_int64(), ctypes.c_int64()
+        check(lib().cbh_plan_info(self.h, ctypes.byref(f), ctypes.byref(z)), self.ctx.h)
+        return f.value, z.value
+
+    def multiply_slots(self, SR: Semiring, s0: int, s1: int, flags=0) -> SpDCCols:
+        h = ctypes.c_void_p()
+        check(lib().cbh_plan_spgemm_slots(self.h, SR.code, int(s0), int(s1), flags, ctypes.byref(h)), self.ctx.h)
+        return SpDCCols(self.ctx, h)
+
+    def multiply(self, SR: Semiring, c0: int, c1: int) -> SpDCCols:
+        """C = A * B(:, c0:c1) as an m x B.n block (columns of B in [c0, c1))"""
+        import torch
+
+        if self.B.nzc == 0:
+            return self.multiply_slots(SR, 0, 0)
+        if self._jc is None:
+            self._jc = self.B.tensors()[1]
+        s0, s1 = (int(x) for x in torch.searchsorted(
+            self._jc, torch.tensor([c0, c1], dtype=torch.int64, device=self._jc.device)).cpu())
+        return self.multiply_slots(SR, s0, s1)
+
+    def close(self):
+        if self.h:
+            lib().cbh_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
 def EstimateLocalFLOP(SR: Semiring, A: SpDCCols, B: SpDCCols, clearA=False, clearB=False) -> int:
     """mtSpGEMM.h:662-689"""
     return estimateFLOPandNNZ(A, B)[0]

@@ -152,7 +152,7 @@ def _stage_blocks(A, B, grid, stages):
     return Ab, Bb, vdtype
 
 
-def _phase_cuts(be, Ab, Bb, ncols, phases, budget_entries, groups=()):
+def _phase_cuts(be, plans, Bb, ncols, phases, budget_entries, groups=()):
     """Column ranges [c0, c1) of the local output block. With phases <= 0 they are planned from
     the exact per-column nnz of the stage partials, each phase's partials staying within
     budget_entries. The counts and the budget are reduced over every group in `groups` in turn
@@ -167,9 +167,9 @@ def _phase_cuts(be, Ab, Bb, ncols, phases, budget_entries, groups=()):
         allreduce_(t, g, torch.distributed.ReduceOp.MIN)
     budget_entries = int(t.item())
     col = torch.zeros(ncols + 1, dtype=torch.int64, device=be.device)
-    for a, b in zip(Ab, Bb):
+    for p, b in zip(plans, Bb):
         if be.dims(b)[3]:
-            col.index_add_(0, be.arrays(b)[1], be.col_nnz(a, b))
+            col.index_add_(0, be.arrays(b)[1], p.col_nnz())
     for g in groups:
         allreduce_(col, g)
     cum = np.concatenate([[0], np.cumsum(col[:ncols].cpu().numpy())])
@@ -317,11 +317,12 @@ def MemEfficientSpGEMM(SR, A: SpParMat, B: SpParMat, phases=0, hardThreshold=Non
     be = A.backend
     Ab, Bb, vdtype = _stage_blocks(A, B, grid, stages)
     m, n = be.dims(A.seq)[0], be.dims(B.seq)[1]
-    cuts = _phase_cuts(be, Ab, Bb, n, phases, _budget_entries(be, vdtype, perProcessMemory, 2),
+    plans = [be.plan(a, b) for a, b in zip(Ab, Bb)]  # the one symbolic pass per stage pair
+    cuts = _phase_cuts(be, plans, Bb, n, phases, _budget_entries(be, vdtype, perProcessMemory, 2),
                        groups=(grid.colWorld,))
     out = []
     for c0, c1 in cuts:
-        parts = [be.multiply(SR, a, _colslice(be, b, c0, c1)) for a, b in zip(Ab, Bb)]
+        parts = [p.multiply(SR, c0, c1) for p in plans]
         C = _merge(be, SR, parts, m, n, vdtype)
         if hardThreshold is not None:
             C = _mcl_block(be, C, grid.colWorld, hardThreshold, selectNum, recoverNum, recoverPct)
@@ -329,6 +330,8 @@ def MemEfficientSpGEMM(SR, A: SpParMat, B: SpParMat, phases=0, hardThreshold=Non
             on_phase(C, c0, c1)
         else:
             out.append(C)
+    for p in plans:
+        p.close()
     if on_phase is not None:
         return len(cuts)
     return SpParMat(_concat_cols(be, out, m, n, vdtype), grid, be, A.m, B.n, A.row_off, B.col_off)
@@ -390,12 +393,13 @@ def Mult_AnXBn_SUMMA3D(SR, A: SpParMat3D, B: SpParMat3D, phases=1, perProcessMem
     be = A.backend
     Ab, Bb, vdtype = _stage_blocks(A, B, grid, stages)
     m, n = be.dims(A.seq)[0], be.dims(B.seq)[1]
-    cuts = _phase_cuts(be, Ab, Bb, n, phases, _budget_entries(be, vdtype, perProcessMemory, 3),
+    plans = [be.plan(a, b) for a, b in zip(Ab, Bb)]  # the one symbolic pass per stage pair
+    cuts = _phase_cuts(be, plans, Bb, n, phases, _budget_entries(be, vdtype, perProcessMemory, 3),
                        groups=(g3.fiberWorld, grid.colWorld))
     div = _divisions3d(n, g3.gridLayers)
     out, mine0 = [], 0
     for c0, c1 in cuts:
-        parts = [be.multiply(SR, a, _colslice(be, b, c0, c1)) for a, b in zip(Ab, Bb)]
+        parts = [p.multiply(SR, c0, c1) for p in plans]
         P = _merge(be, SR, parts, m, n, vdtype)
         C, mine0 = _fiber_reduce_scatter(be, SR, P, g3, m, n, vdtype)
         w = div[g3.rankInFiber]
@@ -404,6 +408,8 @@ def Mult_AnXBn_SUMMA3D(SR, A: SpParMat3D, B: SpParMat3D, phases=1, perProcessMem
             on_phase(C, p0, p1)
         else:
             out.append(C)
+    for p in plans:
+        p.close()
     if on_phase is not None:
         return len(cuts)
     w = div[g3.rankInFiber]

@@ -113,6 +113,10 @@ class Context:
     def synchronize(self):
         check(lib().cbh_ctx_synchronize(self.h), self.h)
 
+    def trim(self):
+        """return the built-in allocator's cached blocks and the phase workspace to HIP"""
+        check(lib().cbh_ctx_trim(self.h), self.h)
+
     def enable_timing(self, on=True):
         check(lib().cbh_ctx_enable_timing(self.h, int(on)), self.h)
 

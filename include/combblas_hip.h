@@ -90,9 +90,12 @@ int cbh_ctx_destroy(cbh_ctx* ctx);
 int cbh_ctx_set_stream(cbh_ctx* ctx, void* hip_stream);
 void* cbh_ctx_stream(cbh_ctx* ctx);
 int cbh_ctx_synchronize(cbh_ctx* ctx);
+/* Synchronize and return the context's cached device blocks and phase workspace to HIP (the
+ * default allocator keeps freed blocks for reuse in stream order).                            */
+int cbh_ctx_trim(cbh_ctx* ctx);
 const char* cbh_last_error(cbh_ctx* ctx);
 /* Route every device allocation of this context through caller callbacks (e.g. the torch
- * caching allocator), stream-ordered on `stream`. NULL alloc restores hipMallocAsync.        */
+ * caching allocator), stream-ordered on `stream`. NULL alloc restores the built-in block cache.        */
 typedef void* (*cbh_alloc_fn)(void* user, int64_t bytes, void* stream);
 typedef void (*cbh_free_fn)(void* user, void* ptr, void* stream);
 int cbh_ctx_set_allocator(cbh_ctx* ctx, cbh_alloc_fn alloc, cbh_free_fn release, void* user);
@@ -213,6 +216,12 @@ int cbh_plan_numeric(cbh_plan* plan, cbh_dtype dtype, int64_t value_bytes, uint3
  * and the device-side consistency checks. */
 int cbh_plan_finish(cbh_plan* plan, cbh_mat* C, uint32_t flags);
 int cbh_plan_destroy(cbh_plan* plan);
+/* Phase loops over one planned product (MemEfficientSpGEMM, ParFriends.h:449-730: per phase a
+ * LocalSpGEMM of A with a column slice of B) without a second symbolic pass: the exact nnz of
+ * every nonzero column slot of B (device int64[B.nzc]), and C = A * B(:, slots [s0, s1)) for a
+ * built-in semiring -- the same m x B.n matrix cbh_spgemm returns for that column slice.      */
+int cbh_plan_col_nnz(const cbh_plan* plan, int64_t* col_nnz_dev);
+int cbh_plan_spgemm_slots(cbh_plan* plan, cbh_semiring sr, int64_t s0, int64_t s1, uint32_t flags, cbh_mat** C);
 
 /* ---------------------------------------------------------------- callers around the hot path
  * (device kernels in combblas_amd/csrc/apps.h)                           */

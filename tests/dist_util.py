@@ -91,6 +91,23 @@ class OracleBackend:
     def merge(self, SR, blocks, m, n):
         return self._from_dcsc(self.o.merge([b.dcsc() for b in blocks], ORACLE_SR[SR.name]))
 
+    def plan(self, A, B):
+        be = self
+
+        class _Plan:  # the phase-loop protocol of HipBackend.plan, on the oracle
+            def col_nnz(self):
+                return be.col_nnz(A, B)
+
+            def multiply(self, SR, c0, c1):
+                from combblas_amd.parfriends import _colslice
+
+                return be.multiply(SR, A, _colslice(be, B, c0, c1))
+
+            def close(self):
+                pass
+
+        return _Plan()
+
     def col_nnz(self, A, B):
         if A.ir.numel() == 0 or B.ir.numel() == 0:
             return torch.zeros(B.jc.numel(), dtype=torch.int64)

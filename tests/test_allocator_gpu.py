@@ -1,0 +1,98 @@
+"""Allocator invariants behind the phased driver.
+
+Every library allocation and free is ordered on the context's one stream. These tests run
+back-to-back phased products (many phases, so scratch blocks are recycled between phases and
+products) and require identical digests:
+  * CBH_ALLOC_POISON=1 with the built-in block cache: freed blocks are overwritten with 0xFF and
+    never reused, so a use after free would change the digest;
+  * the torch caching allocator on an explicit side stream while unrelated torch work allocates
+    and frees on the default stream;
+  * cbh_ctx_trim between products.
+"""
+import numpy as np
+import pytest
+
+import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+
+def _gen(scale):
+    import combblas_amd as cb
+
+    A = cb.rmat(scale)
+    return H.Dcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num)
+
+
+def _products(ctx, A, budgets, between=None):
+    import combblas_amd as cb
+
+    out = []
+    h = cb.HostDcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num)
+    for b in budgets:
+        dA = cb.SpDCCols.from_host(ctx, h)
+        dB = cb.SpDCCols.from_host(ctx, h)
+        st = cb.PhasedSpGEMM(cb.PlusTimesSRing, dA, dB, checksum=True, budget_bytes=b)
+        out.append((st["nnz"], st["value_sum"], st["digest"]))
+        dA.free()
+        dB.free()
+        if between:
+            between()
+    return out
+
+
+@pytest.fixture(scope="module")
+def expected(oracle):
+    A = _gen(12)
+    return A, H.digest(oracle.spgemm(A, A, "plus_times", threads=4))
+
+
+def test_poisoned_frees_keep_phased_digests(monkeypatch, expected):
+    import combblas_amd as cb
+
+    A, (vs, dg) = expected
+    monkeypatch.setenv("CBH_ALLOC_POISON", "1")
+    ctx = cb.Context(0, torch_allocator=False)
+    try:
+        res = _products(ctx, A, [64 * 1024, 1 << 20, 64 * 1024, 0])
+    finally:
+        ctx.close()
+    for nnz, v, d in res:
+        assert v == vs and d == dg, res
+
+
+def test_torch_allocator_side_stream_back_to_back(expected):
+    import torch
+    import combblas_amd as cb
+
+    A, (vs, dg) = expected
+    side = torch.cuda.Stream()
+    ctx = cb.Context(0, torch_allocator=True, stream=side)
+    noise = []
+
+    def churn():  # unrelated allocations on the default stream reuse torch's freed blocks
+        with torch.cuda.stream(torch.cuda.default_stream()):
+            t = torch.full((1 << 24,), -1, dtype=torch.int64, device="cuda")
+            noise.append(int(t.sum().item()))
+            del t
+
+    try:
+        res = _products(ctx, A, [64 * 1024, 1 << 20, 64 * 1024], between=churn)
+    finally:
+        ctx.close()
+    for nnz, v, d in res:
+        assert v == vs and d == dg, res
+    assert noise == [-(1 << 24)] * 3
+
+
+def test_trim_between_products(expected):
+    import combblas_amd as cb
+
+    A, (vs, dg) = expected
+    ctx = cb.Context(0, torch_allocator=False)
+    try:
+        res = _products(ctx, A, [1 << 20, 0], between=ctx.trim)
+    finally:
+        ctx.close()
+    for nnz, v, d in res:
+        assert v == vs and d == dg, res

@@ -231,3 +231,34 @@ def test_torch_tensors_view_results(ctx, fixtures):
     np.testing.assert_array_equal(ir.cpu().numpy(), exp.ir)
     C2 = cb.SpDCCols.from_tensors(ctx, C.m, C.n, cp.clone(), jc.clone(), ir.clone(), num.clone())
     H.assert_dcsc_equal(host(C2), exp)
+
+
+def test_plan_phase_slices_match_column_products(ctx):
+    """SpGEMMPlan (cbh_plan_col_nnz / cbh_plan_spgemm_slots): one symbolic pass, then C = A*B(:, c0:c1)
+    per phase equals cbh_spgemm on the column slice, with and without CBH_KEEP_EMPTY_COLS, and the
+    per-slot nnz equals the symbolic pass's."""
+    import combblas_amd as cb
+    from combblas_amd._lib import CBH_KEEP_EMPTY_COLS
+    from combblas_amd.backend import HipBackend
+    from combblas_amd.parfriends import _colslice
+
+    A = H.values_for("pt_i64", _gen(11))
+    dA, dB = dev(ctx, A), dev(ctx, A)
+    be = HipBackend(ctx)
+    plan = cb.SpGEMMPlan(dA, dB)
+    try:
+        ref_nnz = cb.estimateFLOPandNNZ(dA, dB, per_column=True)[3]
+        assert bool((plan.col_nnz() == ref_nnz).all().item())
+        n = A.n
+        cuts = [0, 1, 700, 701, 1500, n // 2, n]
+        for c0, c1 in zip(cuts[:-1], cuts[1:]):
+            got = plan.multiply(cb.PlusTimesSRing, c0, c1)
+            exp = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dA, _colslice(be, dB, c0, c1))
+            H.assert_dcsc_equal(host(got), host(exp), msg=f"cols [{c0},{c1})")
+        s1 = dB.nzc // 3
+        keep = plan.multiply_slots(cb.PlusTimesSRing, 0, s1, flags=CBH_KEEP_EMPTY_COLS)
+        assert keep.nzc == s1
+        empty = plan.multiply_slots(cb.PlusTimesSRing, 5, 5)
+        assert empty.nnz == 0
+    finally:
+        plan.close()
