@@ -169,7 +169,6 @@ def merge_measurement(A, frac, steps):
     wall = (time.perf_counter() - t0) / steps
     ctx.enable_timing(False)
     ks = ctx.kernel_stats()
-    log(f"{args.steps} timed step(s): {(t1 - t0) / max(args.steps, 1) * 1e3:.1f} ms/step")
     M = cb.MultiwayMerge(cb.PlusTimesSRing, P, A.m, A.n)
     full = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, cb.SpDCCols.from_host(ctx, A), cb.SpDCCols.from_host(ctx, B))
     ok = M.nnz == full.nnz and bool((M.tensors()[2] == full.tensors()[2]).all().item()) and \

@@ -250,7 +250,7 @@ def test_plan_phase_slices_match_column_products(ctx):
         ref_nnz = cb.estimateFLOPandNNZ(dA, dB, per_column=True)[3]
         assert bool((plan.col_nnz() == ref_nnz).all().item())
         n = A.n
-        cuts = [0, 1, 700, 701, 1500, n // 2, n]
+        cuts = [0, 1, 700, 701, n // 2, n // 2 + 333, n]
         for c0, c1 in zip(cuts[:-1], cuts[1:]):
             got = plan.multiply(cb.PlusTimesSRing, c0, c1)
             exp = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dA, _colslice(be, dB, c0, c1))

@@ -34,6 +34,7 @@ python3 "$R/tools/pmc_calib.py" "$OUT/calib" "$OUT/pmc_calib.json" || exit 1
 step phase timing
 timeout -k 10 300 python3 -u "$R/tools/phase_timing.py" 22 2 > "$OUT/ks.log" 2>&1 || { tail -20 "$OUT/ks.log"; exit 1; }
 tail -3 "$OUT/ks.log"
+mkdir -p "$OUT/bins"
 i=0
 for PMC in "FETCH_SIZE TCC_HIT_sum" "WRITE_SIZE TCC_MISS_sum GRBM_GUI_ACTIVE" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_BUSY_CYCLES"; do

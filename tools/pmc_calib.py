@@ -25,7 +25,8 @@ def main(src, dst):
     # pmc_calib launches 2 dispatches per kernel (warm-up, timed) in CALIB-line order
     rows = []
     for f in sorted(glob.glob(src + "/pmc*/**/*counter_collection.csv", recursive=True)):
-        rows += [r for r in csv.DictReader(open(f)) if r["Counter_Name"] == "FETCH_SIZE"]
+        rows += [r for r in csv.DictReader(open(f))
+                 if r["Counter_Name"] == "FETCH_SIZE" and not r["Kernel_Name"].startswith("__amd")]  # hipMemset fill
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     names = list(known)
     fetch = collections.defaultdict(list)
