@@ -318,6 +318,25 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(const int64_t* __restr
   if (b > 0) cols[base[b] + r] = (int32_t)(c + col0);
 }
 
+// launch order inside a bin by row block (rowkey): keys = bin * 256 + rowkey, bin 0 last
+__global__ void bin_key_kernel(const int64_t* __restrict__ work, int64_t n, int64_t col0, BinCaps caps,
+                               const int32_t* __restrict__ rowkey, uint32_t* __restrict__ keys,
+                               int32_t* __restrict__ vals) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const int b = bin_of(work[c], caps);
+  keys[c] = b == 0 ? 0xFFFFFFFFu : (uint32_t)b * 256u + (uint32_t)(rowkey[c] & 255);
+  vals[c] = (int32_t)(c + col0);
+}
+
+// per task: the row block of its middle row (tasks of one row block read the same lines of the
+// hub columns of A)
+__global__ void task_rowkey_kernel(const int32_t* __restrict__ tlo, const int32_t* __restrict__ thi, int64_t n,
+                                   int32_t RB, int32_t* __restrict__ key) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) key[t] = (int32_t)(((int64_t)tlo[t] + thi[t]) / 2 / RB);
+}
+
 __global__ void fill_i64_kernel(int64_t* p, int64_t n, int64_t v) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
@@ -468,8 +487,17 @@ struct BinLists {
 };
 // Unit sums are gathered only when the context records timings (bench/roofline); `units` is
 // indexed like `work`.
+// CBH_ROWORDER=1: inside each bin, tasks launch in row-block order (rowkey), so the tasks in
+// flight at a time read one slice of A (A/B switch while measuring).
+static bool row_order_enabled() {
+  static int v = [] {
+    const char* e = std::getenv("CBH_ROWORDER");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v != 0;
+}
 static int make_bins(cbh_ctx* ctx, Scratch& S, const int64_t* work, int64_t n, int64_t col0, int32_t* ids,
-                     BinLists* out, BinCaps caps, const int64_t* units = nullptr) {
+                     BinLists* out, BinCaps caps, const int64_t* units = nullptr, const int32_t* rowkey = nullptr) {
   constexpr int NS = kGroups;
   unsigned long long* counts;
   CBH_TRY(S.get(&counts, 2 * kNB + NS));
@@ -489,11 +517,35 @@ static int make_bins(cbh_ctx* ctx, Scratch& S, const int64_t* work, int64_t n, i
     off[b] = run;
     run += h[b];
   }
-  unsigned long long* cursor = counts + kNB;
-  CBH_HIP(ctx, hipMemcpyAsync(cursor, off, sizeof(off), hipMemcpyHostToDevice, ctx->stream));
-  hipLaunchKernelGGL(bin_scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, work, n, col0,
-                     caps, cursor, ids);
-  CBH_HIP(ctx, hipGetLastError());
+  if (rowkey && row_order_enabled() && n > 0) {
+    uint32_t *kin, *kout;
+    int32_t* vin;
+    CBH_TRY(S.get(&kin, n));
+    CBH_TRY(S.get(&kout, n));
+    CBH_TRY(S.get(&vin, n));
+    hipLaunchKernelGGL(bin_key_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, work, n, col0, caps,
+                       rowkey, kin, vin);
+    CBH_HIP(ctx, hipGetLastError());
+    int32_t* vout = ids;  // the first `run` sorted items are the binned ones, in bin order
+    int32_t* vtmp = nullptr;
+    if ((int64_t)run < n) {  // ids holds only `run` slots: sort into scratch, copy the prefix
+      CBH_TRY(S.get(&vtmp, n));
+      vout = vtmp;
+    }
+    size_t tmp = 0;
+    CBH_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kin, kout, vin, vout, (int)n, 0, 16, ctx->stream));
+    void* tbuf;
+    CBH_TRY(S.get(reinterpret_cast<char**>(&tbuf), tmp));
+    CBH_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(tbuf, tmp, kin, kout, vin, vout, (int)n, 0, 16, ctx->stream));
+    if (vtmp && run > 0)
+      CBH_HIP(ctx, hipMemcpyAsync(ids, vtmp, sizeof(int32_t) * run, hipMemcpyDeviceToDevice, ctx->stream));
+  } else {
+    unsigned long long* cursor = counts + kNB;
+    CBH_HIP(ctx, hipMemcpyAsync(cursor, off, sizeof(off), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(bin_scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, work, n, col0,
+                       caps, cursor, ids);
+    CBH_HIP(ctx, hipGetLastError());
+  }
   // the host copy of `off` must outlive the async H2D copy
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (sums)
@@ -790,6 +842,9 @@ struct Plan {  // device arrays describing C = A*B (B's nonzero column slots, ta
   int64_t* gcur0 = nullptr;
   int64_t* gcur1 = nullptr;
   int64_t* gend = nullptr;
+  int32_t* trk = nullptr;     // per task: row block of its middle row (launch order key)
+  int32_t* gnx0 = nullptr;    // row at each committed cursor (double-buffered like gcur)
+  int32_t* gnx1 = nullptr;
   int64_t total_flops = 0, total_nnz = 0;
 };
 
@@ -820,6 +875,8 @@ static TaskArgs task_args(const cbh_mat* A, const cbh_mat* B, const Plan& P, cbh
   a.gcur0 = P.gcur0;
   a.gcur1 = P.gcur1;
   a.gend = P.gend;
+  a.gnx0 = P.gnx0;
+  a.gnx1 = P.gnx1;
   return a;
 }
 
@@ -865,9 +922,12 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   CBH_TRY(S.get(&P.tcnt, nt + 1));
   CBH_TRY(S.get(&P.toff, nt + 1));
   CBH_TRY(S.get(&P.order, nt));
+  CBH_TRY(S.get(&P.trk, nt));
   hipLaunchKernelGGL(task_fill_kernel, dim3(blocks_for(n, 4)), dim3(256), 0, ctx->stream, P.tstart, P.flop, P.rmin,
                      P.rmax, B->cp, n, P.RB, P.tcol, P.tlo, P.thi, P.tfull, P.twork, P.tunits);
   CBH_HIP(ctx, hipGetLastError());
+  hipLaunchKernelGGL(task_rowkey_kernel, dim3(blocks_for(P.ntasks, 256)), dim3(256), 0, ctx->stream, P.tlo, P.thi,
+                     P.ntasks, P.RB, P.trk);
   {  // row-block table of A's hub columns: task boundaries and long-segment stops
     int64_t *hflag, *hpos;
     CBH_TRY(S.get(&hflag, A->n + 1));
@@ -906,13 +966,15 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
       CBH_TRY(S.get(&P.gcur0, (size_t)gtot));
       CBH_TRY(S.get(&P.gcur1, (size_t)gtot));
       CBH_TRY(S.get(&P.gend, (size_t)gtot));
+      CBH_TRY(S.get(&P.gnx0, (size_t)gtot));
+      CBH_TRY(S.get(&P.gnx1, (size_t)gtot));
     } else {
       P.goff = nullptr;
     }
   }
   CBH_HIP(ctx, hipMemsetAsync(P.tcnt, 0, sizeof(int64_t) * (nt + 1), ctx->stream));
   BinLists bl;
-  CBH_TRY(make_bins(ctx, S, P.twork, P.ntasks, 0, P.order, &bl, BinCaps{kSmallCap, kSmallCap}, P.tunits));
+  CBH_TRY(make_bins(ctx, S, P.twork, P.ntasks, 0, P.order, &bl, BinCaps{kSmallCap, kSmallCap}, P.tunits, P.trk));
   TaskArgs a = task_args(A, B, P, ctx);
   a.twork = P.twork;
   a.cnt = P.tcnt;
@@ -957,9 +1019,9 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
                      kDenseEnabled() ? 1 : 0, wd, wh);
   CBH_HIP(ctx, hipGetLastError());
   BinLists bd, bl;
-  CBH_TRY(make_bins(ctx, S, wd, nt, t0, P.order, &bd, BinCaps{kSmallCap, kSmallCap}, P.tunits + t0));
+  CBH_TRY(make_bins(ctx, S, wd, nt, t0, P.order, &bd, BinCaps{kSmallCap, kSmallCap}, P.tunits + t0, P.trk + t0));
   const int64_t nd = bd.small_count + bd.mid_count + bd.large_count;
-  CBH_TRY(make_bins(ctx, S, wh, nt, t0, P.order + nd, &bl, BinCaps{kSmallCap, kSmallCap}, P.tunits + t0));
+  CBH_TRY(make_bins(ctx, S, wh, nt, t0, P.order + nd, &bl, BinCaps{kSmallCap, kSmallCap}, P.tunits + t0, P.trk + t0));
   bl.small_first += nd;
   bl.mid_first += nd;
   bl.large_first += nd;
@@ -1593,9 +1655,9 @@ int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t
                      (kDenseEnabled() && !(flags & CBH_PLAN_NO_DENSE)) ? 1 : 0, wd, wh);
   CBH_HIP(ctx, hipGetLastError());
   BinLists bd, bl;
-  CBH_TRY(make_bins(ctx, p->S, wd, nt, 0, P.order, &bd, BinCaps{kSmallCap, kSmallCap}));
+  CBH_TRY(make_bins(ctx, p->S, wd, nt, 0, P.order, &bd, BinCaps{kSmallCap, kSmallCap}, nullptr, P.trk));
   const int64_t nd = bd.small_count + bd.mid_count + bd.large_count;
-  CBH_TRY(make_bins(ctx, p->S, wh, nt, 0, P.order + nd, &bl, BinCaps{kSmallCap, kSmallCap}));
+  CBH_TRY(make_bins(ctx, p->S, wh, nt, 0, P.order + nd, &bl, BinCaps{kSmallCap, kSmallCap}, nullptr, P.trk));
   const cbh_mat* A = p->A;
   const cbh_mat* B = p->B;
   out->Acp = P.Adense;
@@ -1618,6 +1680,8 @@ int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t
   out->gcur0 = P.gcur0;
   out->gcur1 = P.gcur1;
   out->gend = P.gend;
+  out->gnx0 = P.gnx0;
+  out->gnx1 = P.gnx1;
   out->err = ctx->d_err;
   out->nnzA = A->nnz;
   out->ncolA = A->n;

@@ -135,6 +135,65 @@ def _rowrange(be, blk, r0, r1):
     return be.wrap(m, n, cpn, jc[nz].contiguous(), ir[keep].contiguous(), num[keep].contiguous())
 
 
+def _hcat(be, blocks, m, vdtype):
+    """[A_0 A_1 ...]: column concatenation of m x k_i blocks (column ids shifted by sum k_<i)"""
+    dims = [be.dims(b) for b in blocks]
+    kout = int(sum(d[1] for d in dims))
+    live = [(b, off) for b, off, d in zip(blocks, np.cumsum([0] + [d[1] for d in dims])[:-1], dims) if d[3] > 0]
+    if not live:
+        return _empty(be, m, kout, vdtype)
+    arrs = [be.arrays(b) for b, _ in live]
+    cps, base = [], 0
+    for i, (cp, jc, ir, num) in enumerate(arrs):
+        cps.append((cp[:-1] if i + 1 < len(arrs) else cp) - cp[0] + base)
+        base += int(ir.numel())
+    return be.wrap(m, kout, torch.cat(cps), torch.cat([a[1] + int(off) for a, (_, off) in zip(arrs, live)]),
+                   torch.cat([a[2] for a in arrs]), torch.cat([a[3] for a in arrs]))
+
+
+def _vcat(be, blocks, n, vdtype):
+    """[B_0; B_1; ...]: row concatenation of k_i x n blocks (row ids shifted by sum k_<i). A stable
+    sort by column keeps every column's rows ascending (block i's rows all precede block i+1's)."""
+    dims = [be.dims(b) for b in blocks]
+    kout = int(sum(d[0] for d in dims))
+    offs = np.cumsum([0] + [d[0] for d in dims])[:-1]
+    cols, rows, vals = [], [], []
+    for b, off, d in zip(blocks, offs, dims):
+        if d[2] == 0:
+            continue
+        cp, jc, ir, num = be.arrays(b)
+        cols.append(torch.repeat_interleave(jc, cp[1:] - cp[:-1]))
+        rows.append(ir + int(off))
+        vals.append(num)
+    if not cols:
+        return _empty(be, kout, n, vdtype)
+    col = torch.cat(cols)
+    key, perm = torch.sort(col, stable=True)
+    jc, cnt = torch.unique_consecutive(key, return_counts=True)
+    cp = torch.zeros(jc.numel() + 1, dtype=torch.int64, device=col.device)
+    torch.cumsum(cnt, 0, out=cp[1:])
+    return be.wrap(kout, n, cp, jc.contiguous(), torch.cat(rows)[perm].contiguous(), torch.cat(vals)[perm].contiguous())
+
+
+def _stage_product_operands(be, A, B, grid, stages, Ab, Bb, vdtype):
+    """The strips A(r, :) = [A_0 ... A_{s-1}] and B(:, c) = [B_0; ...; B_{s-1}] of this rank's C
+    block. sum_i A_i B_i (the stage partials the reference merges, ParFriends.h:1064-1104) is then
+    ONE local product over the inner dimension of all stages: the kernels accumulate every k, so
+    no partial is materialised and no MultiwayMerge pass runs; C is the same matrix (integer and
+    boolean semirings bit for bit; floating-point sums in another order). The received stage
+    blocks are released once copied."""
+    m, n = be.dims(A.seq)[0], be.dims(B.seq)[1]
+    Acat = _hcat(be, Ab, m, vdtype)
+    Bcat = _vcat(be, Bb, n, vdtype)
+    Aself, Bself = grid.GetRankInProcRow(), grid.GetRankInProcCol()
+    for i in range(stages):
+        if i != Aself and Ab[i] is not Acat:
+            be.free(Ab[i])
+        if i != Bself and Bb[i] is not Bcat:
+            be.free(Bb[i])
+    return Acat, Bcat
+
+
 def _check_dims(A, B):
     if A.getncol() != B.getnrow():
         raise CombBLASHipError(DIMMISMATCH, f"Can not multiply, dimensions does not match {A.getncol()} != {B.getnrow()}")
@@ -317,13 +376,13 @@ def MemEfficientSpGEMM(SR, A: SpParMat, B: SpParMat, phases=0, hardThreshold=Non
     be = A.backend
     Ab, Bb, vdtype = _stage_blocks(A, B, grid, stages)
     m, n = be.dims(A.seq)[0], be.dims(B.seq)[1]
-    plans = [be.plan(a, b) for a, b in zip(Ab, Bb)]  # the one symbolic pass per stage pair
-    cuts = _phase_cuts(be, plans, Bb, n, phases, _budget_entries(be, vdtype, perProcessMemory, 2),
+    Acat, Bcat = _stage_product_operands(be, A, B, grid, stages, Ab, Bb, vdtype)
+    plans = [be.plan(Acat, Bcat)]  # one symbolic pass for every phase
+    cuts = _phase_cuts(be, plans, [Bcat], n, phases, _budget_entries(be, vdtype, perProcessMemory, 1),
                        groups=(grid.colWorld,))
     out = []
     for c0, c1 in cuts:
-        parts = [p.multiply(SR, c0, c1) for p in plans]
-        C = _merge(be, SR, parts, m, n, vdtype)
+        C = plans[0].multiply(SR, c0, c1)
         if hardThreshold is not None:
             C = _mcl_block(be, C, grid.colWorld, hardThreshold, selectNum, recoverNum, recoverPct)
         if on_phase is not None:
@@ -332,6 +391,8 @@ def MemEfficientSpGEMM(SR, A: SpParMat, B: SpParMat, phases=0, hardThreshold=Non
             out.append(C)
     for p in plans:
         p.close()
+    be.free(Acat)
+    be.free(Bcat)
     if on_phase is not None:
         return len(cuts)
     return SpParMat(_concat_cols(be, out, m, n, vdtype), grid, be, A.m, B.n, A.row_off, B.col_off)
@@ -393,14 +454,14 @@ def Mult_AnXBn_SUMMA3D(SR, A: SpParMat3D, B: SpParMat3D, phases=1, perProcessMem
     be = A.backend
     Ab, Bb, vdtype = _stage_blocks(A, B, grid, stages)
     m, n = be.dims(A.seq)[0], be.dims(B.seq)[1]
-    plans = [be.plan(a, b) for a, b in zip(Ab, Bb)]  # the one symbolic pass per stage pair
-    cuts = _phase_cuts(be, plans, Bb, n, phases, _budget_entries(be, vdtype, perProcessMemory, 3),
+    Acat, Bcat = _stage_product_operands(be, A, B, grid, stages, Ab, Bb, vdtype)
+    plans = [be.plan(Acat, Bcat)]  # one symbolic pass for every phase
+    cuts = _phase_cuts(be, plans, [Bcat], n, phases, _budget_entries(be, vdtype, perProcessMemory, 2),
                        groups=(g3.fiberWorld, grid.colWorld))
     div = _divisions3d(n, g3.gridLayers)
     out, mine0 = [], 0
     for c0, c1 in cuts:
-        parts = [p.multiply(SR, c0, c1) for p in plans]
-        P = _merge(be, SR, parts, m, n, vdtype)
+        P = plans[0].multiply(SR, c0, c1)
         C, mine0 = _fiber_reduce_scatter(be, SR, P, g3, m, n, vdtype)
         w = div[g3.rankInFiber]
         p0, p1 = min(max(c0 - mine0, 0), w), min(max(c1 - mine0, 0), w)
@@ -410,6 +471,8 @@ def Mult_AnXBn_SUMMA3D(SR, A: SpParMat3D, B: SpParMat3D, phases=1, perProcessMem
             out.append(C)
     for p in plans:
         p.close()
+    be.free(Acat)
+    be.free(Bcat)
     if on_phase is not None:
         return len(cuts)
     w = div[g3.rankInFiber]

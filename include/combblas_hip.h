@@ -198,6 +198,7 @@ typedef struct cbh_numeric_plan {
   const int32_t* tcol; const int32_t* tlo; const int32_t* thi; const uint8_t* tfull; /* tasks    */
   const int64_t* tcnt; const int64_t* toff;                  /* outputs per task, output offsets  */
   const int64_t* goff; int64_t* gcur0; int64_t* gcur1; int64_t* gend; /* chunked-task cursors    */
+  int32_t* gnx0; int32_t* gnx1;                              /* rows at those cursors             */
   int* err;                                                  /* device consistency flags          */
   int64_t nnzA, ncolA, ntasks;
   const int32_t* order;                                      /* task ids in launch order          */

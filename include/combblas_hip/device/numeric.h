@@ -97,6 +97,8 @@ inline TaskArgs numeric_args(const cbh_numeric_plan& p, int64_t cbase, int32_t* 
   a.gcur0 = p.gcur0;
   a.gcur1 = p.gcur1;
   a.gend = p.gend;
+  a.gnx0 = p.gnx0;
+  a.gnx1 = p.gnx1;
   return a;
 }
 

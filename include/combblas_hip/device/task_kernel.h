@@ -36,7 +36,6 @@ namespace cbh {
 enum : int { MODE_TSYM = 0, MODE_TNUM = 1, MODE_TDENSE = 2 };
 constexpr int32_t kNoRow = 0x7fffffff;
 constexpr int kFill8 = 4;  // numeric sub-tile: planned outputs, in eighths of the T home slots
-constexpr int kWin = 8;    // numeric commit: neighbour slots read on either side of an occupied slot
 // dense sub-tiles of one window keep their products in registers between the bitmap and the value
 // pass (else the value pass gathers them again)
 #ifndef CBH_DENSE_CARRY
@@ -98,6 +97,11 @@ struct TaskArgs {
   int64_t* gcur0;
   int64_t* gcur1;
   int64_t* gend;
+  // the row at each committed cursor (kNoRow: done), same double buffering: a later sub-tile
+  // knows which entries are idle without gathering A, and loads the rest of an entry's state
+  // only when it is active
+  int32_t* gnx0;
+  int32_t* gnx1;
   // merge mode (MultiwayMerge of k partial lists): entry l of output column slot c is list l's
   // segment [mstart[c*nl+l], +mlen[c*nl+l]) of lir[l] / lnum[l]; no multiply
   const int64_t* mstart;
@@ -385,7 +389,7 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
   // entry state of entries [first, first+cnt): cursor at the first row >= lo
   const int64_t go = chunked ? a.goff[task] : 0;
   int par = 0;  // which HBM cursor buffer holds the committed cursors
-  auto load_entries = [&](int64_t first, int cnt, int32_t lo, bool lo_is_start, bool from_state) {
+  auto load_entries = [&](int64_t first, int cnt, int32_t lo, int32_t hi, bool lo_is_start, bool from_state) {
     if constexpr (MERGE) {  // entry i = list i; positions are list 0-relative row indices
       for (int i = tid; i < cnt; i += BS) {
         const int64_t rdelta = (int64_t)(a.lir[i] - a.lir[0]);
@@ -405,6 +409,28 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
     }
     for (int i = tid; i < cnt; i += BS) {
       const int64_t p = e0 + first + i;
+      if (from_state) {  // later sub-tile of a chunked task: committed cursor and its row from HBM
+        const int64_t g = go + first + i;
+        const int32_t nx = (par ? a.gnx1 : a.gnx0)[g];
+        epos[i] = (par ? a.gcur1 : a.gcur0)[g];
+        enext[i] = nx;
+        if (nx >= hi) {  // idle in this sub-tile: segments() reads only the cursor and its row
+          ecol[i] = 0;
+          continue;
+        }
+        const int32_t k = a.Bir[p];
+        if (k < 0 || k >= a.ncolA) {
+          bad |= 1 << 1;
+          ecol[i] = 0;
+          eend[i] = epos[i];
+          enext[i] = kNoRow;
+          continue;
+        }
+        ecol[i] = k;
+        eend[i] = a.gend[g];
+        if constexpr (NUM) escale[i] = reinterpret_cast<const b_t*>(a.Bnum)[p];
+        continue;
+      }
       const int32_t k = a.Bir[p];
       if constexpr (NUM) escale[i] = reinterpret_cast<const b_t*>(a.Bnum)[p];
       if (k < 0 || k >= a.ncolA) {
@@ -412,17 +438,14 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
         ecol[i] = 0;
         epos[i] = eend[i] = 0;
         enext[i] = kNoRow;
+        if (chunked) {
+          a.gend[go + first + i] = 0;
+          (par ? a.gcur1 : a.gcur0)[go + first + i] = 0;
+          (par ? a.gnx1 : a.gnx0)[go + first + i] = kNoRow;
+        }
         continue;
       }
       ecol[i] = k;
-      if (from_state) {  // later sub-tile of a chunked task: cursor and end from HBM, no search
-        const int64_t* gc = par ? a.gcur1 : a.gcur0;
-        const int64_t pos = gc[go + first + i], cend = a.gend[go + first + i];
-        epos[i] = pos;
-        eend[i] = cend;
-        enext[i] = pos < cend ? rowsA[pos] : kNoRow;
-        continue;
-      }
       int64_t base = a.Acp[k], end = a.Acp[k + 1];
       if (base < 0 || end < base || end > a.nnzA) {
         bad |= 1 << 2;
@@ -445,11 +468,13 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
       }
       epos[i] = pos;
       eend[i] = cend;
+      const int32_t nx = pos < cend ? rowsA[pos] : kNoRow;
+      enext[i] = nx;
       if (chunked) {  // the first sub-tile's cursors are committed state too (dense value pass)
         a.gend[go + first + i] = cend;
         (par ? a.gcur1 : a.gcur0)[go + first + i] = pos;
+        (par ? a.gnx1 : a.gnx0)[go + first + i] = nx;
       }
-      enext[i] = pos < cend ? rowsA[pos] : kNoRow;
     }
   };
   // segment of every entry inside [lo, hi) (idle entries -- next row >= hi -- cost one LDS read),
@@ -525,7 +550,7 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
   auto set_ovf = [&]() { __hip_atomic_store(&s_ovf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
 
   if (!chunked) {
-    load_entries(0, (int)ne, tlo, (full & 1) != 0, false);
+    load_entries(0, (int)ne, tlo, thi, (full & 1) != 0, false);
   }
   uint32_t* dwords = words;  // dense: bitmap words past the CAPD keys; int16 prefix past CAPD vals
   int16_t* dpre = nullptr;
@@ -574,7 +599,7 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
       if (chunked) {
         const int64_t first = (int64_t)ch * EMAX;
         nec = (int)((ne - first) < EMAX ? (ne - first) : EMAX);
-        load_entries(first, nec, lo, lo == tlo && (full & 1), lo != tlo);
+        load_entries(first, nec, lo, hi, lo == tlo && (full & 1), lo != tlo);
         __syncthreads();
       }
       const int P = segments(nec, hi, hi_is_end);
@@ -651,14 +676,39 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
         for (int i = tid; i < nec; i += BS) epos[i] += eoff[i];  // back to the cursors
         break;
       }
-      if (chunked) {  // this chunk's cursors after the sub-tile, into the other buffer
+      if (chunked) {  // this chunk's cursors (and their rows) after the sub-tile, into the other buffer
         int64_t* gn = par ? a.gcur0 : a.gcur1;
-        for (int i = tid; i < nec; i += BS) gn[go + (int64_t)ch * EMAX + i] = epos[i] + eoff[i + 1];
+        int32_t* gx = par ? a.gnx0 : a.gnx1;
+        for (int i = tid; i < nec; i += BS) {
+          gn[go + (int64_t)ch * EMAX + i] = epos[i] + eoff[i + 1];
+          gx[go + (int64_t)ch * EMAX + i] = enext2[i];
+        }
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the stores land before the barrier
         __syncthreads();  // entry state is reloaded by the next chunk
       }
     }
     int dtotal = 0;
+    // hash numeric: occupied slots per wave (slot ranges of SPW) -> every wave's queue offset and
+    // the total; a sub-tile whose occupied slots exceed the commit queue is retried like an overflow
+    constexpr int SPW = ((TA + NW - 1) / NW + 63) / 64 * 64;
+    int qbase = 0, qtot = 0;
+    if constexpr (NUM && !dense) {
+      const int sb = wid * SPW < TA ? wid * SPW : TA;
+      const int se = sb + SPW < TA ? sb + SPW : TA;
+      int wc = 0;
+      for (int s0 = sb; s0 < se; s0 += 64) {
+        const int sl = s0 + lane;
+        wc += __popcll(__ballot(sl < se && keys[sl] != kEmpty));
+      }
+      if (lane == 0) red[NW + wid] = wc;
+      __syncthreads();
+#pragma unroll
+      for (int x = 0; x < NW; ++x) {
+        const int rr = red[NW + x];
+        qbase += (x < wid) ? rr : 0;
+        qtot += rr;
+      }
+    }
     if constexpr (NUM && dense) {
       if (dense && !__hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
         // output rank of every word's first row: exclusive scan of the bitmap's popcounts
@@ -706,11 +756,11 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
               const int64_t* gc = par ? a.gcur1 : a.gcur0;
               const int64_t* gn = par ? a.gcur0 : a.gcur1;
               for (int i = tid; i < nec; i += BS) {
-                const int64_t pe = e0 + first + i;
-                escale[i] = reinterpret_cast<const b_t*>(a.Bnum)[pe];
                 const int64_t p0 = gc[go + first + i];
+                const int32_t len = (int32_t)(gn[go + first + i] - p0);
                 epos[i] = p0;
-                eoff[i] = (int32_t)(gn[go + first + i] - p0);
+                eoff[i] = len;
+                if (len > 0) escale[i] = reinterpret_cast<const b_t*>(a.Bnum)[e0 + first + i];
               }
               __syncthreads();
               block_scan_excl<BS>(eoff, nec, red);
@@ -722,7 +772,7 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
         __syncthreads();
       }
     }
-    if (__hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {  // table could not hold the sub-tile: halve the row range, redo
+    if (qtot > WIN || __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {  // table could not hold the sub-tile: halve the row range, redo
       if (!chunked && dense)  // the value pass never ran: restore the cursors the bitmap pass moved
         for (int i = tid; i < (int)ne; i += BS) epos[i] += eoff[i];
       __syncthreads();
@@ -762,98 +812,79 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
         out_pos += dtotal;
       }
     } else if constexpr (NUM) {
-      // rank commit. Slot s holding key x goes to (occupied slots before s) - (s - start of its
-      // run) + (keys of its run smaller than x). Wave w owns the 64-aligned slots
-      // [w*SPW, (w+1)*SPW); its occupied slots are queued in slot order (ballot + prefix
-      // popcount, into enext2: dead until the next sub-tile's entries pass) and committed 64 at
-      // a time, so the window reads run on full waves. A lane reads the kWin slots on either side
-      // of its slot at once, which gives the run's extent and the rank for every run of
-      // <= 2*kWin+1 slots without a dependent chain; longer runs (clustered rows) walk LDS.
-      constexpr int SPW = ((TA + NW - 1) / NW + 63) / 64 * 64;
-      const int sb = wid * SPW < TA ? wid * SPW : TA;
-      const int se = sb + SPW < TA ? sb + SPW : TA;
-      int wc = 0;
-      for (int s0 = sb; s0 < se; s0 += 64) {
-        const int s = s0 + lane;
-        wc += __popcll(__ballot(s < se && keys[s] != kEmpty));
+      // rank commit. The occupied slots are compacted in slot order into a queue Q (the owner
+      // map's LDS, dead here): queue index q = occupied slots before Q[q]. A run of occupied
+      // slots is a run of consecutive queue entries with consecutive slots, so slot Q[q] goes
+      // to (start of its run in the queue) + (keys of its run smaller than its key). Waves take
+      // 64 queue entries at a time: run boundaries come from comparing each slot with its queue
+      // neighbours (shuffles), run extents from two ballots, ranks from shuffling the run's keys
+      // (runs are short at fill 1/2); only runs that cross a batch edge read further keys from LDS.
+      int16_t* Q = reinterpret_cast<int16_t*>(own);
+      {
+        const int sb = wid * SPW < TA ? wid * SPW : TA;
+        const int se = sb + SPW < TA ? sb + SPW : TA;
+        const uint64_t lt = (1ull << lane) - 1ull;
+        int qo = qbase;
+        for (int s0 = sb; s0 < se; s0 += 64) {
+          const int sl = s0 + lane;
+          const bool occ = sl < se && keys[sl] != kEmpty;
+          const uint64_t mask = __ballot(occ);
+          if (occ) Q[qo + __popcll(mask & lt)] = (int16_t)sl;
+          qo += __popcll(mask);
+        }
       }
-      if (lane == 0) red[NW + wid] = wc;
       __syncthreads();
-      CBH_STAMP(10);
-      int64_t o = out_pos;
-      int tot = 0;
-#pragma unroll
-      for (int x = 0; x < NW; ++x) {
-        const int rr = red[NW + x];
-        o += (x < wid) ? rr : 0;
-        tot += rr;
-      }
-      const uint64_t lt = (1ull << lane) - 1ull;
-      auto emit = [&](int s, int32_t key, acc_t val, int64_t base) {
-        int32_t kl[kWin], kr[kWin];
-#pragma unroll
-        for (int d = 0; d < kWin; ++d) {
-          const int xl = s - 1 - d, xr = s + 1 + d;
-          kl[d] = keys[xl >= 0 ? xl : 0];
-          kr[d] = keys[xr < TA ? xr : TA - 1];
-          if (xl < 0) kl[d] = kEmpty;
-          if (xr >= TA) kr[d] = kEmpty;
+      for (int b0 = wid * 64; b0 < qtot; b0 += NW * 64) {
+        const int q = b0 + lane;
+        const bool valid = q < qtot;
+        const int sq = valid ? (int)Q[q] : -4;
+        const int32_t key = valid ? keys[sq] : kNoRow;
+        const int sup = __shfl_up(sq, 1);
+        const int sdn = __shfl_down(sq, 1);
+        const int sprev = lane == 0 ? (b0 > 0 ? (int)Q[b0 - 1] : -10) : sup;
+        const int snext = (q + 1 < qtot) ? (lane == 63 ? (int)Q[q + 1] : sdn) : -10;
+        const uint64_t mstart = __ballot(valid && sq != sprev + 1);
+        const uint64_t mend = __ballot(valid && snext != sq + 1);
+        const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+        const uint64_t below = mstart & upto;
+        const uint64_t above = mend & ~((1ull << lane) - 1ull);
+        const int rs = below ? 63 - __clzll(below) : -1;  // run start lane (-1: before the batch)
+        const int re = above ? __ffsll((long long)above) - 1 : 64;  // run end lane (64: after it)
+        const int lo_l = rs < 0 ? 0 : rs, hi_l = re > 63 ? 63 : re;
+        int rank = 0;
+        for (int j = 0;; ++j) {
+          const bool act = valid && lo_l + j <= hi_l;
+          if (__ballot(act) == 0ull) break;
+          const int32_t kj = __shfl(key, (lo_l + j) & 63);
+          rank += (act && kj < key) ? 1 : 0;
         }
-        bool lgo = true, rgo = true;
-        int left = 0, right = 0, rank = 0;
-#pragma unroll
-        for (int d = 0; d < kWin; ++d) {
-          lgo = lgo && kl[d] != kEmpty;
-          rgo = rgo && kr[d] != kEmpty;
-          left += lgo ? 1 : 0;
-          right += rgo ? 1 : 0;
-          rank += (lgo && kl[d] < key) ? 1 : 0;
-          rank += (rgo && kr[d] < key) ? 1 : 0;
+        int rstart = b0 + lo_l;
+        if (valid && rs < 0) {  // the run began in an earlier batch
+          int qq = b0 - 1;
+          while (qq >= 0 && (int)Q[qq] == (int)Q[qq + 1] - 1) {
+            rank += keys[Q[qq]] < key ? 1 : 0;
+            --qq;
+          }
+          rstart = qq + 1;
         }
-        if (lgo || rgo) {  // the run extends past the window (clustered rows)
-          int rs = s - left, re = s + right + 1;
-          if (lgo)
-            while (rs > 0 && keys[rs - 1] != kEmpty) --rs;
-          if (rgo)
-            while (re < TA && keys[re] != kEmpty) ++re;
-          rank = 0;
-          for (int x = rs; x < re; ++x) rank += keys[x] < key ? 1 : 0;
-          left = s - rs;
+        if (valid && re > 63) {  // the run goes on in a later batch
+          int qq = b0 + 64;
+          while (qq < qtot && (int)Q[qq] == (int)Q[qq - 1] + 1) {
+            rank += keys[Q[qq]] < key ? 1 : 0;
+            ++qq;
+          }
         }
-        const int64_t pos = base - left + rank;
-        if (pos >= out_end || pos >= a.ccap || pos < out_pos) {
-          bad |= 1 << 5;
-        } else {
-          a.Cir[pos] = key;
-          reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(val);
-        }
-      };
-      static_assert(NW * 128 * sizeof(int16_t) <= EMAX * sizeof(int32_t) && TA < 32768, "commit queue");
-      int16_t* cq = reinterpret_cast<int16_t*>(enext2) + wid * 128;
-      int qn = 0;  // queued slots (wave-uniform)
-      for (int s0 = sb; s0 < se; s0 += 64) {
-        const int s = s0 + lane;
-        const bool occ = s < se && keys[s] != kEmpty;
-        const uint64_t mask = __ballot(occ);
-        if (occ) cq[qn + __popcll(mask & lt)] = (int16_t)s;
-        qn += __popcll(mask);
-        __builtin_amdgcn_wave_barrier();
-        if (qn >= 64) {
-          const int sq = cq[lane];
-          emit(sq, keys[sq], vals[sq], o + lane);
-          o += 64;
-          qn -= 64;
-          const int16_t rest = lane < qn ? cq[64 + lane] : (int16_t)0;
-          __builtin_amdgcn_wave_barrier();
-          if (lane < qn) cq[lane] = rest;
-          __builtin_amdgcn_wave_barrier();
+        if (valid) {
+          const int64_t pos = out_pos + rstart + rank;
+          if (pos >= out_end || pos >= a.ccap || pos < out_pos) {
+            bad |= 1 << 5;
+          } else {
+            a.Cir[pos] = key;
+            reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(vals[sq]);
+          }
         }
       }
-      if (lane < qn) {
-        const int sq = cq[lane];
-        emit(sq, keys[sq], vals[sq], o + lane);
-      }
-      out_pos += tot;
+      out_pos += qtot;
     }
     lo = hi;
     w = wnom;
