@@ -35,6 +35,9 @@ namespace cbh {
 
 enum : int { MODE_TSYM = 0, MODE_TNUM = 1, MODE_TDENSE = 2 };
 constexpr int32_t kNoRow = 0x7fffffff;
+// cursor row not loaded yet (< every row range: the entry counts as active, and its first
+// segment search starts AT the cursor, whose row the search loads with the following ones)
+constexpr int32_t kUnknownRow = -2;
 constexpr int kFill8 = 4;  // numeric sub-tile: planned outputs, in eighths of the T home slots
 // dense sub-tiles of one window keep their products in registers between the bitmap and the value
 // pass (else the value pass gathers them again)
@@ -468,7 +471,7 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
       }
       epos[i] = pos;
       eend[i] = cend;
-      const int32_t nx = pos < cend ? rowsA[pos] : kNoRow;
+      const int32_t nx = pos < cend ? kUnknownRow : kNoRow;
       enext[i] = nx;
       if (chunked) {  // the first sub-tile's cursors are committed state too (dense value pass)
         a.gend[go + first + i] = cend;
@@ -494,7 +497,7 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
         } else {
           const int32_t k = ecol[i];
           const int32_t* blk = MERGE ? nullptr : hub_blk(k);
-          stop = stop_search<8>(rowsA, p + 1, end, hi, blk, blk ? a.Acp[k] : 0, a.RB, nx2);
+          stop = stop_search<8>(rowsA, nx == kUnknownRow ? p : p + 1, end, hi, blk, blk ? a.Acp[k] : 0, a.RB, nx2);
         }
       }
       eoff[i] = (int32_t)(stop - p);

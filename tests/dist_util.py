@@ -14,6 +14,7 @@ import os
 import socket
 import sys
 import tempfile
+import time
 import traceback
 
 import numpy as np
@@ -211,8 +212,9 @@ def run_world(fn, world, *args, timeout=240):
         procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, d)) for r in range(world)]
         for p in procs:
             p.start()
+        deadline = time.monotonic() + timeout  # one budget for the whole world, not per rank
         for p in procs:
-            p.join(timeout)
+            p.join(max(0.0, deadline - time.monotonic()))
         for p in procs:
             if p.is_alive():
                 p.kill()

@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 if [ -n "$K" ]; then KARG=(-k "$K"); else KARG=(); fi
 echo "== $(date +%T) pytest"
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${KARG[@]}" > "$OUT/pytest_gpu.log" 2>&1 \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread "${KARG[@]}" > "$OUT/pytest_gpu.log" 2>&1 \
   || { tail -60 "$OUT/pytest_gpu.log"; exit 1; }
 tail -2 "$OUT/pytest_gpu.log"
 echo "== $(date +%T) bench"
