@@ -90,3 +90,39 @@ def test_gpu_summa3d_1x1x2(golden):
 def test_gpu_summa3d_2x2x2(golden):
     res = run_world(_gpu_worker, 8, 12, "pt_i64", "3d", 2, 0, 2, timeout=150)
     _check(res, golden["digests"]["rmat12_pt_i64"])
+
+
+def _gpu_ccgrid_worker(rank, world, scale, tag, c, g):
+    """the standalone 3D API (spgemm3d: CCGrid / SplitMat / multiply) on the device"""
+    import torch
+
+    import combblas_amd as cb
+    from combblas_amd import spgemm3d as s3
+    from combblas_amd.backend import HipBackend
+    from combblas_amd.spparmat import SpParMat, _gather, block_range
+
+    torch.cuda.set_device(0)
+    ctx = cb.Context(0)
+    be = HipBackend(ctx)
+    A = cb.rmat(scale)
+    d = H.values_for(tag, H.Dcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num))
+    h = cb.HostDcsc(d.m, d.n, d.jc, d.cp, d.ir, d.num)
+    CMG = s3.CCGrid(c, g)
+    vdt = {"pt_i64": torch.int64, "pt_f64": torch.float64}[tag]
+    root = CMG.layer_grid == 0
+    sA = s3.SplitMat(CMG, SpParMat.distribute(h, CMG.layerGrid, be).seq if root else None, be, False, vdt)
+    sB = s3.SplitMat(CMG, SpParMat.distribute(h, CMG.layerGrid, be).seq if root else None, be, True, vdt)
+    C = s3.multiply(sA, sB, CMG, False, True, be)
+    r0 = block_range(d.m, g, CMG.RankInCol)[0]
+    c0, c1 = block_range(d.n, g, CMG.RankInRow)
+    G = _gather(be, C, r0, c0 + CMG.layer_grid * ((c1 - c0) // c), d.m, d.n)
+    torch.cuda.synchronize()
+    ctx.close()
+    if rank == 0:
+        return (G.m, G.n, G.jc, G.cp, G.ir, G.num)
+    return None
+
+
+def test_gpu_ccgrid_multiply_2x2x2(golden):
+    res = run_world(_gpu_ccgrid_worker, 8, 12, "pt_i64", 2, 2, timeout=150)
+    _check(res, golden["digests"]["rmat12_pt_i64"])
