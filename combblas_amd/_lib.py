@@ -92,6 +92,9 @@ SIGNATURES = {
     "cbh_kernel_stats_reset": (ctypes.c_int, [ctypes.c_void_p]),
     "cbh_spgemm_masked": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_transpose": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_mat_checksum": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_uint64)]),
     "cbh_ewise_mult": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_col_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p]),
@@ -120,6 +123,8 @@ ERRORS = {3001: "GRIDMISMATCH", 3002: "DIMMISMATCH", 3005: "MATRIXALIAS", 4001: 
 
 CBH_KEEP_EMPTY_COLS = 0x2
 CBH_MASK_PATTERN = 0x4
+CBH_MASK_EXPAND = 0x8
+CBH_MASK_DOT = 0x10
 CBH_PHASE_CHECKSUM = 0x100
 CBH_TUPLES_DROP_LOOPS = 0x1
 

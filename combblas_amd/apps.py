@@ -16,7 +16,7 @@ import ctypes
 
 import torch
 
-from ._lib import CBH_MASK_PATTERN, check, lib
+from ._lib import CBH_MASK_DOT, CBH_MASK_EXPAND, CBH_MASK_PATTERN, check, lib
 from .semirings import Semiring
 from .spdccols import SpDCCols
 
@@ -27,10 +27,19 @@ def _p(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
-def MaskedSpGEMM(SR: Semiring, A: SpDCCols, B: SpDCCols, M: SpDCCols, pattern=False) -> SpDCCols:
+def MaskedSpGEMM(SR: Semiring, A: SpDCCols, B: SpDCCols, M: SpDCCols, pattern=False, method="auto") -> SpDCCols:
+    """method: "expand" (products of A*B looked up in the mask column), "dot" (row i of A
+    intersected with column j of B per mask entry), "auto" (dot from nnz(A) >= 65536)"""
+    flags = (CBH_MASK_PATTERN if pattern else 0) | {"auto": 0, "expand": CBH_MASK_EXPAND, "dot": CBH_MASK_DOT}[method]
     h = ctypes.c_void_p()
-    check(lib().cbh_spgemm_masked(A.ctx.h, SR.code, A.h, B.h, M.h, CBH_MASK_PATTERN if pattern else 0,
-                                  ctypes.byref(h)), A.ctx.h)
+    check(lib().cbh_spgemm_masked(A.ctx.h, SR.code, A.h, B.h, M.h, flags, ctypes.byref(h)), A.ctx.h)
+    return SpDCCols(A.ctx, h)
+
+
+def Transpose(A: SpDCCols) -> SpDCCols:
+    """A' as a new device block (SpDCCols::Transpose), rows ascending in every column"""
+    h = ctypes.c_void_p()
+    check(lib().cbh_transpose(A.ctx.h, A.h, ctypes.byref(h)), A.ctx.h)
     return SpDCCols(A.ctx, h)
 
 
@@ -40,14 +49,14 @@ def EWiseMult(A: SpDCCols, B: SpDCCols) -> SpDCCols:
     return SpDCCols(A.ctx, h)
 
 
-def TriangleCount(L: SpDCCols, L2: SpDCCols = None) -> int:
+def TriangleCount(L: SpDCCols, L2: SpDCCols = None, method="auto") -> int:
     """TC.cpp:108-115: C = (L*L) .* L, triangles = sum(C). L2 is a second copy of L (the
     product's operands must not alias, ParFriends.h:172-179)."""
     from .semirings import PlusTimesSRing
     own = L2 is None
     if own:
         L2 = SpDCCols.from_tensors(L.ctx, L.m, L.n, *[t.clone() for t in L.tensors()])
-    C = MaskedSpGEMM(PlusTimesSRing, L, L2, L)
+    C = MaskedSpGEMM(PlusTimesSRing, L, L2, L, method=method)
     tri = int(C.tensors()[3].sum().item()) if C.nnz else 0
     C.free()
     if own:
@@ -84,3 +93,28 @@ def PruneColumn(A: SpDCCols, thresh) -> SpDCCols:
     h = ctypes.c_void_p()
     check(lib().cbh_prune_columns(A.ctx.h, A.h, _p(thresh.contiguous()), ctypes.byref(h)), A.ctx.h)
     return SpDCCols(A.ctx, h)
+
+
+def TCLower(ctx, scale: int, edgefactor: int = 16, seed=None) -> SpDCCols:
+    """Applications/TC.cpp:98-104,139-150 on the device: the packed Graph500 R-MAT edges (bit-identical
+    to DEL->GenGraph500Data), RemoveLoops, Symmetricize (A += A'), Apply(1) and
+    GetLowerTriangular -- L keeps every entry of the symmetric pattern, value 1 below the
+    diagonal and an explicit 0 above it. The tuples are combined on the device
+    (cbh_tuples_to_dcsc; duplicates OR'ed as bools, so every kept entry is exactly 0 or 1)."""
+    from .rmat import DEFAULT_SEED, rmat_edges
+    from .spdccols import _torch
+
+    torch = _torch()
+    src, dst = rmat_edges(scale, edgefactor, DEFAULT_SEED if seed is None else seed)
+    dev = ctx.tdevice
+    s, d = torch.from_numpy(src).to(dev), torch.from_numpy(dst).to(dev)
+    del src, dst
+    rows, cols = torch.cat([s, d]), torch.cat([d, s])
+    del s, d
+    n = 1 << scale
+    P = SpDCCols.from_tuples(ctx, n, n, rows.to(torch.int32), cols, rows > cols, removeloops=True)
+    del rows, cols
+    cp, jc, ir, num = P.tensors()
+    L = SpDCCols.from_tensors(ctx, n, n, cp.clone(), jc.clone(), ir.clone(), num.to(torch.int64))
+    P.free()
+    return L

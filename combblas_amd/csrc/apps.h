@@ -146,6 +146,281 @@ __global__ __launch_bounds__(BS) void masked_kernel(MaskArgs a) {
   if (tid == 0) a.hits[c] = nhits;
 }
 
+// ---------------------------------------------------------------------------- masked SpGEMM, dot form
+// C = (A*B) .* M evaluated per MASK ENTRY (i, j): the sorted k-lists of row i of A (column i of
+// AT = A') and of column j of B are intersected, SR::add of SR::multiply(A(i,k), B(k,j)) over the
+// common k in ascending order; the entry exists iff the intersection is not empty (explicit zeros
+// count, as in the expanding form). Work is sum over mask entries of the shorter list (x a search
+// in the longer one), instead of the full flops of A*B: TC's (L*L) .* L at R-MAT scale 24
+// enumerates ~10^12 products of the symmetric pattern, the dot form a few 10^10 probes.
+// Mask entries are classified by the shorter list: short (thread per entry, galloping merge),
+// long (pieces of kDotPiece elements, one wave per piece, partials reduced in piece order).
+constexpr int kDotThread = 64;   // shorter list <= this: one thread per entry
+constexpr int kDotPiece = 2048;  // long entries: elements of the shorter list per wave piece
+
+struct DotArgs {
+  const int64_t* ATd;  // AT dense column pointers (A.m + 1): row i of A = AT(:, i), rows = k
+  const int32_t* ATir;
+  const void* ATnum;
+  const int64_t* Bd;  // B dense column pointers (B.n + 1)
+  const int32_t* Bir;
+  const void* Bnum;
+  const int64_t* Mcol;  // per mask entry: its column id
+  const int32_t* Mir;
+  int64_t nnzM, mA, nB;
+  void* Tnum;      // per mask entry: the sum (where Tflag)
+  uint8_t* Tflag;  // per mask entry: intersection not empty
+  int* err;
+};
+
+// first q in [lo, hi) with rows[q] >= key by galloping from lo
+__device__ __forceinline__ int64_t dot_gallop(const int32_t* __restrict__ rows, int64_t lo, int64_t hi, int32_t key) {
+  if (lo >= hi || rows[lo] >= key) return lo;
+  return gallop64(rows, lo + 1, hi, key);
+}
+
+template <class V>
+__device__ __forceinline__ V shfl_down_val(V v, int d) {
+  if constexpr (sizeof(V) == 8) {
+    return __builtin_bit_cast(V, (unsigned long long)__shfl_down(__builtin_bit_cast(unsigned long long, v), d));
+  } else if constexpr (sizeof(V) == 4) {
+    return __builtin_bit_cast(V, (unsigned)__shfl_down(__builtin_bit_cast(unsigned, v), d));
+  } else {
+    static_assert(sizeof(V) == 1, "value width");
+    return (V)__shfl_down((int)v, d);
+  }
+}
+
+// the two lists of mask entry p; returns false (and counts a guard) on out-of-range ids
+__device__ __forceinline__ bool dot_lists(const DotArgs& a, int64_t p, int64_t& a0, int64_t& a1, int64_t& b0,
+                                          int64_t& b1) {
+  const int64_t i = a.Mir[p], j = a.Mcol[p];
+  if (i < 0 || i >= a.mA || j < 0 || j >= a.nB) return false;
+  a0 = a.ATd[i];
+  a1 = a.ATd[i + 1];
+  b0 = a.Bd[j];
+  b1 = a.Bd[j + 1];
+  return true;
+}
+
+// class of every mask entry: 0 = empty intersection for sure (a list is empty: flag 0 written
+// here), 1 = thread, 2 = long (pieces). Waves append their entries to the class lists with one
+// atomic per class; npiece[x] = pieces of long entry x.
+__global__ __launch_bounds__(256) void dot_classify_kernel(DotArgs a, int32_t* __restrict__ lthr,
+                                                           int32_t* __restrict__ llong, int64_t* __restrict__ npiece,
+                                                           unsigned long long* __restrict__ counts) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  int cls = -1;
+  int64_t ls = 0;
+  if (p < a.nnzM) {
+    int64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+    if (!dot_lists(a, p, a0, a1, b0, b1)) atomicOr(&a.err[2], 1);
+    ls = (a1 - a0) < (b1 - b0) ? (a1 - a0) : (b1 - b0);
+    cls = ls <= 0 ? 0 : (ls <= kDotThread ? 1 : 2);
+    if (cls == 0) a.Tflag[p] = 0;
+  }
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const uint64_t m1 = __ballot(cls == 1), m2 = __ballot(cls == 2);
+  unsigned long long base1 = 0, base2 = 0;
+  if (lane == 0) {
+    if (m1) base1 = atomicAdd(&counts[0], (unsigned long long)__popcll(m1));
+    if (m2) base2 = atomicAdd(&counts[1], (unsigned long long)__popcll(m2));
+  }
+  base1 = __shfl(base1, 0);
+  base2 = __shfl(base2, 0);
+  if (cls == 1) lthr[base1 + __popcll(m1 & lt)] = (int32_t)p;
+  if (cls == 2) {
+    const int64_t x = (int64_t)base2 + __popcll(m2 & lt);
+    llong[x] = (int32_t)p;
+    npiece[x] = (ls + kDotPiece - 1) / kDotPiece;
+  }
+}
+
+// thread per short entry: the shorter list drives, the longer one is galloped through
+template <class SR>
+__global__ __launch_bounds__(256) void dot_thread_kernel(DotArgs a, const int32_t* __restrict__ list, int64_t n) {
+  using val_t = typename SR::val_t;
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= n) return;
+  const int64_t p = list[x];
+  int64_t a0, a1, b0, b1;
+  if (!dot_lists(a, p, a0, a1, b0, b1)) return;
+  const val_t* __restrict__ av = reinterpret_cast<const val_t*>(a.ATnum);
+  const val_t* __restrict__ bv = reinterpret_cast<const val_t*>(a.Bnum);
+  val_t acc{};
+  bool hit = false;
+  if (a1 - a0 <= b1 - b0) {
+    int64_t q = b0;
+    for (int64_t s = a0; s < a1 && q < b1; ++s) {
+      const int32_t k = a.ATir[s];
+      q = dot_gallop(a.Bir, q, b1, k);
+      if (q < b1 && a.Bir[q] == k) {
+        const val_t pr = SR::multiply(av[s], bv[q]);
+        acc = hit ? SR::add(acc, pr) : pr;
+        hit = true;
+      }
+    }
+  } else {
+    int64_t q = a0;
+    for (int64_t s = b0; s < b1 && q < a1; ++s) {
+      const int32_t k = a.Bir[s];
+      q = dot_gallop(a.ATir, q, a1, k);
+      if (q < a1 && a.ATir[q] == k) {
+        const val_t pr = SR::multiply(av[q], bv[s]);
+        acc = hit ? SR::add(acc, pr) : pr;
+        hit = true;
+      }
+    }
+  }
+  a.Tflag[p] = hit ? 1 : 0;
+  if (hit) reinterpret_cast<val_t*>(a.Tnum)[p] = acc;
+}
+
+// piece -> (long entry, piece number): item y of long entry x for y in [poff[x], poff[x+1])
+__global__ __launch_bounds__(256) void dot_items_kernel(const int64_t* __restrict__ poff, int64_t nlong,
+                                                        int32_t* __restrict__ item_entry) {
+  const int lane = threadIdx.x & 63;
+  // wave-strided: a grid's work-item count is 32-bit (AQL dispatch), so the grid is capped
+  for (int64_t x = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); x < nlong; x += (int64_t)gridDim.x * 4)
+    for (int64_t y = poff[x] + lane; y < poff[x + 1]; y += 64) item_entry[y] = (int32_t)x;
+}
+
+// piece y of a long entry (one wave): lanes take 64 consecutive elements of the shorter list at a
+// time and binary-search them in the longer one (bounded below by the previous batch's last
+// position); the lane partials are folded in lane order into the piece's partial
+template <class SR>
+__device__ __forceinline__ void dot_piece(const DotArgs& a, const int32_t* __restrict__ llong,
+                                          const int64_t* __restrict__ poff, const int32_t* __restrict__ item_entry,
+                                          int64_t y, void* __restrict__ pval, uint8_t* __restrict__ phit, int lane) {
+  using val_t = typename SR::val_t;
+  const int32_t x = item_entry[y];
+  const int64_t p = llong[x];
+  int64_t a0, a1, b0, b1;
+  if (!dot_lists(a, p, a0, a1, b0, b1)) {
+    if (lane == 0) phit[y] = 0;
+    return;
+  }
+  const val_t* __restrict__ av = reinterpret_cast<const val_t*>(a.ATnum);
+  const val_t* __restrict__ bv = reinterpret_cast<const val_t*>(a.Bnum);
+  const bool a_short = a1 - a0 <= b1 - b0;
+  const int32_t* __restrict__ srow = a_short ? a.ATir : a.Bir;
+  const int32_t* __restrict__ lrow = a_short ? a.Bir : a.ATir;
+  const int64_t s0 = (a_short ? a0 : b0) + (y - poff[x]) * (int64_t)kDotPiece;
+  const int64_t s1e = a_short ? a1 : b1;
+  const int64_t s1 = s0 + kDotPiece < s1e ? s0 + kDotPiece : s1e;
+  int64_t lo = a_short ? b0 : a0;
+  const int64_t hi = a_short ? b1 : a1;
+  val_t acc{};
+  bool hit = false;
+  for (int64_t base = s0; base < s1 && lo < hi; base += 64) {
+    const int64_t s = base + lane;
+    int64_t q = hi;
+    if (s < s1) {
+      const int32_t k = srow[s];
+      q = lb_rows64(lrow, lo, hi, k);
+      if (q < hi && lrow[q] == k) {
+        const val_t pr = a_short ? SR::multiply(av[s], bv[q]) : SR::multiply(av[q], bv[s]);
+        acc = hit ? SR::add(acc, pr) : pr;
+        hit = true;
+      }
+    }
+    // the next batch's keys are larger than every key of this one
+    const int last = (s1 - base) < 64 ? (int)(s1 - base) - 1 : 63;
+    lo = __shfl(q, last);
+  }
+  // fold lanes in order: lane l absorbs lane l + d (higher lanes hold larger k)
+  for (int d = 1; d < 64; d <<= 1) {
+    const val_t o = shfl_down_val(acc, d);
+    const int oh = __shfl_down((int)hit, d);
+    if ((lane & (2 * d - 1)) == 0 && lane + d < 64 && oh) {
+      acc = hit ? SR::add(acc, o) : o;
+      hit = true;
+    }
+  }
+  if (lane == 0) {
+    phit[y] = hit ? 1 : 0;
+    if (hit) reinterpret_cast<val_t*>(pval)[y] = acc;
+  }
+}
+
+template <class SR>
+__global__ __launch_bounds__(256) void dot_wave_kernel(DotArgs a, const int32_t* __restrict__ llong,
+                                                       const int64_t* __restrict__ poff,
+                                                       const int32_t* __restrict__ item_entry, int64_t nitems,
+                                                       void* __restrict__ pval, uint8_t* __restrict__ phit) {
+  const int lane = threadIdx.x & 63;
+  // wave-strided over the pieces (the grid is capped: a dispatch counts work-items in 32 bits)
+  for (int64_t y = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); y < nitems; y += (int64_t)gridDim.x * 4)
+    dot_piece<SR>(a, llong, poff, item_entry, y, pval, phit, lane);
+}
+
+// long entry x: its pieces folded in order
+template <class SR>
+__global__ __launch_bounds__(256) void dot_fold_kernel(DotArgs a, const int32_t* __restrict__ llong,
+                                                       const int64_t* __restrict__ poff, int64_t nlong,
+                                                       const void* __restrict__ pval, const uint8_t* __restrict__ phit) {
+  using val_t = typename SR::val_t;
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= nlong) return;
+  val_t acc{};
+  bool hit = false;
+  for (int64_t y = poff[x]; y < poff[x + 1]; ++y)
+    if (phit[y]) {
+      const val_t v = reinterpret_cast<const val_t*>(pval)[y];
+      acc = hit ? SR::add(acc, v) : v;
+      hit = true;
+    }
+  const int64_t p = llong[x];
+  a.Tflag[p] = hit ? 1 : 0;
+  if (hit) reinterpret_cast<val_t*>(a.Tnum)[p] = acc;
+}
+
+// hits per mask column (wave per slot) and, with WRITE, the compaction of the hit entries in
+// mask order: C(ir, num) at off[slot] + rank, num = sum * M's value (EWiseMult, Friends.h:871)
+// unless PATTERN
+template <class V, bool WRITE, bool PATTERN>
+__global__ __launch_bounds__(256) void dot_collect_kernel(const int64_t* __restrict__ Mcp, const int32_t* __restrict__ Mir,
+                                                          const V* __restrict__ Mnum, int64_t nzcM,
+                                                          const uint8_t* __restrict__ Tflag, const V* __restrict__ Tnum,
+                                                          int64_t* __restrict__ hits, const int64_t* __restrict__ off,
+                                                          int32_t* __restrict__ Cir, V* __restrict__ Cnum) {
+  const int lane = threadIdx.x & 63;
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= nzcM) return;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  int64_t o = WRITE ? off[s] : 0;
+  for (int64_t base = Mcp[s]; base < Mcp[s + 1]; base += 64) {
+    const int64_t p = base + lane;
+    const bool h = p < Mcp[s + 1] && Tflag[p];
+    const uint64_t m = __ballot(h);
+    if (WRITE && h) {
+      const int64_t d = o + __popcll(m & lt);
+      Cir[d] = Mir[p];
+      V v = Tnum[p];
+      if constexpr (!PATTERN) v = (V)(v * Mnum[p]);
+      Cnum[d] = v;
+    }
+    o += __popcll(m);
+  }
+  if (!WRITE && lane == 0) hits[s] = o;
+}
+
+// A's entries as the tuples of A' (wave per column slot): row = A's column id, col = A's row id
+__global__ __launch_bounds__(256) void transpose_tuples_kernel(const int64_t* __restrict__ jc,
+                                                               const int64_t* __restrict__ cp, int64_t nzc,
+                                                               const int32_t* __restrict__ ir, int32_t* __restrict__ trow,
+                                                               int64_t* __restrict__ tcol) {
+  const int lane = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= nzc) return;
+  const int32_t j = (int32_t)jc[c];
+  for (int64_t p = cp[c] + lane; p < cp[c + 1]; p += 64) {
+    trow[p] = j;
+    tcol[p] = ir[p];
+  }
+}
+
 // per slot of X: Y's slot holding the same column id (both jc arrays ascending), -1 if none
 __global__ void match_slots_kernel(const int64_t* __restrict__ Xjc, int64_t nzcX, const int64_t* __restrict__ Yjc,
                                    int64_t nzcY, int64_t* __restrict__ yslot) {

@@ -587,6 +587,9 @@ static int sum_i64(cbh_ctx* ctx, Scratch& S, const int64_t* in, int64_t n, int64
 }
 
 static inline unsigned blocks_for(int64_t n, int bs) { return (unsigned)std::max<int64_t>(1, (n + bs - 1) / bs); }
+// grid cap of the wave-strided kernels (an AQL dispatch counts work-items in 32 bits: a direct
+// grid of blocks_for(n, 4) x 256 threads overflows from n = 2^26 items)
+constexpr unsigned kWaveGridCap = 1u << 16;
 
 static int check_err(cbh_ctx* ctx) {
   int h[16];
@@ -1963,16 +1966,178 @@ int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* p
 // ============================================================================ callers around the hot path
 // (TC's masked product, EWiseMult, HipMCL's column prune/select/recover)
 
+}  // extern "C"
+
+extern "C" int cbh_mat_checksum(cbh_ctx* ctx, const cbh_mat* M, double* value_sum, uint64_t* digest) {
+  if (!ctx || !M || !value_sum || !digest) return fail(ctx, CBH_E_ARG, "null argument");
+  Scratch S(ctx);
+  double* d_sum;
+  unsigned long long* d_dig;
+  CBH_TRY(S.get(&d_sum, 1));
+  CBH_TRY(S.get(&d_dig, 1));
+  CBH_HIP(ctx, hipMemsetAsync(d_sum, 0, sizeof(double), ctx->stream));
+  CBH_HIP(ctx, hipMemsetAsync(d_dig, 0, sizeof(unsigned long long), ctx->stream));
+  auto run = [&](auto tag) {
+    using VT = decltype(tag);
+    hipLaunchKernelGGL(checksum_kernel<VT>, dim3(blocks_for(M->nzc, 4)), dim3(256), 0, ctx->stream, M->jc, M->cp,
+                       (int64_t)0, M->nzc, M->ir, reinterpret_cast<const VT*>(M->num), (int64_t)0, d_sum, d_dig);
+  };
+  if (M->nzc > 0) {
+    switch (M->dtype) {
+      case CBH_F64: run(double{}); break;
+      case CBH_I64: run(int64_t{}); break;
+      case CBH_F32: run(float{}); break;
+      case CBH_I32: run(int32_t{}); break;
+      case CBH_BOOL: run(uint8_t{}); break;
+      default: return fail(ctx, CBH_E_ARG, "checksum: opaque value type");
+    }
+    CBH_HIP(ctx, hipGetLastError());
+  }
+  double hs = 0;
+  unsigned long long hd = 0;
+  CBH_HIP(ctx, hipMemcpyAsync(&hs, d_sum, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipMemcpyAsync(&hd, d_dig, sizeof(hd), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  *value_sum = hs;
+  *digest = hd;
+  return CBH_OK;
+}
+
+extern "C" int cbh_transpose(cbh_ctx* ctx, const cbh_mat* A, cbh_mat** AT) {
+  if (!ctx || !A || !AT) return fail(ctx, CBH_E_ARG, "null argument");
+  *AT = nullptr;
+  if (A->n > INT32_MAX) return fail(ctx, CBH_E_DIMMISMATCH, "transpose: column count exceeds 32-bit row ids");
+  if (A->nnz == 0) return empty_result(ctx, A->n, A->m, A->dtype, AT);
+  Scratch S(ctx);
+  int32_t* trow;
+  int64_t* tcol;
+  CBH_TRY(S.get(&trow, A->nnz));
+  CBH_TRY(S.get(&tcol, A->nnz));
+  hipLaunchKernelGGL(transpose_tuples_kernel, dim3(blocks_for(A->nzc, 4)), dim3(256), 0, ctx->stream, A->jc, A->cp,
+                     A->nzc, A->ir, trow, tcol);
+  CBH_HIP(ctx, hipGetLastError());
+  return cbh_tuples_to_dcsc(ctx, A->n, A->m, A->nnz, trow, tcol, A->num, (cbh_dtype)A->dtype, 0, AT);
+}
+
+// C = (A*B) .* M, dot form (apps.h, "masked SpGEMM, dot form")
+template <class SR>
+static int masked_dot(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, const cbh_mat* M, bool pattern, cbh_mat** C) {
+  using VT = typename SR::val_t;
+  if (M->nnz > INT32_MAX) return fail(ctx, CBH_E_ARG, "dot-form mask: at most 2^31-1 entries");
+  cbh_mat* AT = nullptr;
+  CBH_TRY(cbh_transpose(ctx, A, &AT));
+  struct ATGuard {
+    cbh_ctx* c;
+    cbh_mat* m;
+    ~ATGuard() { cbh_mat_free(c, m); }
+  } atg{ctx, AT};
+  Scratch S(ctx);
+  const int64_t nm = M->nnz, nzc = M->nzc;
+  int64_t *ATd, *Bd, *Mcol, *npiece, *poff, *hits, *off, *flag, *pos;
+  int32_t *lthr, *llong, *item;
+  unsigned long long* counts;
+  VT* Tnum;
+  uint8_t* Tflag;
+  CBH_TRY(S.get(&ATd, A->m + 1));
+  CBH_TRY(S.get(&Bd, B->n + 1));
+  CBH_TRY(S.get(&Mcol, nm));
+  CBH_TRY(S.get(&lthr, nm));
+  CBH_TRY(S.get(&llong, nm));
+  CBH_TRY(S.get(&npiece, nm + 1));
+  CBH_TRY(S.get(&counts, 2));
+  CBH_TRY(S.get(&Tnum, nm));
+  CBH_TRY(S.get(&Tflag, nm));
+  hipLaunchKernelGGL(densify_cp_kernel, dim3(blocks_for(A->m + 1, 256)), dim3(256), 0, ctx->stream, AT->jc, AT->cp,
+                     AT->nzc, A->m, AT->nnz, ATd);
+  hipLaunchKernelGGL(densify_cp_kernel, dim3(blocks_for(B->n + 1, 256)), dim3(256), 0, ctx->stream, B->jc, B->cp,
+                     B->nzc, B->n, B->nnz, Bd);
+  hipLaunchKernelGGL(expand_cols_kernel, dim3(blocks_for(nzc, 4)), dim3(256), 0, ctx->stream, M->jc, M->cp, nzc, Mcol);
+  CBH_HIP(ctx, hipMemsetAsync(counts, 0, 2 * sizeof(unsigned long long), ctx->stream));
+  DotArgs a{ATd, AT->ir, AT->num, Bd, B->ir, B->num, Mcol, M->ir, nm, A->m, B->n, Tnum, Tflag, ctx->d_err};
+  hipLaunchKernelGGL(dot_classify_kernel, dim3(blocks_for(nm, 256)), dim3(256), 0, ctx->stream, a, lthr, llong, npiece,
+                     counts);
+  CBH_HIP(ctx, hipGetLastError());
+  unsigned long long cnt[2];
+  CBH_HIP(ctx, hipMemcpyAsync(cnt, counts, sizeof(cnt), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  CBH_TRY(check_err(ctx));
+  const int64_t nthr = (int64_t)cnt[0], nlong = (int64_t)cnt[1];
+  if (nthr > 0)
+    hipLaunchKernelGGL(dot_thread_kernel<SR>, dim3(blocks_for(nthr, 256)), dim3(256), 0, ctx->stream, a, lthr, nthr);
+  if (nlong > 0) {
+    CBH_TRY(S.get(&poff, nlong + 1));
+    CBH_HIP(ctx, hipMemsetAsync(npiece + nlong, 0, sizeof(int64_t), ctx->stream));
+    CBH_TRY(exclusive_scan_i64(ctx, S, npiece, poff, nlong + 1));
+    int64_t nitems = 0;
+    CBH_HIP(ctx, hipMemcpyAsync(&nitems, poff + nlong, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (nitems > INT32_MAX) return fail(ctx, CBH_E_ARG, "dot-form mask: too many pieces");
+    VT* pval;
+    uint8_t* phit;
+    CBH_TRY(S.get(&item, nitems));
+    CBH_TRY(S.get(&pval, nitems));
+    CBH_TRY(S.get(&phit, nitems));
+    // wave-strided kernels: capped grids (a dispatch's work-item count is 32-bit)
+    hipLaunchKernelGGL(dot_items_kernel, dim3(std::min(blocks_for(nlong, 4), kWaveGridCap)), dim3(256), 0, ctx->stream,
+                       poff, nlong, item);
+    hipLaunchKernelGGL(dot_wave_kernel<SR>, dim3(std::min(blocks_for(nitems, 4), kWaveGridCap)), dim3(256), 0,
+                       ctx->stream, a, llong, poff, item, nitems, pval, phit);
+    hipLaunchKernelGGL(dot_fold_kernel<SR>, dim3(blocks_for(nlong, 256)), dim3(256), 0, ctx->stream, a, llong, poff,
+                       nlong, pval, phit);
+  }
+  CBH_HIP(ctx, hipGetLastError());
+  CBH_TRY(S.get(&hits, nzc + 1));
+  CBH_TRY(S.get(&off, nzc + 1));
+  CBH_TRY(S.get(&flag, nzc + 1));
+  CBH_TRY(S.get(&pos, nzc + 1));
+  const VT* Mnum = reinterpret_cast<const VT*>(M->num);
+  hipLaunchKernelGGL((dot_collect_kernel<VT, false, false>), dim3(blocks_for(nzc, 4)), dim3(256), 0, ctx->stream, M->cp,
+                     M->ir, Mnum, nzc, Tflag, Tnum, hits, nullptr, nullptr, nullptr);
+  CBH_HIP(ctx, hipMemsetAsync(hits + nzc, 0, sizeof(int64_t), ctx->stream));
+  CBH_TRY(exclusive_scan_i64(ctx, S, hits, off, nzc + 1));
+  hipLaunchKernelGGL(nz_flag_kernel, dim3(blocks_for(nzc + 1, 256)), dim3(256), 0, ctx->stream, hits, nzc + 1, flag);
+  CBH_TRY(exclusive_scan_i64(ctx, S, flag, pos, nzc + 1));
+  int64_t h[2];
+  CBH_HIP(ctx, hipMemcpyAsync(&h[0], off + nzc, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipMemcpyAsync(&h[1], pos + nzc, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  CBH_TRY(check_err(ctx));
+  cbh_mat* out;
+  CBH_TRY(new_mat(ctx, A->m, B->n, h[0], h[1], A->dtype, &out));
+  if (pattern)
+    hipLaunchKernelGGL((dot_collect_kernel<VT, true, true>), dim3(blocks_for(nzc, 4)), dim3(256), 0, ctx->stream, M->cp,
+                       M->ir, Mnum, nzc, Tflag, Tnum, hits, off, out->ir, reinterpret_cast<VT*>(out->num));
+  else
+    hipLaunchKernelGGL((dot_collect_kernel<VT, true, false>), dim3(blocks_for(nzc, 4)), dim3(256), 0, ctx->stream, M->cp,
+                       M->ir, Mnum, nzc, Tflag, Tnum, hits, off, out->ir, reinterpret_cast<VT*>(out->num));
+  hipLaunchKernelGGL(compact_cols_kernel, dim3(blocks_for(nzc, 256)), dim3(256), 0, ctx->stream, hits, pos, M->jc, off,
+                     nzc, out->jc, out->cp);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    cbh_mat_free(ctx, out);
+    return fail(ctx, CBH_E_HIP, std::string("masked dot: ") + hipGetErrorString(e));
+  }
+  *C = out;
+  return CBH_OK;
+}
+
+extern "C" {
+
 int cbh_spgemm_masked(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh_mat* B, const cbh_mat* M,
                       uint32_t flags, cbh_mat** C) {
   CBH_TRY(validate_pair(ctx, A, B));
   if (!M || !C) return fail(ctx, CBH_E_ARG, "null mask or output");
   if (M->m != A->m || M->n != B->n) return fail(ctx, CBH_E_DIMMISMATCH, "mask dimensions differ from A*B's");
   if (M->dtype != A->dtype) return fail(ctx, CBH_E_ARG, "mask dtype differs from A's");
+  if ((flags & CBH_MASK_DOT) && (flags & CBH_MASK_EXPAND)) return fail(ctx, CBH_E_ARG, "DOT and EXPAND both set");
   *C = nullptr;
   if (A->nnz == 0 || B->nnz == 0 || M->nnz == 0) return empty_result(ctx, A->m, B->n, A->dtype, C);
-  if (B->nzc > INT32_MAX) return fail(ctx, CBH_E_ARG, "too many columns for one launch");
   const bool pattern = (flags & CBH_MASK_PATTERN) != 0;
+  const bool dot = (flags & CBH_MASK_DOT) || (!(flags & CBH_MASK_EXPAND) && A->nnz >= 65536);
+  if (dot)
+    return dispatch_sr(ctx, sr, A->dtype,
+                       [&](auto srv) -> int { return masked_dot<decltype(srv)>(ctx, A, B, M, pattern, C); });
+  if (B->nzc > INT32_MAX) return fail(ctx, CBH_E_ARG, "too many columns for one launch");
   return dispatch_sr(ctx, sr, A->dtype, [&](auto srv) -> int {
     using SR = decltype(srv);
     using VT = typename SR::val_t;

@@ -258,6 +258,13 @@ class SpDCCols:
                                      num.ctypes.data, 0), self.ctx.h)
         return HostDcsc(self.m, self.n, jc, cp, ir, num)
 
+    def checksum(self):
+        """(value sum, order-sensitive digest) computed on the device (cbh_mat_checksum; the same
+        definition as tests/helpers.digest and the phased product's CBH_PHASE_CHECKSUM)"""
+        s, d = ctypes.c_double(), ctypes.c_uint64()
+        check(lib().cbh_mat_checksum(self.ctx.h, self.h, ctypes.byref(s), ctypes.byref(d)), self.ctx.h)
+        return s.value, d.value
+
     def free(self):
         if self.h is not None and self.ctx.h:
             lib().cbh_mat_free(self.ctx.h, self.h)

@@ -228,10 +228,23 @@ int cbh_plan_spgemm_slots(cbh_plan* plan, cbh_semiring sr, int64_t s0, int64_t s
  * (device kernels in combblas_amd/csrc/apps.h)                           */
 /* C = (A*B) .* M in one pass: Applications/TC.cpp:108-110 (Mult_AnXBn_Synch(L, L) then
  * C.EWiseMult(L, false), Friends.h:834-887). Pattern = pattern(A*B) ∩ pattern(M) (explicit zeros
- * count), rows ascending; values SR-sum * M(i,j), or the SR-sum alone with CBH_MASK_PATTERN.   */
+ * count), rows ascending; values SR-sum * M(i,j), or the SR-sum alone with CBH_MASK_PATTERN.
+ * Two evaluation orders, same result: EXPAND enumerates the products of A*B whose rows fall in
+ * the mask column (work = flops of A*B); DOT intersects row i of A (A transposed on the device)
+ * with column j of B for every mask entry (work = sum of the shorter lists) -- TC at scale 24.
+ * Default: DOT when nnz(A) >= 65536, else EXPAND; the flags force one.                         */
 #define CBH_MASK_PATTERN 0x4u
+#define CBH_MASK_EXPAND 0x8u
+#define CBH_MASK_DOT 0x10u
 int cbh_spgemm_masked(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh_mat* B, const cbh_mat* M,
                       uint32_t flags, cbh_mat** C);
+/* AT = A' on the device (SpDCCols::Transpose, SpDCCols.cpp): rows ascending in every column.
+ * A.n < 2^31, nnz(A) < 2^31.                                                                   */
+int cbh_transpose(cbh_ctx* ctx, const cbh_mat* A, cbh_mat** AT);
+/* Value sum and order-sensitive digest of a block, the definition cbh_spgemm_phased's
+ * CBH_PHASE_CHECKSUM and the oracle use: sum over entries p (in DCSC order) of
+ * mix64(p ^ mix64(col ^ mix64(row ^ mix64(value bits)))) mod 2^64. Built-in dtypes only.        */
+int cbh_mat_checksum(cbh_ctx* ctx, const cbh_mat* M, double* value_sum, uint64_t* digest);
 /* C = A .* B (SpParMat::EWiseMult(B, false) -> Friends.h:834-887): intersection, values A*B. */
 int cbh_ewise_mult(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, cbh_mat** C);
 /* HipMCL column operations on f64 blocks (ParFriends.h:185-353). Vectors are device arrays over

@@ -37,8 +37,9 @@ static_assert(kChunkMin <= TSymSmall::EMAX && kChunkMin <= TSymLarge::EMAX && kC
                   kChunkMin <= TNumLarge::EMAX,
               "every chunked task needs HBM cursor state");
 
-// Launches task_kernel<SR, CFG, MODE> over order[first, first+count) on `stream` (grid slices of
-// at most 2^30 workgroups). The dynamic-LDS attribute is set once per instantiation.
+// Launches task_kernel<SR, CFG, MODE> over order[first, first+count) on `stream`, in grid slices
+// of fewer than 2^32 work-items (an AQL dispatch counts work-items in 32 bits). The dynamic-LDS
+// attribute is set once per instantiation.
 template <class SR, class CFG, int MODE, bool MERGE = false>
 hipError_t launch_tasks(const TaskArgs& args, int64_t first, int64_t count, hipStream_t stream) {
   if (count <= 0) return hipSuccess;
@@ -51,7 +52,7 @@ hipError_t launch_tasks(const TaskArgs& args, int64_t first, int64_t count, hipS
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  const int64_t kMaxGrid = 1ll << 30;
+  const int64_t kMaxGrid = ((1ll << 32) - 1) / CFG::BS;
   for (int64_t off = 0; off < count; off += kMaxGrid) {
     const int64_t n = std::min(kMaxGrid, count - off);
     TaskArgs b = args;

@@ -16,7 +16,7 @@
 // (segment starts + block max-scan) names the entry.
 //
 //   symbolic (MODE_TSYM): distinct rows of the task -> cnt[task]        [estimateNNZ_Hash, mtSpGEMM.h:806-933]
-//            sub-tile = an LDS bitmap over 32*T rows (exact, no hashing) or, for sparse ranges,
+//            sub-tile = an LDS bitmap over 32*TA rows (exact, no hashing) or, for sparse ranges,
 //            an LDS key hash of <= T/2 products -- whichever needs fewer sub-tiles.
 //   offsets : exclusive scan of cnt over tasks (a column's tasks are consecutive, in row order),
 //             so every task knows where its outputs go and C's column pointers fall out.
@@ -38,6 +38,7 @@ constexpr int32_t kNoRow = 0x7fffffff;
 // cursor row not loaded yet (< every row range: the entry counts as active, and its first
 // segment search starts AT the cursor, whose row the search loads with the following ones)
 constexpr int32_t kUnknownRow = -2;
+constexpr int kSymWords = 13312;  // bitmap words of the large symbolic configuration (see TaskCfg::TA)
 constexpr int kFill8 = 4;  // numeric sub-tile: planned outputs, in eighths of the T home slots
 // dense sub-tiles of one window keep their products in registers between the bitmap and the value
 // pass (else the value pass gathers them again)
@@ -243,8 +244,11 @@ __device__ __forceinline__ int block_excl_sum(int v, int* red, int& total) {
 
 // Numeric task plan shared by the binning (host launch) and the kernel: a task runs DENSE when a
 // bitmap over each sub-tile's rows fits the NWB LDS words and the sub-tiles it then needs (at
-// most 15/16 of CAPD outputs each) are not more than 5/4 of the hash sub-tiles (T/2 outputs).
-// Returns the dense sub-tile count, or 0 when the task stays on the hash.
+// most 15/16 of CAPD outputs each) are not more than CBH_DENSE_RATIO/4 of the hash sub-tiles
+// (T/2 outputs). Returns the dense sub-tile count, or 0 when the task stays on the hash.
+#ifndef CBH_DENSE_RATIO
+#define CBH_DENSE_RATIO 5
+#endif
 __host__ __device__ inline int64_t dense_subtiles(int64_t work, int64_t span, int64_t T, int64_t capd, int64_t nwb) {
   if (work <= 0 || span <= 0) return 0;
   const int64_t cap = T / 2;
@@ -253,7 +257,7 @@ __host__ __device__ inline int64_t dense_subtiles(int64_t work, int64_t span, in
   int64_t Rd = (work + cd - 1) / cd;
   const int64_t Rw = (span + 32 * nwb - 1) / (32 * nwb);
   Rd = Rd > Rw ? Rd : Rw;
-  return Rd <= R + R / 4 ? Rd : 0;
+  return 4 * Rd <= CBH_DENSE_RATIO * R ? Rd : 0;
 }
 
 template <class SR, int T, int BS, int EMAX, int U, int MODE>
@@ -264,15 +268,12 @@ struct TaskCfg {
   using acc_t = typename SR::acc_t;
   using a_t = typename sr_a_type<SR>::type;  // A's values (NT1)
   using b_t = typename sr_b_type<SR>::type;  // B's values (NT2)
-  static constexpr int TA = NUM ? T + kGuard : T;  // slots (symbolic: 32-bit words, keys or bitmap)
+  // slots (symbolic: 32-bit words, a key hash over the first T or a bitmap over all TA). The large
+  // symbolic configuration fills two workgroups' share of LDS with bitmap words: 13312 words =
+  // 426 K rows per sub-tile instead of 262 K, so fewer sub-tiles re-scan a column's entries
+  static constexpr int TA = NUM ? T + kGuard : (T >= 8192 && BS >= 512 ? kSymWords : T);
   static constexpr int NW = BS / 64;
   static constexpr int WIN = U * BS;
-  // dense numeric sub-tiles: CAPD outputs (keys + values at the front of the two tables); the
-  // rest of the key table holds the bitmap (NWB words), the rest of the value table the int16
-  // prefix popcounts of the words
-  static constexpr int CAPD = T / 2;
-  static constexpr int NWB = TA - CAPD;
-  static_assert(!DENSE || (TA - CAPD) * sizeof(acc_t) >= 2 * (size_t)NWB, "dense prefix array fits");
   // owner map entries are entry indices (< EMAX): 16 bits leave LDS room for larger windows
   using own_t = int16_t;
   static_assert(EMAX < 32768, "owner map entries are 16-bit");
@@ -280,6 +281,15 @@ struct TaskCfg {
   static constexpr size_t o_keys = 0;
   static constexpr size_t o_vals = al(o_keys + sizeof(int32_t) * TA);
   static constexpr size_t o_pos = al(o_vals + (NUM ? sizeof(acc_t) * TA : 0));
+  // dense numeric sub-tiles (MODE_TDENSE) lay the two tables out differently: CAPD output rows,
+  // CAPD values, then the rest of both tables is the bitmap (NWB words) followed by the int16
+  // prefix popcount of every word -- 32*NWB rows per sub-tile (135 K for T = 4096 with f64)
+  static constexpr int CAPD = T / 2;
+  static constexpr size_t o_dvals = al(o_keys + sizeof(int32_t) * CAPD);
+  static constexpr size_t o_dbits = al(o_dvals + sizeof(acc_t) * CAPD);
+  static constexpr int NWB = NUM ? (int)((o_pos - o_dbits) / 6) / 8 * 8 : 0;
+  static constexpr size_t o_dpre = al(o_dbits + sizeof(uint32_t) * NWB);
+  static_assert(!DENSE || o_dpre + sizeof(int16_t) * NWB <= o_pos, "dense bitmap and prefix fit the tables");
   static constexpr size_t o_end = al(o_pos + sizeof(int64_t) * EMAX);
   static constexpr size_t o_scale = al(o_end + sizeof(int64_t) * EMAX);
   static constexpr size_t o_next = al(o_scale + (NUM ? sizeof(b_t) * EMAX : 0));
@@ -312,7 +322,7 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int32_t* keys = reinterpret_cast<int32_t*>(smem + C::o_keys);
   uint32_t* words = reinterpret_cast<uint32_t*>(smem + C::o_keys);
-  acc_t* vals = reinterpret_cast<acc_t*>(smem + C::o_vals);
+  acc_t* vals = reinterpret_cast<acc_t*>(smem + (C::DENSE ? C::o_dvals : C::o_vals));
   // epos: cursor (absolute index into A); between the segment scan and the end of the sub-tile
   // it holds cursor - exclusive offset (the gather base of the entry's products)
   int64_t* epos = reinterpret_cast<int64_t*>(smem + C::o_pos);
@@ -366,7 +376,7 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
     constexpr int64_t cap = NUM ? (int64_t)T * kFill8 / 8 : T / 2;  // outputs (keys) per sub-tile
     R = (work + cap - 1) / cap;
     if constexpr (!NUM) {
-      const int64_t Rb = (span + 32ll * T - 1) / (32ll * T);
+      const int64_t Rb = (span + 32ll * TA - 1) / (32ll * TA);
       if (Rb <= R) {
         bitmap = true;
         R = Rb;
@@ -555,11 +565,11 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
   if (!chunked) {
     load_entries(0, (int)ne, tlo, thi, (full & 1) != 0, false);
   }
-  uint32_t* dwords = words;  // dense: bitmap words past the CAPD keys; int16 prefix past CAPD vals
+  uint32_t* dwords = words;  // dense: bitmap words and their int16 prefix past the CAPD keys and values
   int16_t* dpre = nullptr;
   if constexpr (NUM) {
-    dwords = reinterpret_cast<uint32_t*>(smem + C::o_keys + sizeof(int32_t) * C::CAPD);
-    dpre = reinterpret_cast<int16_t*>(smem + C::o_vals + sizeof(acc_t) * C::CAPD);
+    dwords = reinterpret_cast<uint32_t*>(smem + C::o_dbits);
+    dpre = reinterpret_cast<int16_t*>(smem + C::o_dpre);
     if constexpr (dense)  // dense accumulators start at the identity; every commit resets what it read
       for (int s = tid; s < C::CAPD; s += BS) vals[s] = SR::identity();
   }
@@ -586,7 +596,7 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
     } else if constexpr (dense) {
       for (int s = tid; s < nwd; s += BS) dwords[s] = 0u;
     } else {
-      for (int s = tid; s < TA; s += BS) {
+      for (int s = tid; s < (NUM ? TA : T); s += BS) {
         keys[s] = kEmpty;
         if constexpr (NUM && !LOCKED) vals[s] = SR::identity();
       }

@@ -36,18 +36,90 @@ def _host(S):
     return H.Dcsc(h.m, h.n, h.jc, h.cp, h.ir, h.num)
 
 
+@pytest.mark.parametrize("method", ["expand", "dot"])
 @pytest.mark.parametrize("scale", [8, 10])
-def test_tc_masked_vs_reference(ctx, apps, apps_meta, scale):
+def test_tc_masked_vs_reference(ctx, apps, apps_meta, scale, method):
     from combblas_amd.apps import MaskedSpGEMM, TriangleCount
     from combblas_amd.semirings import PlusTimesSRing
 
     L = apps[f"tc{scale}_L"]  # the reference's L: upper entries kept as explicit zeros (TC.cpp:98-104)
     dL, dL2 = _dev(ctx, L), _dev(ctx, L)
-    C = MaskedSpGEMM(PlusTimesSRing, dL, dL2, dL)
-    H.assert_dcsc_equal(_host(C), apps[f"tc{scale}_C"], msg=f"(L*L).*L scale {scale}")
-    assert TriangleCount(dL, dL2) == apps_meta["tc"][str(scale)]["triangles"]
+    C = MaskedSpGEMM(PlusTimesSRing, dL, dL2, dL, method=method)
+    H.assert_dcsc_equal(_host(C), apps[f"tc{scale}_C"], msg=f"(L*L).*L scale {scale} {method}")
+    assert TriangleCount(dL, dL2, method=method) == apps_meta["tc"][str(scale)]["triangles"]
     for S in (C, dL, dL2):
         S.free()
+
+
+@pytest.mark.parametrize("scale,method", [(12, "expand"), (12, "dot"), (14, "dot"), (16, "dot")])
+def test_tc_device_lower_vs_reference_digest(ctx, scale, method):
+    """TC.cpp's whole flow on the device (TCLower: R-MAT -> L; masked (L*L).*L) against the
+    reference's C at scales 12-16 (tests/golden/tc.json: nnz, nonzero columns, value sum =
+    triangles, order-sensitive digest)"""
+    import json
+
+    from combblas_amd.apps import MaskedSpGEMM, TCLower
+    from combblas_amd.semirings import PlusTimesSRing
+
+    with open(os.path.join(H.GOLDEN, "tc.json")) as f:
+        ref = json.load(f)["scales"][str(scale)]
+    L = TCLower(ctx, scale)
+    assert L.nnz == ref["nnzL"]
+    L2 = TCLower(ctx, scale)
+    C = MaskedSpGEMM(PlusTimesSRing, L, L2, L, method=method)
+    c = _host(C)
+    vs, dg = H.digest(c)
+    assert (c.nnz, c.nzc) == (ref["nnzC"], ref["nzcC"])
+    assert int(c.num.sum()) == ref["triangles"] and vs == ref["sumC"] and dg == int(ref["digestC"])
+    for S in (C, L, L2):
+        S.free()
+
+
+@pytest.mark.parametrize("tag", ["pt_i64", "pt_f64", "max_i64", "min_i64", "bool"])
+@pytest.mark.parametrize("pattern", [False, True])
+def test_masked_dot_vs_oracle(ctx, oracle, tag, pattern):
+    """the dot form on a rectangular product with long rows of A and long columns of B (pieces of
+    the wave kernel), every semiring, explicit zeros, empty mask columns"""
+    from combblas_amd.apps import MaskedSpGEMM
+    from combblas_amd.semirings import ALL
+
+    rng = np.random.default_rng(17)
+
+    def vals(n):
+        v = rng.integers(-3, 4, n)
+        return {"pt_f64": v / 4.0, "bool": (v != 0).astype(np.uint8)}.get(tag, v.astype(np.int64))
+
+    def with_lines(d, rows, cols):
+        c0, r0, _ = d.to_coo_sorted()
+        key = np.unique(np.concatenate([c0, cols]) * d.m + np.concatenate([r0, rows]))
+        return H.Dcsc.from_coo(d.m, d.n, key % d.m, key // d.m, vals(key.size))
+
+    # two dense rows of A and a dense column of B: shorter lists above the 2048-element piece
+    a = with_lines(H.random_dcsc(rng, 300, 9000, 0.02), np.r_[np.full(9000, 7), np.full(9000, 123)],
+                   np.r_[np.arange(9000), np.arange(9000)])
+    b = with_lines(H.random_dcsc(rng, 9000, 200, 0.02), np.arange(0, 9000, 2), np.full(4500, 11))
+    M = H.with_explicit_zeros(H.random_dcsc(rng, a.m, b.n, 0.1, dtype=a.num.dtype, empty_cols=0.3))
+    sr = {"pt_i64": "plus_times", "pt_f64": "plus_times", "max_i64": "select_max", "min_i64": "min_plus",
+          "bool": "or_and"}[tag]
+    SR = ALL[{"pt_i64": "PlusTimesSRing", "pt_f64": "PlusTimesSRing", "max_i64": "SelectMaxSRing",
+              "min_i64": "MinPlusSRing", "bool": "OrAndSRing"}[tag]]
+    mask = H.Dcsc(M.m, M.n, M.jc, M.cp, M.ir, np.ones(M.nnz, a.num.dtype)) if pattern else M
+    exp = AO.ewise_mult(oracle.spgemm(a, b, sr, "hybrid"), mask)
+    dA, dB, dM = _dev(ctx, a), _dev(ctx, b), _dev(ctx, M)
+    C = MaskedSpGEMM(SR, dA, dB, dM, pattern=pattern, method="dot")
+    H.assert_dcsc_equal(_host(C), exp, rtol=1e-12 if tag == "pt_f64" else 0.0, msg=f"masked dot {tag}")
+    for S in (C, dA, dB, dM):
+        S.free()
+
+
+def test_transpose_vs_host(ctx):
+    from combblas_amd.apps import Transpose
+
+    rng = np.random.default_rng(4)
+    a = H.random_dcsc(rng, 333, 217, 0.05, dtype=np.float64, empty_cols=0.2)
+    T = _host(Transpose(_dev(ctx, a)))
+    c, r, v = a.to_coo_sorted()
+    H.assert_dcsc_equal(T, H.Dcsc.from_coo(a.n, a.m, c, r, v), msg="transpose")
 
 
 def test_tc_known_answer_scale10(ctx, apps):
