@@ -1497,16 +1497,29 @@ int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh
     CBH_HIP(ctx, hipMemcpyAsync(hcp.data(), P.Ccp, sizeof(int64_t) * (P.nzcB + 1), hipMemcpyDeviceToHost, ctx->stream));
     CBH_HIP(ctx, hipMemcpyAsync(hts.data(), P.tstart, sizeof(int64_t) * (P.nzcB + 1), hipMemcpyDeviceToHost, ctx->stream));
     CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    std::vector<int64_t> cuts{0};
     int64_t maxcol = 0;
     for (int64_t c = 0; c < P.nzcB; ++c) maxcol = std::max(maxcol, hcp[c + 1] - hcp[c]);
     budget = std::max(budget, maxcol);
-    while (cuts.back() < P.nzcB) {
-      const int64_t c0 = cuts.back();
-      const int64_t lim = hcp[c0] + budget;
-      int64_t c1 = (int64_t)(std::upper_bound(hcp.begin() + c0 + 1, hcp.end(), lim) - hcp.begin()) - 1;
-      if (c1 <= c0) c1 = c0 + 1;
-      cuts.push_back(c1);
+    auto cut_with = [&](int64_t bud) {
+      std::vector<int64_t> cs{0};
+      while (cs.back() < P.nzcB) {
+        const int64_t c0 = cs.back();
+        const int64_t lim = hcp[c0] + bud;
+        int64_t c1 = (int64_t)(std::upper_bound(hcp.begin() + c0 + 1, hcp.end(), lim) - hcp.begin()) - 1;
+        if (c1 <= c0) c1 = c0 + 1;
+        cs.push_back(c1);
+      }
+      return cs;
+    };
+    std::vector<int64_t> cuts = cut_with(budget);
+    // balance: the greedy cuts leave a short last phase that pays its own launch tails; the same
+    // number of phases at an even share of the entries (plus the widest column of slack) is kept
+    // when it needs no more phases
+    if (cuts.size() > 2) {
+      const int64_t np = (int64_t)cuts.size() - 1;
+      const int64_t even = std::min(budget, (P.total_nnz + np - 1) / np + maxcol);
+      std::vector<int64_t> bal = cut_with(even);
+      if (bal.size() == cuts.size()) cuts.swap(bal);
     }
     const int64_t maxphase = [&] {
       int64_t mx = 0;
