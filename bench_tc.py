@@ -63,6 +63,37 @@ def host_check(L, C, ncols, seed=7):
     return int(cols.size), bad
 
 
+def cpu_baseline(scale):
+    """the reference's own TC flow (oracle/_ref/ref_harness tc: Mult_AnXBn_Synch(L, L), EWiseMult,
+    Reduce; TC.cpp:108-115) on this host's cores at a scale it finishes (its unmasked L*L runs
+    out of memory from scale 18 on a 64 GB host); reported as its reference-equivalent GFLOP/s"""
+    import subprocess
+
+    import combblas_amd as cb
+
+    ref = os.path.join(HERE, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(ref):
+        return None
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    env = dict(os.environ, OMP_NUM_THREADS=str(cores), LD_LIBRARY_PATH="/usr/lib/x86_64-linux-gnu:/opt/conda/lib")
+    r = subprocess.run([ref, "tc", str(scale), "-", "-"], env=env, cwd="/tmp", capture_output=True, text=True,
+                       timeout=900)
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode != 0 or not line:
+        return None
+    d = json.loads(line[-1])
+    src, dst = cb.rmat_edges(scale)
+    keep = src != dst
+    key = np.unique(np.concatenate([src[keep] << scale | dst[keep], dst[keep] << scale | src[keep]]))
+    deg = np.bincount(key & ((1 << scale) - 1), minlength=1 << scale).astype(np.int64)
+    flops = int((deg * deg).sum())
+    return {"value": round(2.0 * flops / d["tc_s"] / 1e9, 6), "unit": "GFLOP/s", "cores": d["threads"],
+            "kind": "reference",
+            "sample": f"TC.cpp's flow at R-MAT scale {scale} (Mult_AnXBn_Synch(L, L) + EWiseMult + Reduce, 1 rank x "
+                      f"{d['threads']} threads, oracle/_ref built from the reference sources): {d['tc_s']:.3f} s for "
+                      f"{flops} unmasked products, triangles {d['triangles']}"}
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--scale", type=int, default=24)
@@ -70,6 +101,8 @@ def main():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--check-cols", type=int, default=200)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-scale", type=int, default=16, help="scale of the reference CPU run")
     args = p.parse_args()
     import torch
 
@@ -120,6 +153,7 @@ def main():
            "config": {"workload": f"tc_rmat{args.scale}_ef{args.edgefactor}_masked_LxL_PlusTimes_i64",
                       "scale": args.scale, "nnzL": L.nnz, "flops_unmasked": flops, "probes": probes,
                       "probes_per_s": round(probes / dt, 1), "method": "dot"},
+           "cpu_baseline": None if args.no_cpu_baseline else cpu_baseline(args.cpu_scale),
            "check": {"triangles": tri, "nnzC": C.nnz, "value_sum": vsum, "digest": str(dig),
                      "sampled_columns": checked, "sampled_mismatches": bad, "ok": bad == 0 and vsum == tri}}
     print(json.dumps(out), flush=True)

@@ -22,6 +22,7 @@
 //                                                     MCLPruneRecoverySelect (ParFriends.h:185-353)
 // sr: pt_f64 | pt_i64 | max_i64 | min_i64 | bool ; kernel: hybrid | hash | hashu | heap
 #include <mpi.h>
+#include <omp.h>
 
 #include <algorithm>
 #include <chrono>
@@ -350,14 +351,19 @@ static int do_tc(int scale, const std::string& fl, const std::string& fc) {
     for (auto nzit = L.seq().begnz(colit); nzit != L.seq().endnz(colit); ++nzit)
       if (nzit.rowid() < colit.colid()) nzit.value() = 0;
   Mat Lt = L;
+  // TC.cpp:108-115 timed: the product, the mask and the reduction (the CPU baseline of bench_tc.py)
+  MPI_Barrier(MPI_COMM_WORLD);
+  const double t0 = MPI_Wtime();
   Mat C = Mult_AnXBn_Synch<PlusTimesSRing<int64_t, int64_t>, int64_t, SpDCCols<int64_t, int64_t>>(L, Lt);
   C.EWiseMult(L, false);
   FullyDistVec<int64_t, int64_t> tri = C.Reduce(Column, std::plus<int64_t>(), static_cast<int64_t>(0));
   const int64_t result = tri.Reduce(std::plus<int64_t>(), static_cast<int64_t>(0));
-  cbm::write(fl, from_spdccols<int64_t>(L.seq()));
-  cbm::write(fc, from_spdccols<int64_t>(C.seq()));
-  std::printf("{\"triangles\": %lld, \"nnzL\": %lld, \"nnzC\": %lld}\n", (long long)result, (long long)L.getnnz(),
-              (long long)C.getnnz());
+  MPI_Barrier(MPI_COMM_WORLD);
+  const double tc_s = MPI_Wtime() - t0;
+  if (!fl.empty() && fl != "-") cbm::write(fl, from_spdccols<int64_t>(L.seq()));
+  if (!fc.empty() && fc != "-") cbm::write(fc, from_spdccols<int64_t>(C.seq()));
+  std::printf("{\"triangles\": %lld, \"nnzL\": %lld, \"nnzC\": %lld, \"tc_s\": %.6f, \"threads\": %d}\n",
+              (long long)result, (long long)L.getnnz(), (long long)C.getnnz(), tc_s, omp_get_max_threads());
   delete A;
   return 0;
 }
