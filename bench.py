@@ -33,8 +33,11 @@ sys.path.insert(0, HERE)
 
 METRIC = "semiring GFLOP/s for R-MAT A² SpGEMM at 1/2/4/8 GPUs; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
-DOMINANT = "num_large"
-DOMINANT_KERNEL = "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 8, 1, false>"
+# the task kernels of one product (bench kernel kinds -> rocprof names); the roofline line reports
+# the one with the most time per step
+KERNELS = {"num_large": "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 8, 1, false>",
+           "num_dense": "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 8, 2, false>",
+           "sym_large": "cbh::task_kernel<cbh::PlusTimesD<long>, 8192, 512, 512, 8, 0, false>"}
 
 
 _T0 = time.perf_counter()
@@ -355,18 +358,24 @@ def main():
     nnzC = allreduce(float(st["nnz"]), dist.ReduceOp.SUM if world > 1 else None)
     value = 2.0 * flops / step_s / 1e9
 
-    k = ks[DOMINANT]
-    achieved = (k["alg_bytes"] / (k["ms"] / 1e3) / 1e9) if k["ms"] > 0 else 0.0
+    def kernel_roof(kind):
+        k = ks[kind]
+        a = (k["alg_bytes"] / (k["ms"] / 1e3) / 1e9) if k["ms"] > 0 else 0.0
+        return k, a
+
+    dominant = max(KERNELS, key=lambda kind: ks[kind]["ms"])
+    k, achieved = kernel_roof(dominant)
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": DOMINANT_KERNEL, "launches": k["launches"],
+                "kernel": KERNELS[dominant], "launches": k["launches"],
                 "avg_launch_ms": round(k["ms"] / max(k["launches"], 1), 4),
-                "alg_bytes_per_launch": round(k["alg_bytes"] / max(k["launches"], 1))}
-    pmc = os.path.join(HERE, "profiles", "pmc_num_large.json")
+                "alg_bytes_per_launch": round(k["alg_bytes"] / max(k["launches"], 1)),
+                "others": {kind: round(kernel_roof(kind)[1] / HBM_PEAK_GBS, 4) for kind in KERNELS if kind != dominant}}
+    pmc = os.path.join(HERE, "profiles", f"pmc_{dominant}.json")
     if os.path.exists(pmc):  # PMC passes of the same kernel (tools/pmc_traffic.py); stale files are ignored
         try:
             p = json.load(open(pmc))
-            if p.get("kernel") == DOMINANT_KERNEL:
+            if p.get("kernel") == KERNELS[dominant]:
                 roofline["traffic"] = p.get("hbm_bytes_per_launch")
                 roofline["traffic_note"] = (f"HBM bytes per launch from rocprofv3 PMC (2xFETCH_SIZE+WRITE_SIZE, gfx950 "
                                             f"correction; raw {p.get('hbm_bytes_per_launch_raw')}), {p.get('source')}")

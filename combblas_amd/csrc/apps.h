@@ -157,6 +157,7 @@ __global__ __launch_bounds__(BS) void masked_kernel(MaskArgs a) {
 // long (pieces of kDotPiece elements, one wave per piece, partials reduced in piece order).
 constexpr int kDotThread = 64;   // shorter list <= this: one thread per entry
 constexpr int kDotPiece = 2048;  // long entries: elements of the shorter list per wave piece
+constexpr int kDotMergeRatio = 8;  // long entries: merge when longer <= 8 x shorter, else binary search
 
 struct DotArgs {
   const int64_t* ATd;  // AT dense column pointers (A.m + 1): row i of A = AT(:, i), rows = k
@@ -286,9 +287,10 @@ __global__ __launch_bounds__(256) void dot_items_kernel(const int64_t* __restric
     for (int64_t y = poff[x] + lane; y < poff[x + 1]; y += 64) item_entry[y] = (int32_t)x;
 }
 
-// piece y of a long entry (one wave): lanes take 64 consecutive elements of the shorter list at a
-// time and binary-search them in the longer one (bounded below by the previous batch's last
-// position); the lane partials are folded in lane order into the piece's partial
+// piece y of a long entry (one wave): a merge of the two lists when their lengths are within
+// kDotMergeRatio, else lanes take 64 consecutive elements of the shorter list at a time and
+// binary-search them in the longer one (bounded below by the previous batch's last position); the
+// lane partials are folded in lane order into the piece's partial
 template <class SR>
 __device__ __forceinline__ void dot_piece(const DotArgs& a, const int32_t* __restrict__ llong,
                                           const int64_t* __restrict__ poff, const int32_t* __restrict__ item_entry,
@@ -313,21 +315,61 @@ __device__ __forceinline__ void dot_piece(const DotArgs& a, const int32_t* __res
   const int64_t hi = a_short ? b1 : a1;
   val_t acc{};
   bool hit = false;
-  for (int64_t base = s0; base < s1 && lo < hi; base += 64) {
-    const int64_t s = base + lane;
-    int64_t q = hi;
-    if (s < s1) {
-      const int32_t k = srow[s];
-      q = lb_rows64(lrow, lo, hi, k);
-      if (q < hi && lrow[q] == k) {
-        const val_t pr = a_short ? SR::multiply(av[s], bv[q]) : SR::multiply(av[q], bv[s]);
-        acc = hit ? SR::add(acc, pr) : pr;
-        hit = true;
+  if ((hi - lo) <= kDotMergeRatio * (s1e - (a_short ? a0 : b0))) {
+    // comparable lengths: merge. The wave walks this piece of the shorter list and the longer
+    // list in chunks of 64 (coalesced loads); every undecided element not above the longer
+    // chunk's last value is looked up among its 64 values by a shuffle binary search; the
+    // shorter chunk advances once all its elements are decided, else the longer one does.
+    // (Measured at scale 24: 8.1 s; loading 3 chunks ahead 8.8 s; staging 1024-element blocks
+    // in LDS with lockstep LDS searches 11.3 s.)
+    int64_t lp = lb_rows64(lrow, lo, hi, srow[s0]);
+    int64_t sp = s0;
+    int32_t sv = sp + lane < s1 ? srow[sp + lane] : kNoRow;
+    bool und = sp + lane < s1;
+    while (sp < s1 && lp < hi) {
+      const int32_t lv = lp + lane < hi ? lrow[lp + lane] : kNoRow;
+      const int32_t lmax = __shfl(lv, 63);
+      int pos = 0;
+#pragma unroll
+      for (int st = 32; st >= 1; st >>= 1)
+        if (__shfl(lv, pos + st - 1) < sv) pos += st;
+      const int32_t at = __shfl(lv, pos & 63);
+      if (und && sv <= lmax) {
+        und = false;
+        if (pos < 64 && at == sv) {
+          const int64_t s = sp + lane, q = lp + pos;
+          const val_t pr = a_short ? SR::multiply(av[s], bv[q]) : SR::multiply(av[q], bv[s]);
+          acc = hit ? SR::add(acc, pr) : pr;
+          hit = true;
+        }
+      }
+      if (__ballot(und) == 0ull) {
+        sp += 64;
+        und = sp + lane < s1;
+        sv = und ? srow[sp + lane] : kNoRow;
+      } else {
+        lp += 64;
       }
     }
-    // the next batch's keys are larger than every key of this one
-    const int last = (s1 - base) < 64 ? (int)(s1 - base) - 1 : 63;
-    lo = __shfl(q, last);
+  } else {
+    // much longer other list: every element binary-searches it (an interpolation start measured
+    // slower: 9.7 vs 8.1 s at scale 24 -- the bisection's first levels are shared L2 hits)
+    for (int64_t base = s0; base < s1 && lo < hi; base += 64) {
+      const int64_t s = base + lane;
+      int64_t q = hi;
+      if (s < s1) {
+        const int32_t k = srow[s];
+        q = lb_rows64(lrow, lo, hi, k);
+        if (q < hi && lrow[q] == k) {
+          const val_t pr = a_short ? SR::multiply(av[s], bv[q]) : SR::multiply(av[q], bv[s]);
+          acc = hit ? SR::add(acc, pr) : pr;
+          hit = true;
+        }
+      }
+      // the next batch's keys are larger than every key of this one
+      const int last = (s1 - base) < 64 ? (int)(s1 - base) - 1 : 63;
+      lo = __shfl(q, last);
+    }
   }
   // fold lanes in order: lane l absorbs lane l + d (higher lanes hold larger k)
   for (int d = 1; d < 64; d <<= 1) {

@@ -39,7 +39,10 @@ constexpr int32_t kNoRow = 0x7fffffff;
 // segment search starts AT the cursor, whose row the search loads with the following ones)
 constexpr int32_t kUnknownRow = -2;
 constexpr int kSymWords = 13312;  // bitmap words of the large symbolic configuration (see TaskCfg::TA)
-constexpr int kFill8 = 4;  // numeric sub-tile: planned outputs, in eighths of the T home slots
+#ifndef CBH_FILL8
+#define CBH_FILL8 4
+#endif
+constexpr int kFill8 = CBH_FILL8;  // numeric sub-tile: planned outputs, in eighths of the T home slots
 // dense sub-tiles of one window keep their products in registers between the bitmap and the value
 // pass (else the value pass gathers them again)
 #ifndef CBH_DENSE_CARRY
