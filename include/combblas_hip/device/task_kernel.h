@@ -39,16 +39,9 @@ constexpr int32_t kNoRow = 0x7fffffff;
 // segment search starts AT the cursor, whose row the search loads with the following ones)
 constexpr int32_t kUnknownRow = -2;
 constexpr int kSymWords = 13312;  // bitmap words of the large symbolic configuration (see TaskCfg::TA)
-#ifndef CBH_FILL8
-#define CBH_FILL8 4
-#endif
-constexpr int kFill8 = CBH_FILL8;  // numeric sub-tile: planned outputs, in eighths of the T home slots
-// dense sub-tiles of one window keep their products in registers between the bitmap and the value
-// pass (else the value pass gathers them again)
-#ifndef CBH_DENSE_CARRY
-#define CBH_DENSE_CARRY 0
-#endif
-constexpr bool kDenseCarry = CBH_DENSE_CARRY != 0;
+// numeric sub-tile: planned outputs, in eighths of the T home slots (3/8 and 5/8 measured slower:
+// 97.6 and 93.5 vs 98.6 GFLOP/s at scale 22)
+constexpr int kFill8 = 4;
 
 // Diagnostic build only (-DCBH_STAMPS, libcombblas_hip_stamps.so): thread 0 of every workgroup
 // adds the s_memtime cycles of each kernel phase (delimited by block barriers) into g_stamps.
@@ -247,11 +240,9 @@ __device__ __forceinline__ int block_excl_sum(int v, int* red, int& total) {
 
 // Numeric task plan shared by the binning (host launch) and the kernel: a task runs DENSE when a
 // bitmap over each sub-tile's rows fits the NWB LDS words and the sub-tiles it then needs (at
-// most 15/16 of CAPD outputs each) are not more than CBH_DENSE_RATIO/4 of the hash sub-tiles
-// (T/2 outputs). Returns the dense sub-tile count, or 0 when the task stays on the hash.
-#ifndef CBH_DENSE_RATIO
-#define CBH_DENSE_RATIO 5
-#endif
+// most 15/16 of CAPD outputs each) are not more than 5/4 of the hash sub-tiles (T/2 outputs;
+// 4/4, 8/4 and 12/4 measured slower). Returns the dense sub-tile count, or 0 when the task stays
+// on the hash.
 __host__ __device__ inline int64_t dense_subtiles(int64_t work, int64_t span, int64_t T, int64_t capd, int64_t nwb) {
   if (work <= 0 || span <= 0) return 0;
   const int64_t cap = T / 2;
@@ -260,7 +251,7 @@ __host__ __device__ inline int64_t dense_subtiles(int64_t work, int64_t span, in
   int64_t Rd = (work + cd - 1) / cd;
   const int64_t Rw = (span + 32 * nwb - 1) / (32 * nwb);
   Rd = Rd > Rw ? Rd : Rw;
-  return 4 * Rd <= CBH_DENSE_RATIO * R ? Rd : 0;
+  return 4 * Rd <= 5 * R ? Rd : 0;
 }
 
 template <class SR, int T, int BS, int EMAX, int U, int MODE>
@@ -309,8 +300,9 @@ struct TaskCfg {
 // per-list element offset (all device allocations share one address space, 256-byte aligned),
 // so the sub-tile machinery above runs unchanged and the "product" is the list value itself.
 template <class SR, int T, int BS, int EMAX, int U, int MODE, bool MERGE = false>
-// 512-thread groups: two per CU (LDS-bound), so 4 waves per SIMD -> <= 128 VGPRs
-__global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(TaskArgs a) {
+// 512-thread groups: two per CU (LDS-bound), so 4 waves per SIMD -> <= 128 VGPRs; a 1024-thread
+// group is alone on its CU, same 4 waves per SIMD
+__global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) void task_kernel(TaskArgs a) {
   using C = TaskCfg<SR, T, BS, EMAX, U, MODE>;
   using val_t = typename C::val_t;
   using acc_t = typename C::acc_t;
@@ -522,7 +514,7 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
     for (int i = tid; i < nec; i += BS) epos[i] -= eoff[i];
     return eoff[nec];
   };
-  // products of the sub-tile held in registers between the two dense passes (single window)
+  // the U products of the current window this thread holds
   int32_t r[U];
   val_t av[U];  // numeric: A value * B value (the product), once values are gathered
   // One sweep over the windows of the current entry set: owner map, gather U products per
@@ -609,7 +601,6 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
     __syncthreads();
     CBH_STAMP(1);
 
-    bool single = false;  // dense, one window, products kept in registers for the value pass
     for (int ch = 0; ch < nchunks; ++ch) {
       int nec = (int)ne;
       if (chunked) {
@@ -633,8 +624,7 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
           else atomicOr(&words[d >> 5], 1u << (d & 31));
         });
       } else if constexpr (dense) {
-        single = kDenseCarry && !chunked && P <= WIN;
-        sweep(nec, P, single, [&](int u) {
+        sweep(nec, P, false, [&](int u) {
           const uint32_t d = (uint32_t)(r[u] - lo);
           if (d >= tw) bad |= 1 << 8;
           else atomicOr(&dwords[d >> 5], 1u << (d & 31));
@@ -757,13 +747,10 @@ __global__ __launch_bounds__(BS, BS >= 512 ? 2048 / BS : 4) void task_kernel(Tas
           keys[slot] = r[u];
           SR::lds_acc(&vals[slot], vv);
         };
-        if (single) {
-#pragma unroll
-          for (int u = 0; u < U; ++u)
-            if (tid + u * BS < (int)eoff[ne]) place(u);
-        } else {
+        {
           // value pass over the same products again (second gather, mostly cache hits): the
-          // segments are known -- LDS (one chunk) or the two HBM cursor buffers (chunked)
+          // segments are known -- LDS (one chunk) or the two HBM cursor buffers (chunked). Keeping
+          // one-window sub-tiles' products in registers instead measured slower (96.2 vs 97.7).
           for (int ch = 0; ch < nchunks; ++ch) {
             int nec = (int)ne;
             if (chunked) {
