@@ -89,3 +89,25 @@ def test_galerkin_inputs_and_oracle(apps, oracle):
     AT = oracle.spgemm(A, T, "plus_times", "hybrid")
     SAT = oracle.spgemm(S, AT, "plus_times", "hybrid")
     H.assert_dcsc_equal(SAT, apps["gal_SAT"], msg="SAT")  # dyadic values: exact
+
+
+@pytest.mark.parametrize("nx", [4, 8, 16])
+def test_galerkin_column_order_generators(nx):
+    """the sort-free generators bench_galerkin.py uses at 256^3 build exactly the pinned operators"""
+    from combblas_amd.galerkin import poisson27, poisson27_csc, prolongation, prolongation_csc
+
+    for slow, fast in ((poisson27(nx), poisson27_csc(nx)), (prolongation(nx), prolongation_csc(nx))):
+        H.assert_dcsc_equal(H.Dcsc(fast.m, fast.n, fast.jc, fast.cp, fast.ir, fast.num),
+                            H.Dcsc(slow.m, slow.n, slow.jc, slow.cp, slow.ir, slow.num), msg=f"nx {nx}")
+
+
+def test_galerkin_closed_form_sum(oracle):
+    """sum(R^T A R) = (R 1)^T A (R 1): the size-independent check of the C3 bench line"""
+    from bench_galerkin import closed_form_sum
+    from combblas_amd.galerkin import poisson27_csc, prolongation_csc, transpose
+
+    A, R = poisson27_csc(8), prolongation_csc(8)
+    S = transpose(R)
+    d = lambda h: H.Dcsc(h.m, h.n, h.jc, h.cp, h.ir, h.num)  # noqa: E731
+    SAT = oracle.spgemm(d(S), oracle.spgemm(d(A), d(R), "plus_times", "hybrid"), "plus_times", "hybrid")
+    assert float(SAT.num.sum()) == closed_form_sum(A, R)
