@@ -42,6 +42,10 @@ constexpr int kSymWords = 13312;  // bitmap words of the large symbolic configur
 // numeric sub-tile: planned outputs, in eighths of the T home slots (3/8 and 5/8 measured slower:
 // 97.6 and 93.5 vs 98.6 GFLOP/s at scale 22)
 constexpr int kFill8 = 4;
+// dense numeric sub-tile capacity in quarters of T (build knob for the A/B; 3 = 3072 values)
+#ifndef CBH_CAPD4
+#define CBH_CAPD4 3
+#endif
 
 // Diagnostic build only (-DCBH_STAMPS, libcombblas_hip_stamps.so): thread 0 of every workgroup
 // adds the s_memtime cycles of each kernel phase (delimited by block barriers) into g_stamps.
@@ -275,11 +279,12 @@ struct TaskCfg {
   static constexpr size_t o_keys = 0;
   static constexpr size_t o_vals = al(o_keys + sizeof(int32_t) * TA);
   static constexpr size_t o_pos = al(o_vals + (NUM ? sizeof(acc_t) * TA : 0));
-  // dense numeric sub-tiles (MODE_TDENSE) lay the two tables out differently: CAPD output rows,
-  // CAPD values, then the rest of both tables is the bitmap (NWB words) followed by the int16
-  // prefix popcount of every word -- 32*NWB rows per sub-tile (135 K for T = 4096 with f64)
-  static constexpr int CAPD = T / 2;
-  static constexpr size_t o_dvals = al(o_keys + sizeof(int32_t) * CAPD);
+  // dense numeric sub-tiles (MODE_TDENSE) lay the two tables out differently: CAPD values (the
+  // output rows are not stored: the commit reads them off the bitmap), then the rest of both
+  // tables is the bitmap (NWB words) followed by the int16 prefix popcount of every word --
+  // 32*NWB rows per sub-tile (CAPD 3072 and 135 K rows for T = 4096 with f64)
+  static constexpr int CAPD = T / 4 * CBH_CAPD4;
+  static constexpr size_t o_dvals = o_keys;
   static constexpr size_t o_dbits = al(o_dvals + sizeof(acc_t) * CAPD);
   static constexpr int NWB = NUM ? (int)((o_pos - o_dbits) / 6) / 8 * 8 : 0;
   static constexpr size_t o_dpre = al(o_dbits + sizeof(uint32_t) * NWB);
@@ -560,7 +565,7 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
   if (!chunked) {
     load_entries(0, (int)ne, tlo, thi, (full & 1) != 0, false);
   }
-  uint32_t* dwords = words;  // dense: bitmap words and their int16 prefix past the CAPD keys and values
+  uint32_t* dwords = words;  // dense: bitmap words and their int16 prefix past the CAPD values
   int16_t* dpre = nullptr;
   if constexpr (NUM) {
     dwords = reinterpret_cast<uint32_t*>(smem + C::o_dbits);
@@ -744,7 +749,6 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
           if (d >= tw) return;
           const uint32_t wv = dwords[d >> 5];
           const int slot = dpre[d >> 5] + __popc(wv & ((1u << (d & 31)) - 1u));
-          keys[slot] = r[u];
           SR::lds_acc(&vals[slot], vv);
         };
         {
@@ -801,16 +805,23 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
     if (!NUM && bitmap) {
       for (int s = tid; s < nwd; s += BS) my_count += __popc(words[s]);
     } else if constexpr (dense) {
-      if constexpr (NUM) {  // outputs are already in row order: straight copy
-        for (int i = tid; i < dtotal; i += BS) {
-          const int64_t pos = out_pos + i;
-          if (pos >= out_end || pos >= a.ccap) {
-            bad |= 1 << 5;
-          } else {
-            a.Cir[pos] = keys[i];
-            reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(vals[i]);
+      if constexpr (NUM) {  // values are already in row order; word x's set bits are ranks dpre[x]..
+        for (int x = tid; x < nwd; x += BS) {
+          uint32_t wv = dwords[x];
+          int rk = dpre[x];
+          while (wv) {
+            const int b = __builtin_ctz(wv);
+            wv &= wv - 1u;
+            const int64_t pos = out_pos + rk;
+            if (pos >= out_end || pos >= a.ccap) {
+              bad |= 1 << 5;
+            } else {
+              a.Cir[pos] = lo + 32 * x + b;
+              reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(vals[rk]);
+            }
+            vals[rk] = SR::identity();
+            ++rk;
           }
-          vals[i] = SR::identity();
         }
         out_pos += dtotal;
       }

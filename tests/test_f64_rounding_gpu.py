@@ -1,0 +1,66 @@
+"""f64 rounding of the device accumulation, stated and bounded (PlusTimes<double> with
+non-dyadic values). The device kernels add the products of an output entry with LDS atomics, in
+arrival order, and long columns are split into sub-tiles/chunks -- so the summation order is not
+the reference's (mtSpGEMM.h:401-416 adds in B's entry order) and may differ between runs. What
+every order guarantees is the standard recursive-summation bound: for an entry with k products,
+    |fl(sum) - sum| <= gamma_{k-1} * sum |a_ik * b_kj|,   gamma_m = m*eps / (1 - m*eps),
+so any two orders (two device runs, or device vs the CPU oracle) differ by at most twice that.
+These tests check exactly that bound on every entry, with the structure bit-exact, on an R-MAT
+pattern whose hub columns exercise the hash, dense and chunked (ne > 512) task paths."""
+import numpy as np
+import pytest
+
+import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+EPS = np.finfo(np.float64).eps
+
+
+def _operand(scale, seed):
+    import combblas_amd as cb
+
+    A = cb.rmat(scale, 16, dtype=np.float64)
+    rng = np.random.default_rng(seed)
+    num = rng.uniform(-1.0, 1.0, A.nnz) * 3.0 ** rng.integers(-8, 9, A.nnz)  # non-dyadic, mixed signs
+    return H.Dcsc(A.m, A.n, A.jc, A.cp, A.ir, num)
+
+
+def _with(d, num):
+    return H.Dcsc(d.m, d.n, d.jc, d.cp, d.ir, num)
+
+
+def _bound(oracle, A, B):
+    """per-entry 2 * gamma_{k-1} * sum |a b| (in the oracle's output order)"""
+    absC = oracle.spgemm(_with(A, np.abs(A.num)), _with(B, np.abs(B.num)), "plus_times", "hybrid", threads=8)
+    cnt = oracle.spgemm(_with(A, np.ones_like(A.num)), _with(B, np.ones_like(B.num)), "plus_times", "hybrid", threads=8)
+    m = np.maximum(cnt.num - 1.0, 0.0)
+    gamma = m * EPS / (1.0 - m * EPS)
+    return 2.0 * gamma * absC.num * (1.0 + 4 * EPS)
+
+
+@pytest.mark.parametrize("scale", [13, 15])
+def test_f64_rounding_within_summation_bound(ctx, oracle, scale):
+    import combblas_amd as cb
+
+    A = _operand(scale, 5 + scale)
+    hA = cb.HostDcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num)
+    dA, dB = cb.SpDCCols.from_host(ctx, hA), cb.SpDCCols.from_host(ctx, hA)  # operands may not alias
+    runs = []
+    for _ in range(2):
+        C = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dA, dB)
+        h = C.to_host()
+        runs.append(H.Dcsc(h.m, h.n, h.jc, h.cp, h.ir, h.num))
+        C.free()
+    ref = oracle.spgemm(A, A, "plus_times", "hybrid", threads=8)
+    bound = _bound(oracle, A, A)
+    for got in runs:
+        assert np.array_equal(got.jc, ref.jc) and np.array_equal(got.cp, ref.cp) and np.array_equal(got.ir, ref.ir)
+        err = np.abs(got.num - ref.num)
+        worst = int(np.argmax(err - bound))
+        assert np.all(err <= bound), f"entry {worst}: |dev - oracle| {err[worst]:.3e} > bound {bound[worst]:.3e}"
+    d12 = np.abs(runs[0].num - runs[1].num)
+    assert np.all(d12 <= bound)
+    # single-product entries have a zero bound (bit-exact); enough entries sum several products
+    # of mixed sign that the orders genuinely differ (heap vs hash on the CPU: ~7 % of entries)
+    assert (bound > 0).mean() > 0.05

@@ -1,0 +1,22 @@
+#!/bin/bash
+# dense sub-tile capacity A/B (CAPD = T/4 * {2,3,4}, rows read off the bitmap): spgemm GPU tests
+# on the product build (3) and the variants, then bench A/B.
+#   gpurun --timeout 900 -- bash tools/gpu_capd.sh TAG
+set -o pipefail
+TAG=${1:-capd}
+OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 1
+for v in base c4 c2; do
+  if [ "$v" = base ]; then L=""; else L=$v; fi
+  echo "== $(date +%T) pytest spgemm $v"
+  CBH_LIB=$L timeout -k 10 400 python -u -m pytest tests/test_spgemm_gpu.py tests/test_scale22_gpu.py tests/test_f64_rounding_gpu.py -x -q --timeout 180 --timeout-method thread > "$OUT/pytest_$v.log" 2>&1 \
+    || { tail -40 "$OUT/pytest_$v.log"; exit 1; }
+  tail -1 "$OUT/pytest_$v.log"
+  echo "== $(date +%T) bench $v"
+  CBH_LIB=$L timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-merge > "$OUT/bench_$v.json" 2> "$OUT/bench_$v.err" \
+    || { tail -20 "$OUT/bench_$v.err"; exit 1; }
+  python3 -c "import json; d=json.load(open('$OUT/bench_$v.json')); print(d['value'], d['ms_per_step'], d['config']['kernel_ms'], d['roofline']['kernel'][-12:], d['roofline']['frac'], d['check']['ok'])"
+done
+echo "== $(date +%T) done"
