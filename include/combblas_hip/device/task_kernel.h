@@ -46,6 +46,10 @@ constexpr int kFill8 = 4;
 #ifndef CBH_CAPD4
 #define CBH_CAPD4 3
 #endif
+// a task runs dense when its dense sub-tiles are at most CBH_DRATIO4/4 of its hash sub-tiles
+#ifndef CBH_DRATIO4
+#define CBH_DRATIO4 5
+#endif
 
 // Diagnostic build only (-DCBH_STAMPS, libcombblas_hip_stamps.so): thread 0 of every workgroup
 // adds the s_memtime cycles of each kernel phase (delimited by block barriers) into g_stamps.
@@ -255,7 +259,7 @@ __host__ __device__ inline int64_t dense_subtiles(int64_t work, int64_t span, in
   int64_t Rd = (work + cd - 1) / cd;
   const int64_t Rw = (span + 32 * nwb - 1) / (32 * nwb);
   Rd = Rd > Rw ? Rd : Rw;
-  return 4 * Rd <= 5 * R ? Rd : 0;
+  return 4 * Rd <= CBH_DRATIO4 * R ? Rd : 0;
 }
 
 template <class SR, int T, int BS, int EMAX, int U, int MODE>
