@@ -72,6 +72,23 @@ def ColumnStats(A: SpDCCols, hard: float):
     return tuple(out)
 
 
+def ColumnStatsKept(A: SpDCCols, thresh):
+    """(count, sum) per column of the entries PruneColumn(thresh) keeps (!(v < thresh[col])), as
+    f64 device vectors -- the statistics of the pruned matrix without forming it"""
+    dev = A.ctx.tdevice
+    out = [torch.empty(A.n, dtype=torch.float64, device=dev) for _ in range(2)]
+    check(lib().cbh_col_stats_kept(A.ctx.h, A.h, _p(thresh.contiguous()), *[_p(t) for t in out]), A.ctx.h)
+    return tuple(out)
+
+
+def kselect_cols(A: SpDCCols, aidx, nact, k):
+    """Kselect1 of whole local columns, one launch: f64 per active index, DBL_MIN where the active
+    column has no entries"""
+    out = torch.full((nact,), 2.2250738585072014e-308, dtype=torch.float64, device=A.ctx.tdevice)
+    check(lib().cbh_kselect_cols(A.ctx.h, A.h, _p(aidx), nact, int(k), _p(out)), A.ctx.h)
+    return out
+
+
 def kselect_hist(A: SpDCCols, aidx, nact, prefix, shift):
     hist = torch.empty(nact * 256, dtype=torch.int32, device=A.ctx.tdevice)
     check(lib().cbh_kselect_hist(A.ctx.h, A.h, _p(aidx), nact, _p(prefix), shift, _p(hist)), A.ctx.h)

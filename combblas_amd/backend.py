@@ -94,6 +94,14 @@ class HipBackend:
         from .apps import ColumnStats
         return ColumnStats(A, hard)
 
+    def col_stats_kept(self, A: SpDCCols, thresh):
+        from .apps import ColumnStatsKept
+        return ColumnStatsKept(A, thresh)
+
+    def kselect_cols(self, A: SpDCCols, aidx, nact, k):
+        from .apps import kselect_cols
+        return kselect_cols(A, aidx, nact, k)
+
     def kselect_hist(self, A: SpDCCols, aidx, nact, prefix, shift):
         from .apps import kselect_hist
         return kselect_hist(A, aidx, nact, prefix, shift)

@@ -9,6 +9,8 @@
 //                        keys; histograms can be summed over a processor column between passes
 //                                                           [SpParMat::Kselect1, SpParMat.cpp:1413-1700]
 //   prune_col_kernel     keep entries !(v < thresh[col])    [Dcsc::PruneColumn, dcsc.cpp:699-760]
+//   colstat_kept_kernel  count / sum of what PruneColumn(thresh) keeps, per column
+//   kselect_cols_kernel  Kselect1 of whole local columns in one launch (LDS-staged radix select)
 //
 // Included once by spgemm.hip (one translation unit).
 #pragma once
@@ -575,6 +577,37 @@ __global__ __launch_bounds__(256) void colstat_kernel(const int64_t* __restrict_
   }
 }
 
+// colstat_kept_kernel: per column, count and sum of the entries that PruneColumn(thresh) keeps
+// (!(v < thresh[col])) -- the statistics of the pruned matrix without forming it
+__global__ __launch_bounds__(256) void colstat_kept_kernel(const int64_t* __restrict__ jc, const int64_t* __restrict__ cp,
+                                                           const double* __restrict__ num, int64_t nzc,
+                                                           const double* __restrict__ thresh, double* __restrict__ cntk,
+                                                           double* __restrict__ sumk) {
+  const int lane = threadIdx.x & 63;
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= nzc) return;
+  const int64_t col = jc[s];
+  const double t = thresh[col];
+  const int64_t p0 = cp[s], p1 = cp[s + 1];
+  double n1 = 0, s1 = 0;
+  for (int64_t p = p0 + lane; p < p1; p += 64) {
+    const double v = num[p];
+    if (!(v < t)) {
+      n1 += 1.0;
+      s1 += v;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    n1 += __shfl_xor(n1, o);
+    s1 += __shfl_xor(s1, o);
+  }
+  if (lane == 0) {
+    cntk[col] = n1;
+    sumk[col] = s1;
+  }
+}
+
 // order-preserving map of a double onto uint64 (larger value -> larger key)
 __device__ __forceinline__ uint64_t fkey(double v) {
   uint64_t b;
@@ -634,6 +667,79 @@ __global__ void kselect_pick_kernel(int64_t nact, const uint32_t* __restrict__ h
 __global__ void kselect_value_kernel(int64_t nact, const uint64_t* __restrict__ prefix, double* __restrict__ out) {
   const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (a < nact) out[a] = fval(prefix[a]);
+}
+
+// Kselect1 of whole local columns in one launch: workgroups stride over the column slots, an
+// active column's keys are staged in LDS once (columns up to kSelStage entries; longer ones are
+// re-read from HBM each pass) and the 8 radix passes run on them -- histogram by LDS atomics, the
+// digit holding descending rank r found by one wave (lane l owns bins 255-4l .. 252-4l, a shuffle
+// prefix and a ballot). out[aidx[col]] = the k-th largest value, the smallest when the column has
+// fewer than k entries (active columns without a slot keep the caller's fill).
+constexpr int kSelStage = 4096;
+__global__ __launch_bounds__(256) void kselect_cols_kernel(const int64_t* __restrict__ jc, const int64_t* __restrict__ cp,
+                                                           const double* __restrict__ num, int64_t nzc,
+                                                           const int32_t* __restrict__ aidx, int64_t k,
+                                                           double* __restrict__ out) {
+  __shared__ uint64_t keys[kSelStage];
+  __shared__ uint32_t h[256];
+  __shared__ uint64_t s_pre;
+  __shared__ int64_t s_rank;
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int64_t s = blockIdx.x; s < nzc; s += gridDim.x) {
+    const int32_t ai = aidx[jc[s]];
+    const int64_t p0 = cp[s], n = cp[s + 1] - p0;
+    if (ai < 0 || n <= 0) continue;  // uniform over the workgroup
+    const bool staged = n <= kSelStage;
+    if (staged)
+      for (int64_t i = tid; i < n; i += 256) keys[i] = fkey(num[p0 + i]);
+    int64_t r = (n >= k ? k : n) - 1;
+    uint64_t pre = 0;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+      h[tid] = 0u;
+      __syncthreads();
+      const uint64_t himask = shift >= 56 ? 0ull : (~0ull << (shift + 8));
+      for (int64_t i = tid; i < n; i += 256) {
+        const uint64_t key = staged ? keys[i] : fkey(num[p0 + i]);
+        if ((key & himask) == pre) atomicAdd(&h[(key >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      if (tid < 64) {
+        uint32_t c[4], sum = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          c[j] = h[255 - 4 * lane - j];
+          sum += c[j];
+        }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t t = __shfl_up(incl, o);
+          if (lane >= o) incl += t;
+        }
+        const uint64_t m = __ballot((int64_t)incl > r);
+        const int L = __ffsll((long long)m) - 1;
+        if (lane == L) {
+          int64_t rr = r - (int64_t)(incl - sum);
+          int d = 255 - 4 * lane;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (rr < (int64_t)c[j]) {
+              d = 255 - 4 * lane - j;
+              break;
+            }
+            rr -= c[j];
+          }
+          s_pre = pre | ((uint64_t)d << shift);
+          s_rank = rr;
+        }
+      }
+      __syncthreads();
+      pre = s_pre;
+      r = s_rank;
+    }
+    if (tid == 0) out[ai] = fval(pre);
+    __syncthreads();
+  }
 }
 
 // keep entry (i, col) iff !(v < thresh[col]): pass 1 counts per slot, pass 2 copies

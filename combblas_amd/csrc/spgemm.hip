@@ -2317,6 +2317,35 @@ int cbh_kselect_value(cbh_ctx* ctx, int64_t nactive, const uint64_t* prefix, dou
   return CBH_OK;
 }
 
+int cbh_col_stats_kept(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, double* cntk, double* sumk) {
+  CBH_TRY(need_f64(ctx, A));
+  if (!thresh || !cntk || !sumk) return fail(ctx, CBH_E_ARG, "null argument");
+  const size_t nb = sizeof(double) * (size_t)A->n;
+  CBH_HIP(ctx, hipMemsetAsync(cntk, 0, nb, ctx->stream));
+  CBH_HIP(ctx, hipMemsetAsync(sumk, 0, nb, ctx->stream));
+  if (A->nzc > 0) {
+    hipLaunchKernelGGL(colstat_kept_kernel, dim3(blocks_for(A->nzc, 4)), dim3(256), 0, ctx->stream, A->jc, A->cp,
+                       reinterpret_cast<const double*>(A->num), A->nzc, thresh, cntk, sumk);
+    CBH_HIP(ctx, hipGetLastError());
+  }
+  return CBH_OK;
+}
+
+int cbh_kselect_cols(cbh_ctx* ctx, const cbh_mat* A, const int32_t* active_index, int64_t nactive, int64_t k,
+                     double* out) {
+  CBH_TRY(need_f64(ctx, A));
+  if (k < 1) return fail(ctx, CBH_E_ARG, "k must be >= 1");
+  if (nactive <= 0) return CBH_OK;
+  if (!active_index || !out) return fail(ctx, CBH_E_ARG, "null argument");
+  if (A->nzc > 0) {
+    const int64_t grid = A->nzc < 8192 ? A->nzc : 8192;  // workgroups stride over the slots
+    hipLaunchKernelGGL(kselect_cols_kernel, dim3((unsigned)grid), dim3(256), 0, ctx->stream, A->jc, A->cp,
+                       reinterpret_cast<const double*>(A->num), A->nzc, active_index, k, out);
+    CBH_HIP(ctx, hipGetLastError());
+  }
+  return CBH_OK;
+}
+
 int cbh_prune_columns(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, cbh_mat** C) {
   CBH_TRY(need_f64(ctx, A));
   if (!thresh || !C) return fail(ctx, CBH_E_ARG, "null argument");

@@ -541,6 +541,9 @@ def Kselect(be, blk, active, k, colgroup=None, total=None):
         total = ColumnStats(be, blk, float("-inf"), colgroup)[0]
     aidx = torch.full((n,), -1, dtype=torch.int32, device=dev)
     aidx[act] = torch.arange(nact, dtype=torch.int32, device=dev)
+    if _whole_columns(colgroup) and hasattr(be, "kselect_cols"):  # one launch, columns staged in LDS
+        kth[act] = be.kselect_cols(blk, aidx, nact, k)
+        return kth
     tot = total[act].to(torch.int64)
     rank = torch.where(tot >= k, torch.full_like(tot, k - 1), tot - 1).contiguous()
     prefix = torch.zeros(nact, dtype=torch.int64, device=dev)  # uint64 key bits
@@ -554,9 +557,23 @@ def Kselect(be, blk, active, k, colgroup=None, total=None):
     return kth
 
 
+def _whole_columns(colgroup):
+    """the block holds its columns whole (no processor column to sum over)"""
+    return colgroup is None or getattr(colgroup, "size", 1) == 1
+
+
+def _kept_stats(be, A, prune, colgroup):
+    """(count, sum) per column of PruneColumn(A, prune) -- the recovery check of ParFriends.h:318-329"""
+    if _whole_columns(colgroup) and hasattr(be, "col_stats_kept"):
+        return be.col_stats_kept(A, prune)  # without forming the pruned matrix
+    S = be.prune_columns(A, prune)
+    _, cnt1, sum1 = ColumnStats(be, S, float("-inf"), colgroup)
+    be.free(S)
+    return cnt1, sum1
+
+
 def _mcl_block(be, A, colgroup, hardThreshold, selectNum, recoverNum, recoverPct):
     """ParFriends.h:185-353 on a local block whose columns may be split over `colgroup`"""
-    inf = float("-inf")
     cnt, cntp, sump = ColumnStats(be, A, hardThreshold, colgroup)  # unpruned nnz, pruned nnz, pruned sums
     prune = torch.full_like(cnt, hardThreshold)
     rec = (cntp < recoverNum) & (cnt > cntp) & (sump < recoverPct)
@@ -567,9 +584,7 @@ def _mcl_block(be, A, colgroup, hardThreshold, selectNum, recoverNum, recoverPct
         if bool(sel.any()):
             prune = torch.where(sel, Kselect(be, A, sel, selectNum, colgroup, cnt), prune)
             if recoverNum > 0:
-                S = be.prune_columns(A, prune)
-                _, cnt1, sum1 = ColumnStats(be, S, inf, colgroup)
-                be.free(S)
+                cnt1, sum1 = _kept_stats(be, A, prune, colgroup)
                 s2 = sel & (cnt1 < recoverNum) & (sum1 < recoverPct)
                 if bool(s2.any()):
                     prune = torch.where(s2, Kselect(be, A, s2, recoverNum, colgroup, cnt), prune)

@@ -256,14 +256,22 @@ int cbh_ewise_mult(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, cbh_mat** C
  *                      at `shift` (56, 48, ..., 0), then pick the digit holding rank (descending).
  *                      Histograms may be summed over a processor column between the two calls.
  *                      active_index[col] = slot in the active list or -1.
- *   cbh_prune_columns  keep entries with !(v < thresh[col]) (Dcsc::PruneColumn, dcsc.cpp:699-760) */
+ *   cbh_kselect_cols   the same Kselect1 for columns held whole by this block, in one launch:
+ *                      out[active_index[col]] = k-th largest (the smallest when fewer than k);
+ *                      active columns without entries keep what out held (the caller's fill)
+ *   cbh_prune_columns  keep entries with !(v < thresh[col]) (Dcsc::PruneColumn, dcsc.cpp:699-760)
+ *   cbh_col_stats_kept count / sum of the entries cbh_prune_columns(thresh) would keep, per column
+ *                      (ParFriends.h:318-329: the recovery check on the selected matrix) */
 int cbh_col_stats(cbh_ctx* ctx, const cbh_mat* A, double hard, double* cnt, double* cntp, double* sump);
 int cbh_kselect_hist(cbh_ctx* ctx, const cbh_mat* A, const int32_t* active_index, int64_t nactive,
                      const uint64_t* prefix, int shift, uint32_t* hist);
 int cbh_kselect_pick(cbh_ctx* ctx, int64_t nactive, const uint32_t* hist, uint64_t* prefix, int64_t* rank,
                      int shift);
 int cbh_kselect_value(cbh_ctx* ctx, int64_t nactive, const uint64_t* prefix, double* out);
+int cbh_kselect_cols(cbh_ctx* ctx, const cbh_mat* A, const int32_t* active_index, int64_t nactive, int64_t k,
+                     double* out);
 int cbh_prune_columns(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, cbh_mat** C);
+int cbh_col_stats_kept(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, double* cntk, double* sumk);
 
 /* ---------------------------------------------------------------- format conversions (device)
  *   cbh_tuples_to_dcsc  device COO (rows, cols, vals; any order, duplicates allowed) -> a DCSC block:

@@ -226,24 +226,51 @@ def test_kselect_edge_cases(ctx):
     from combblas_amd import parfriends as pf
     from combblas_amd.backend import HipBackend
 
+    rng = np.random.default_rng(1)
     cols = [[3.0, 1.0, 2.0], [5.0, 5.0, 5.0, 1.0], [-1.0, -7.5, 0.0, -0.0, 2.5], [4.0], [], [9.0, 8.0],
-            list(np.random.default_rng(1).standard_normal(3000))]
+            list(rng.standard_normal(3000)), list(rng.standard_normal(5000)),  # LDS-staged / re-read from HBM
+            list(np.round(rng.standard_normal(6000), 1))]  # many ties
     rows, cc, vv = [], [], []
     for j, c in enumerate(cols):
         rows += list(range(len(c)))
         cc += [j] * len(c)
         vv += c
-    d = H.Dcsc.from_coo(4000, len(cols), np.array(rows), np.array(cc), np.array(vv, np.float64))
-    be = HipBackend(ctx)
+    d = H.Dcsc.from_coo(8000, len(cols), np.array(rows), np.array(cc), np.array(vv, np.float64))
     dA = _dev(ctx, d)
-    for k in (1, 2, 3, 5, 100):
-        active = torch.tensor([True, True, True, True, True, False, True], device=ctx.tdevice)
-        got = pf.Kselect(be, dA, active, k).cpu().numpy()
-        for j, c in enumerate(cols):
-            if not bool(active[j]):
-                assert np.isnan(got[j])
-            else:
-                assert got[j] == AO.kselect1(np.array(c, np.float64), k), (k, j)
+
+    class MultiPass:  # the backend without the one-launch select: the per-pass histogram path
+        def __init__(self, be):
+            self.be = be
+
+        def __getattr__(self, name):
+            if name == "kselect_cols":
+                raise AttributeError(name)
+            return getattr(self.be, name)
+
+    for be in (HipBackend(ctx), MultiPass(HipBackend(ctx))):
+        for k in (1, 2, 3, 5, 100, 4500, 7000):
+            active = torch.tensor([True, True, True, True, True, False, True, True, True], device=ctx.tdevice)
+            got = pf.Kselect(be, dA, active, k).cpu().numpy()
+            for j, c in enumerate(cols):
+                if not bool(active[j]):
+                    assert np.isnan(got[j])
+                else:
+                    assert got[j] == AO.kselect1(np.array(c, np.float64), k), (type(be).__name__, k, j)
+
+
+def test_column_stats_kept_vs_oracle(ctx, apps):
+    """count / sum of what PruneColumn keeps, without forming it = the stats of the pruned matrix"""
+    import torch
+
+    from combblas_amd.apps import ColumnStatsKept
+
+    A2 = apps["mcl_A2"]
+    rng = np.random.default_rng(3)
+    for t in (np.full(A2.n, 0.01), rng.uniform(0.0, 0.05, A2.n), np.full(A2.n, -np.inf)):
+        got = [x.cpu().numpy() for x in ColumnStatsKept(_dev(ctx, A2), torch.tensor(t, device=ctx.tdevice))]
+        _, cnt, sm = AO.column_stats(AO.prune_column(A2, t), -np.inf)
+        np.testing.assert_array_equal(got[0], cnt)
+        np.testing.assert_allclose(got[1], sm, rtol=1e-12, atol=0)
 
 
 @pytest.mark.parametrize("i", [0, 1])
