@@ -1025,7 +1025,7 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
   BinLists bd, bl;
   CBH_TRY(make_bins(ctx, S, wd, nt, t0, P.order, &bd, BinCaps{kSmallCap, kSmallCap}, P.tunits + t0, P.trk + t0));
   const int64_t nd = bd.small_count + bd.mid_count + bd.large_count;
-  CBH_TRY(make_bins(ctx, S, wh, nt, t0, P.order + nd, &bl, BinCaps{kSmallCap, kSmallCap}, P.tunits + t0, P.trk + t0));
+  CBH_TRY(make_bins(ctx, S, wh, nt, t0, P.order + nd, &bl, BinCaps{kSmallCap, kMidCap}, P.tunits + t0, P.trk + t0));
   bl.small_first += nd;
   bl.mid_first += nd;
   bl.large_first += nd;
@@ -1040,7 +1040,8 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
   constexpr double eb = 4.0 + sizeof(typename SR::val_t);
   const double nb_d = eb * bd.units[2] + 16.0 * bd.large_count;
   const double nb_l = eb * bl.units[2] + 16.0 * bl.large_count;
-  const double nb_s = eb * (bl.units[0] + bl.units[1]) + 16.0 * (bl.small_count + bl.mid_count);
+  const double nb_s = eb * bl.units[0] + 16.0 * bl.small_count;
+  const double nb_m = eb * bl.units[1] + 16.0 * bl.mid_count;
   if (diag_enabled()) {
     CBH_TRY((launch_task_diag<SR, TNumLarge, MODE_TDENSE>(ctx, a, bd, "numeric dense")));
     CBH_TRY((launch_task_diag<SR, TNumLarge, MODE_TNUM>(ctx, a, bl, "numeric hash")));
@@ -1048,10 +1049,10 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
     CBH_TRY((launch_task<SR, TNumLarge, MODE_TDENSE>(ctx, a, bd.large_first, bd.large_count, CBH_K_NUM_DENSE, nb_d)));
     CBH_TRY((launch_task<SR, TNumLarge, MODE_TNUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
   }
-  CBH_TRY((launch_task<SR, TNumSmall, MODE_TNUM>(ctx, a, bl.small_first, bl.small_count + bl.mid_count,
-                                                  CBH_K_NUM_SMALL, nb_s)));
+  CBH_TRY((launch_task<SR, TNumMid, MODE_TNUM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_NUM_SMALL, nb_m)));
+  CBH_TRY((launch_task<SR, TNumSmall, MODE_TNUM>(ctx, a, bl.small_first, bl.small_count, CBH_K_NUM_SMALL, nb_s)));
   if (launches) *launches += (bd.large_count > 0);
-  if (launches) *launches += (bl.large_count > 0) + (bl.small_count + bl.mid_count > 0);
+  if (launches) *launches += (bl.large_count > 0) + (bl.mid_count > 0) + (bl.small_count > 0);
   return CBH_OK;
 }
 

@@ -19,6 +19,12 @@ struct TSymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512, U = 8; }
 struct TNumSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 // (T = 8192 with 1024-thread groups, one per CU: 89.1 vs 98.2 GFLOP/s at scale 22)
 struct TNumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512, U = 8; };
+// mid-size hash tasks (kSmallCap < outputs <= kMidCap) of the library's A^2 path: a quarter of the
+// large kernel's LDS, so four workgroups share a CU and the per-task setup latency overlaps
+#ifndef CBH_MIDCAP
+#define CBH_MIDCAP 1024
+#endif
+struct TNumMid { static constexpr int T = 2 * CBH_MIDCAP, BS = 256, EMAX = 256, U = 4; };
 // wider accumulators (user value types) keep the large table within ~50 KB of LDS
 template <class SR>
 struct TNumLargeFor {
@@ -34,6 +40,7 @@ struct TNumSmallFor {
 };
 constexpr int64_t kChunkMin = 256;  // tasks with more B entries than this keep cursors in HBM
 constexpr int64_t kSmallCap = 256;  // numeric tasks with <= kSmallCap outputs run the small kernel
+constexpr int64_t kMidCap = CBH_MIDCAP;  // ... with <= kMidCap the mid kernel (library numeric pass)
 static_assert(kChunkMin <= TSymSmall::EMAX && kChunkMin <= TSymLarge::EMAX && kChunkMin <= TNumSmall::EMAX &&
                   kChunkMin <= TNumLarge::EMAX,
               "every chunked task needs HBM cursor state");

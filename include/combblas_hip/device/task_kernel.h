@@ -783,8 +783,12 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
         __syncthreads();
       }
     }
-    if (qtot > WIN || __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {  // table could not hold the sub-tile: halve the row range, redo
-      if (!chunked && dense)  // the value pass never ran: restore the cursors the bitmap pass moved
+    const bool ovf_now = __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (qtot > WIN || ovf_now) {  // table could not hold the sub-tile: halve the row range, redo
+      // restore the cursors segments() moved, unless the insertion overflow already did (hash
+      // tables only: the dense passes never raise it during the sweep). A hash sub-tile that
+      // inserted fine but occupies more slots than the commit queue holds lands here unrestored.
+      if (!chunked && (dense || !ovf_now))
         for (int i = tid; i < (int)ne; i += BS) epos[i] += eoff[i];
       __syncthreads();
       my_count = count_before;
