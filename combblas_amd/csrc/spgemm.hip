@@ -978,18 +978,19 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   }
   CBH_HIP(ctx, hipMemsetAsync(P.tcnt, 0, sizeof(int64_t) * (nt + 1), ctx->stream));
   BinLists bl;
-  CBH_TRY(make_bins(ctx, S, P.twork, P.ntasks, 0, P.order, &bl, BinCaps{kSmallCap, kSmallCap}, P.tunits, P.trk));
+  CBH_TRY(make_bins(ctx, S, P.twork, P.ntasks, 0, P.order, &bl, BinCaps{kSmallCap, kSymMidCap}, P.tunits, P.trk));
   TaskArgs a = task_args(A, B, P, ctx);
   a.twork = P.twork;
   a.cnt = P.tcnt;
   using Dummy = PlusTimesD<int64_t>;
   // algorithmic bytes of the symbolic pass: row ids of B and of every gathered A entry + pointers
   const double sb_l = 4.0 * bl.units[2] + 16.0 * bl.large_count;
-  const double sb_s = 4.0 * (bl.units[0] + bl.units[1]) + 16.0 * (bl.small_count + bl.mid_count);
+  const double sb_s = 4.0 * bl.units[0] + 16.0 * bl.small_count;
+  const double sb_m = 4.0 * bl.units[1] + 16.0 * bl.mid_count;
   if (diag_enabled()) CBH_TRY((launch_task_diag<Dummy, TSymLarge, MODE_TSYM>(ctx, a, bl, "symbolic")));
   else CBH_TRY((launch_task<Dummy, TSymLarge, MODE_TSYM>(ctx, a, bl.large_first, bl.large_count, CBH_K_SYM_LARGE, sb_l)));
-  CBH_TRY((launch_task<Dummy, TSymSmall, MODE_TSYM>(ctx, a, bl.small_first, bl.small_count + bl.mid_count,
-                                                     CBH_K_SYM_SMALL, sb_s)));
+  CBH_TRY((launch_task<Dummy, TSymMid, MODE_TSYM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_SYM_SMALL, sb_m)));
+  CBH_TRY((launch_task<Dummy, TSymSmall, MODE_TSYM>(ctx, a, bl.small_first, bl.small_count, CBH_K_SYM_SMALL, sb_s)));
   // task offsets -> column pointers of C
   CBH_TRY(exclusive_scan_i64(ctx, S, P.tcnt, P.toff, P.ntasks + 1));
   hipLaunchKernelGGL(gather_i64_kernel, dim3(blocks_for(n + 1, 256)), dim3(256), 0, ctx->stream, P.toff, P.tstart,

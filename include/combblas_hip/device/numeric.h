@@ -16,6 +16,12 @@ namespace cbh {
 // task-kernel configurations: T slots, BS threads, EMAX entries per chunk, U products per thread
 struct TSymSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 struct TSymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512, U = 8; };
+// mid-size symbolic tasks (kSmallCap < products <= kSymMidCap): one sub-tile in a 16 KB key
+// table, five workgroups per CU, so the per-task setup latency overlaps
+#ifndef CBH_SYMMID
+#define CBH_SYMMID 2048
+#endif
+struct TSymMid { static constexpr int T = 2 * CBH_SYMMID, BS = 256, EMAX = 256, U = 4; };
 struct TNumSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 // (T = 8192 with 1024-thread groups, one per CU: 89.1 vs 98.2 GFLOP/s at scale 22)
 struct TNumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512, U = 8; };
@@ -41,7 +47,9 @@ struct TNumSmallFor {
 constexpr int64_t kChunkMin = 256;  // tasks with more B entries than this keep cursors in HBM
 constexpr int64_t kSmallCap = 256;  // numeric tasks with <= kSmallCap outputs run the small kernel
 constexpr int64_t kMidCap = CBH_MIDCAP;  // ... with <= kMidCap the mid kernel (library numeric pass)
-static_assert(kChunkMin <= TSymSmall::EMAX && kChunkMin <= TSymLarge::EMAX && kChunkMin <= TNumSmall::EMAX &&
+constexpr int64_t kSymMidCap = CBH_SYMMID;  // symbolic tasks with <= kSymMidCap products: the mid kernel
+static_assert(kChunkMin <= TSymSmall::EMAX && kChunkMin <= TSymMid::EMAX && kChunkMin <= TSymLarge::EMAX &&
+                  kChunkMin <= TNumSmall::EMAX && kChunkMin <= TNumMid::EMAX &&
                   kChunkMin <= TNumLarge::EMAX,
               "every chunked task needs HBM cursor state");
 
