@@ -42,6 +42,9 @@ K_NAMES = ["sym_large", "sym_small", "num_large", "num_small", "merge_sym", "mer
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
 FREE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p)
+# per-phase consumer of cbh_spgemm_phased: (user, phase, slot0, slot1, const cbh_mat* view) -> status
+PHASE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                            ctypes.c_void_p)
 
 # every exported symbol with its signature (restype, argtypes); tests check the header against it
 SIGNATURES = {
@@ -55,6 +58,7 @@ SIGNATURES = {
     "cbh_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "cbh_ctx_set_allocator": (ctypes.c_int, [ctypes.c_void_p, ALLOC_FN, FREE_FN, ctypes.c_void_p]),
     "cbh_ctx_set_phase_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    "cbh_ctx_set_phase_consumer": (ctypes.c_int, [ctypes.c_void_p, PHASE_FN, ctypes.c_void_p]),
     "cbh_mat_upload": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cbh_dcsc), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_mat_upload_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cbh_dcsc), ctypes.c_int64,
                                             ctypes.POINTER(ctypes.c_void_p)]),
@@ -122,8 +126,10 @@ SIGNATURES = {
 }
 
 CBH_OK = 0
+ERR_CALLBACK = 4006  # returned by a Python per-phase consumer that raised
 ERRORS = {3001: "GRIDMISMATCH", 3002: "DIMMISMATCH", 3005: "MATRIXALIAS", 4001: "HIP error", 4002: "out of memory",
-          4003: "invalid argument", 4004: "device consistency check failed", 4005: "no HIP device"}
+          4003: "invalid argument", 4004: "device consistency check failed", 4005: "no HIP device",
+          ERR_CALLBACK: "per-phase consumer raised"}
 
 CBH_KEEP_EMPTY_COLS = 0x2
 CBH_MASK_PATTERN = 0x4

@@ -65,6 +65,8 @@ struct cbh_ctx {
   double k_ms[CBH_K_NKINDS] = {0};
   int64_t k_launch[CBH_K_NKINDS] = {0};
   double k_bytes[CBH_K_NKINDS] = {0};
+  cbh_phase_fn phase_fn = nullptr;  // per-phase consumer of cbh_spgemm_phased
+  void* phase_user = nullptr;
 };
 
 struct cbh_mat {
@@ -591,6 +593,13 @@ static inline unsigned blocks_for(int64_t n, int bs) { return (unsigned)std::max
 // grid cap of the wave-strided kernels (an AQL dispatch counts work-items in 32 bits: a direct
 // grid of blocks_for(n, 4) x 256 threads overflows from n = 2^26 items)
 constexpr unsigned kWaveGridCap = 1u << 16;
+// CBH_TEST_GRID_CAP=<blocks> lowers the cap so that a small product exercises the wave-strided
+// loops' wrap-around (tests/test_regress_gpu.py); read on every launch so a test can set it
+static unsigned wave_grid_cap() {
+  const char* e = std::getenv("CBH_TEST_GRID_CAP");
+  const long v = e ? std::atol(e) : 0;
+  return v > 0 && v < (long)kWaveGridCap ? (unsigned)v : kWaveGridCap;
+}
 
 static int check_err(cbh_ctx* ctx) {
   int h[16];
@@ -800,9 +809,9 @@ static int launch_task_diag(cbh_ctx* ctx, const TaskArgs& a, const BinLists& bl,
     std::fprintf(stderr, "[cbh diag] %s work 2^%d: %lld tasks, %.3f ms\n", what, lg, (long long)n, ms);
 #ifdef CBH_STAMPS
     {
-      unsigned long long hs[16];
+      unsigned long long hs[24];
       (void)hipMemcpyFromSymbol(hs, HIP_SYMBOL(g_stamps), sizeof(hs));
-      const unsigned long long z[16] = {0};
+      const unsigned long long z[24] = {0};
       (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
       double tot = 0;
       for (int k = 0; k < 12; ++k) tot += (double)hs[k];
@@ -811,6 +820,9 @@ static int launch_task_diag(cbh_ctx* ctx, const TaskArgs& a, const BinLists& bl,
                    hs[12], tot / std::max(1ull, hs[12]), 100 * hs[0] / tot, 100 * hs[1] / tot, 100 * hs[2] / tot,
                    100 * hs[3] / tot, 100 * hs[4] / tot, 100 * hs[5] / tot, 100 * hs[8] / tot, 100 * hs[9] / tot,
                    100 * hs[10] / tot, 100 * hs[6] / tot, 100 * hs[7] / tot);
+      std::fprintf(stderr, "[cbh stamps]   entry-visits=%llu active=%llu (%.1f%%) short=%llu (%.1f%% of active) short-products=%llu (%.1f%%) committed=%llu\n",
+                   hs[16], hs[17], 100.0 * hs[17] / std::max(1ull, hs[16]), hs[18], 100.0 * hs[18] / std::max(1ull, hs[17]),
+                   hs[19], 100.0 * hs[19] / std::max(1ull, hs[15]), hs[20]);
     }
 #endif
     (void)hipEventDestroy(e0);
@@ -1224,6 +1236,13 @@ int cbh_ctx_set_allocator(cbh_ctx* ctx, cbh_alloc_fn alloc, cbh_free_fn release,
   return CBH_OK;
 }
 
+int cbh_ctx_set_phase_consumer(cbh_ctx* ctx, cbh_phase_fn fn, void* user) {
+  if (!ctx) return CBH_E_ARG;
+  ctx->phase_fn = fn;
+  ctx->phase_user = user;
+  return CBH_OK;
+}
+
 int cbh_ctx_set_phase_budget(cbh_ctx* ctx, int64_t bytes) {
   if (!ctx || bytes < 0) return CBH_E_ARG;
   ctx->phase_budget = bytes;
@@ -1561,10 +1580,36 @@ int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh
     CBH_HIP(ctx, hipMemsetAsync(d_sum, 0, sizeof(double), ctx->stream));
     CBH_HIP(ctx, hipMemsetAsync(d_dig, 0, sizeof(unsigned long long), ctx->stream));
     int64_t launches = 0;
+    int64_t *vcp = nullptr, *vjc = nullptr;  // per-phase consumer: the view's rebased pointers / ids
+    if (ctx->phase_fn) {
+      int64_t maxn = 0;
+      for (size_t i = 1; i < cuts.size(); ++i) maxn = std::max(maxn, cuts[i] - cuts[i - 1]);
+      CBH_TRY(S.get(&vcp, maxn + 1));
+      CBH_TRY(S.get(&vjc, std::max<int64_t>(maxn, 1)));
+    }
     for (size_t i = 1; i < cuts.size(); ++i) {
       const int64_t c0 = cuts[i - 1], c1 = cuts[i];
       const double tp = hnow();
       CBH_TRY(run_numeric<SR>(ctx, S, A, B, P, hts[c0], hts[c1], hcp[c0], ir, num, &launches, maxphase));
+      if (ctx->phase_fn) {
+        hipLaunchKernelGGL(keep_cols_kernel, dim3(blocks_for(c1 - c0 + 1, 256)), dim3(256), 0, ctx->stream, B->jc + c0,
+                           P.Ccp + c0, c1 - c0, hcp[c0], vjc, vcp);
+        CBH_HIP(ctx, hipGetLastError());
+        cbh_mat view;
+        view.m = A->m;
+        view.n = B->n;
+        view.nnz = hcp[c1] - hcp[c0];
+        view.nzc = c1 - c0;
+        view.dtype = A->dtype;
+        view.vbytes = (int64_t)sizeof(VT);
+        view.cp = vcp;
+        view.jc = vjc;
+        view.ir = ir;
+        view.num = num;
+        view.owned = false;
+        const int rc = ctx->phase_fn(ctx->phase_user, (int64_t)i - 1, c0, c1, &view);
+        if (rc != CBH_OK) return fail(ctx, rc, "phase consumer returned " + std::to_string(rc));
+      }
       if (diag_enabled()) {
         CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
         std::fprintf(stderr, "[cbh diag] phase %zu: cols [%lld,%lld) %.1f ms host wall\n", i, (long long)c0,
@@ -1676,7 +1721,7 @@ int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t
   BinLists bd, bl;
   CBH_TRY(make_bins(ctx, p->S, wd, nt, 0, P.order, &bd, BinCaps{kSmallCap, kSmallCap}, nullptr, P.trk));
   const int64_t nd = bd.small_count + bd.mid_count + bd.large_count;
-  CBH_TRY(make_bins(ctx, p->S, wh, nt, 0, P.order + nd, &bl, BinCaps{kSmallCap, kSmallCap}, nullptr, P.trk));
+  CBH_TRY(make_bins(ctx, p->S, wh, nt, 0, P.order + nd, &bl, BinCaps{kSmallCap, kMidCap}, nullptr, P.trk));
   const cbh_mat* A = p->A;
   const cbh_mat* B = p->B;
   out->Acp = P.Adense;
@@ -1711,7 +1756,9 @@ int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t
   out->large_first = nd + bl.large_first;
   out->large_count = bl.large_count;
   out->small_first = nd + bl.small_first;
-  out->small_count = bl.small_count + bl.mid_count;
+  out->small_count = bl.small_count;
+  out->mid_first = nd + bl.mid_first;
+  out->mid_count = bl.mid_count;
   return CBH_OK;
 }
 
@@ -2094,9 +2141,9 @@ static int masked_dot(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, const cb
     CBH_TRY(S.get(&pval, nitems));
     CBH_TRY(S.get(&phit, nitems));
     // wave-strided kernels: capped grids (a dispatch's work-item count is 32-bit)
-    hipLaunchKernelGGL(dot_items_kernel, dim3(std::min(blocks_for(nlong, 4), kWaveGridCap)), dim3(256), 0, ctx->stream,
+    hipLaunchKernelGGL(dot_items_kernel, dim3(std::min(blocks_for(nlong, 4), wave_grid_cap())), dim3(256), 0, ctx->stream,
                        poff, nlong, item);
-    hipLaunchKernelGGL(dot_wave_kernel<SR>, dim3(std::min(blocks_for(nitems, 4), kWaveGridCap)), dim3(256), 0,
+    hipLaunchKernelGGL(dot_wave_kernel<SR>, dim3(std::min(blocks_for(nitems, 4), wave_grid_cap())), dim3(256), 0,
                        ctx->stream, a, llong, poff, item, nitems, pval, phit);
     hipLaunchKernelGGL(dot_fold_kernel<SR>, dim3(blocks_for(nlong, 256)), dim3(256), 0, ctx->stream, a, llong, poff,
                        nlong, pval, phit);

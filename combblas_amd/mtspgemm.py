@@ -154,14 +154,41 @@ def MultiwayMerge(SR: Semiring, lists, mdim=0, ndim=0, delarrs=False) -> SpDCCol
     return cur[0]
 
 
-def PhasedSpGEMM(SR: Semiring, A: SpDCCols, B: SpDCCols, checksum=False, budget_bytes=None):
+def PhasedSpGEMM(SR: Semiring, A: SpDCCols, B: SpDCCols, checksum=False, budget_bytes=None, on_phase=None):
     """MemEfficientSpGEMM's phase loop (ParFriends.h:449-730) for one block: B's columns are
     processed in phases sized from the exact symbolic pass; each phase's C block is materialised
-    in HBM then its buffer reused. Returns {flops, nnz, phases, value_sum, digest}."""
+    in HBM then its buffer reused. Returns {flops, nnz, phases, value_sum, digest}.
+
+    on_phase(phase, slot0, slot1, Cphase): the per-phase consumer (MemEfficientSpGEMM's
+    MCLPruneRecoverySelect + ColConcatenate, :694-721). Cphase is a borrowed m x B.n SpDCCols of
+    C(:, B's column slots [slot0, slot1)) with the phase's empty columns kept; it is valid only
+    during the call (clone() keeps a copy)."""
     if budget_bytes is not None:
         A.ctx.set_phase_budget(budget_bytes)
     st = _lib.cbh_phase_stats()
     flags = _lib.CBH_PHASE_CHECKSUM if checksum else 0
-    check(lib().cbh_spgemm_phased(A.ctx.h, SR.code, A.h, B.h, flags, ctypes.byref(st)), A.ctx.h)
+    cb = None
+    errors = []
+    if on_phase is not None:
+        def _consume(user, phase, s0, s1, view):
+            v = SpDCCols(A.ctx, ctypes.c_void_p(view), borrowed=True)
+            try:
+                on_phase(int(phase), int(s0), int(s1), v)
+            except Exception as e:  # reported after the C call returns
+                errors.append(e)
+                return _lib.ERR_CALLBACK
+            finally:
+                v.h = None
+            return 0
+        cb = _lib.PHASE_FN(_consume)
+        check(lib().cbh_ctx_set_phase_consumer(A.ctx.h, cb, None), A.ctx.h)
+    try:
+        rc = lib().cbh_spgemm_phased(A.ctx.h, SR.code, A.h, B.h, flags, ctypes.byref(st))
+    finally:
+        if cb is not None:
+            lib().cbh_ctx_set_phase_consumer(A.ctx.h, _lib.PHASE_FN(), None)
+    if errors:
+        raise errors[0]
+    check(rc, A.ctx.h)
     return {"flops": st.flops, "nnz": st.nnz, "phases": st.phases, "value_sum": st.value_sum,
             "digest": st.digest}

@@ -157,8 +157,10 @@ class Context:
 class SpDCCols:
     """A device-resident local sparse block (wraps a cbh_mat handle)."""
 
-    def __init__(self, ctx: Context, handle, keepalive=None):
-        self.ctx, self.h, self._keep = ctx, handle, keepalive
+    def __init__(self, ctx: Context, handle, keepalive=None, borrowed=False):
+        # borrowed: a non-owning view the library hands out (the per-phase consumer of
+        # cbh_spgemm_phased); free() only forgets it
+        self.ctx, self.h, self._keep, self._borrowed = ctx, handle, keepalive, borrowed
         m, n, nnz, nzc, dt = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int()
         check(lib().cbh_mat_info(handle, ctypes.byref(m), ctypes.byref(n), ctypes.byref(nnz), ctypes.byref(nzc),
                                  ctypes.byref(dt)))
@@ -265,8 +267,14 @@ class SpDCCols:
         check(lib().cbh_mat_checksum(self.ctx.h, self.h, ctypes.byref(s), ctypes.byref(d)), self.ctx.h)
         return s.value, d.value
 
+    def clone(self):
+        """deep copy on the device (SpDCCols copy constructor, SpDCCols.cpp:214-226)"""
+        h = ctypes.c_void_p()
+        check(lib().cbh_mat_clone(self.ctx.h, self.h, ctypes.byref(h)), self.ctx.h)
+        return SpDCCols(self.ctx, h)
+
     def free(self):
-        if self.h is not None and self.ctx.h:
+        if self.h is not None and self.ctx.h and not self._borrowed:
             lib().cbh_mat_free(self.ctx.h, self.h)
         self.h = None
         self._keep = None

@@ -153,6 +153,16 @@ typedef struct cbh_phase_stats {
 #define CBH_PHASE_CHECKSUM 0x100u /* also compute value_sum/digest (extra read of each phase) */
 int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh_mat* B,
                       uint32_t flags, cbh_phase_stats* stats);
+/* Per-phase consumer of cbh_spgemm_phased (the role of MemEfficientSpGEMM's per-phase
+ * MCLPruneRecoverySelect + ColConcatenate, ParFriends.h:694-721): called once per phase, in
+ * column order, after the phase's numeric launches were queued on the context stream, with a
+ * NON-OWNING view of C(:, B's column slots [slot0, slot1)) -- an m x B.n DCSC that keeps the
+ * phase's empty columns (CBH_KEEP_EMPTY_COLS form). The view's arrays live in the phase
+ * workspace and are overwritten by the next phase: copy (cbh_mat_clone), reduce or prune it on
+ * the context stream before returning. A nonzero return aborts the product with that code.
+ * fn = NULL removes the consumer.                                                              */
+typedef int (*cbh_phase_fn)(void* user, int64_t phase, int64_t slot0, int64_t slot1, const cbh_mat* Cphase);
+int cbh_ctx_set_phase_consumer(cbh_ctx* ctx, cbh_phase_fn fn, void* user);
 
 /* Timing of the last cbh_spgemm/cbh_spgemm_phased call, per kernel class, measured with
  * hipEvents on the context stream (milliseconds; -1 when not recorded).                  */
@@ -204,8 +214,12 @@ typedef struct cbh_numeric_plan {
   const int32_t* order;                                      /* task ids in launch order          */
   int64_t dense_first, dense_count, large_first, large_count, small_first, small_count;
   void* stream;                                              /* hipStream_t of the context        */
+  int64_t mid_first, mid_count;                              /* mid-size hash tasks (<= 1024 out) */
 } cbh_numeric_plan;
-#define CBH_PLAN_NO_DENSE 0x1u /* bin every task for the hash kernels (locked / user semirings) */
+/* bin every task for the hash kernels: the dense (bitmap-rank) kernel needs a lock-free SR::add
+ * and 8-byte accumulators, the layout the plan's dense split is computed for (numeric.h
+ * dense_capable<SR>) */
+#define CBH_PLAN_NO_DENSE 0x1u
 /* Symbolic pass of C = A*B (A and B values may differ in type); the plan owns its scratch. */
 int cbh_plan_create(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, cbh_plan** plan);
 int cbh_plan_info(const cbh_plan* plan, int64_t* flops, int64_t* nnzC);

@@ -23,6 +23,7 @@
 
 #include <mpi.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -121,9 +122,11 @@ cbh_mat* upload(const combblas::SpDCCols<IT, NT>& A) {
   return out;
 }
 
-// column-sorted SpTuples -> device DCSC
+// column-sorted SpTuples -> device DCSC. sort_rows: rows inside a column may be in any order (the
+// unsorted outputs of the stock LocalSpGEMMHash / MultiwayMergeHash(sorted=false), mtSpGEMM.h:624-634);
+// they are sorted per column on the way up, as the device merge reads row-sorted segments.
 template <class IT, class NT>
-cbh_mat* upload(const combblas::SpTuples<IT, NT>& T) {
+cbh_mat* upload(const combblas::SpTuples<IT, NT>& T, bool sort_rows = false) {
   cbh_dcsc h{};
   h.m = T.getnrow();
   h.n = T.getncol();
@@ -143,6 +146,22 @@ cbh_mat* upload(const combblas::SpTuples<IT, NT>& T) {
   }
   if (!jc.empty()) cp.push_back(h.nnz);
   h.nzc = (int64_t)jc.size();
+  if (sort_rows)
+    for (size_t c = 0; c + 1 < cp.size(); ++c) {
+      const int64_t b = cp[c], e = cp[c + 1];
+      bool sorted = true;
+      for (int64_t i = b + 1; i < e && sorted; ++i) sorted = ir[i - 1] < ir[i];
+      if (sorted) continue;
+      std::vector<std::pair<int32_t, NT>> col;
+      for (int64_t i = b; i < e; ++i) col.emplace_back(ir[i], num[i]);
+      std::sort(col.begin(), col.end(), [](const std::pair<int32_t, NT>& x, const std::pair<int32_t, NT>& y) {
+        return x.first < y.first;
+      });
+      for (int64_t i = b; i < e; ++i) {
+        ir[i] = col[i - b].first;
+        num[i] = col[i - b].second;
+      }
+    }
   h.cp = cp.data();
   h.jc = jc.data();
   h.ir = ir.data();
@@ -210,7 +229,7 @@ combblas::SpTuples<IT, NTO>* LocalSpGEMM(const combblas::SpDCCols<IT, NT1>& A, c
 
 template <class SR, class IT, class NT>
 combblas::SpTuples<IT, NT>* MultiwayMerge(std::vector<combblas::SpTuples<IT, NT>*>& lists, IT mdim = 0, IT ndim = 0,
-                                          bool delarrs = false) {
+                                          bool delarrs = false, bool unsorted_rows = false) {
   const int nlists = (int)lists.size();
   if (nlists == 0) return new combblas::SpTuples<IT, NT>(0, mdim, ndim);
   if (nlists == 1) {
@@ -228,14 +247,50 @@ combblas::SpTuples<IT, NT>* MultiwayMerge(std::vector<combblas::SpTuples<IT, NT>
     }
   std::vector<MatGuard> g(nlists);
   std::vector<const cbh_mat*> parts(nlists);
-  for (int i = 0; i < nlists; ++i) parts[i] = g[i].m = upload(*lists[i]);
+  for (int i = 0; i < nlists; ++i) parts[i] = g[i].m = upload(*lists[i], unsorted_rows);
+  // cbh_merge takes at most 16 lists: merge in groups of 16, then the group results, and so on
+  std::vector<cbh_mat*> cur;
+  if (nlists > 16)
+    for (int i = 0; i < nlists; ++i) {  // the hierarchy owns (and frees) the uploaded lists
+      cur.push_back(g[i].m);
+      g[i].m = nullptr;
+    }
   MatGuard c;
-  int rc = cbh_merge(context(), semiring_traits<SR>::code, nlists, parts.data(), &c.m);
-  if (rc != CBH_OK) die(context(), rc, "cbh_merge");
+  if (cur.empty()) {
+    int rc = cbh_merge(context(), semiring_traits<SR>::code, nlists, parts.data(), &c.m);
+    if (rc != CBH_OK) die(context(), rc, "cbh_merge");
+  } else {
+    while (cur.size() > 1) {
+      std::vector<cbh_mat*> next;
+      for (size_t g0 = 0; g0 < cur.size(); g0 += 16) {
+        const size_t k = std::min<size_t>(16, cur.size() - g0);
+        if (k == 1) {
+          next.push_back(cur[g0]);
+          continue;
+        }
+        cbh_mat* r = nullptr;
+        int rc = cbh_merge(context(), semiring_traits<SR>::code, (int)k, cur.data() + g0, &r);
+        if (rc != CBH_OK) die(context(), rc, "cbh_merge");
+        for (size_t i = g0; i < g0 + k; ++i) cbh_mat_free(context(), cur[i]);
+        next.push_back(r);
+      }
+      cur.swap(next);
+    }
+    c.m = cur[0];
+  }
   combblas::SpTuples<IT, NT>* out = download_tuples<IT, NT>(c.m);
   if (delarrs)
     for (auto* l : lists) delete l;
   return out;
+}
+
+// MultiwayMergeHash (MultiwayMerge.h:536-684): same contract; inputs may have unsorted rows inside
+// a column, the output has rows ascending (a valid order for sorted=false as well)
+template <class SR, class IT, class NT>
+combblas::SpTuples<IT, NT>* MultiwayMergeHash(std::vector<combblas::SpTuples<IT, NT>*>& lists, IT mdim = 0,
+                                              IT ndim = 0, bool delarrs = false, bool sorted = true) {
+  (void)sorted;
+  return combblas_hip::MultiwayMerge<SR, IT, NT>(lists, mdim, ndim, delarrs, true);
 }
 
 }  // namespace combblas_hip
@@ -265,5 +320,10 @@ combblas::SpTuples<IT, NT>* MultiwayMerge(std::vector<combblas::SpTuples<IT, NT>
   inline SpTuples<IT, NT>* MultiwayMerge<SR, IT, NT>(std::vector<SpTuples<IT, NT>*> & L, IT mdim, IT ndim,    \
                                                      bool delarrs) {                                          \
     return combblas_hip::MultiwayMerge<SR, IT, NT>(L, mdim, ndim, delarrs);                                  \
+  }                                                                                                           \
+  template <>                                                                                                 \
+  inline SpTuples<IT, NT>* MultiwayMergeHash<SR, IT, NT>(std::vector<SpTuples<IT, NT>*> & L, IT mdim, IT ndim, \
+                                                         bool delarrs, bool sorted) {                         \
+    return combblas_hip::MultiwayMergeHash<SR, IT, NT>(L, mdim, ndim, delarrs, sorted);                      \
   }                                                                                                           \
   }

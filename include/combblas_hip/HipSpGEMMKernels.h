@@ -82,8 +82,7 @@ combblas::SpTuples<IT, NTO>* DeviceLocalSpGEMM(const combblas::SpDCCols<IT, NT1>
     int rc = cbh_plan_create(ctx, a.m, b.m, &plan);
     if (rc != CBH_OK) die(ctx, rc, "cbh_plan_create");
     cbh_numeric_plan np;
-    rc = cbh_plan_numeric(plan, dtype_of<NTO>::value, (int64_t)sizeof(NTO),
-                          cbh::sr_locked<DSR>::value ? CBH_PLAN_NO_DENSE : 0u, &c.m, &np);
+    rc = cbh_plan_numeric(plan, dtype_of<NTO>::value, (int64_t)sizeof(NTO), cbh::plan_flags<DSR>(), &c.m, &np);
     if (rc != CBH_OK) die(ctx, rc, "cbh_plan_numeric");
     const int64_t *cp, *jc;
     const int32_t* ir;

@@ -27,9 +27,9 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
-#include <map>
 #include <memory>
 #include <vector>
 
@@ -121,11 +121,32 @@ inline void rccl_check(ncclResult_t r, const char* what) {
   }
 }
 
-// ncclComm_t mirroring one MPI communicator (ncclUniqueId from its rank 0 over MPI_Bcast).
+// ncclComm_t mirroring one MPI communicator (ncclUniqueId from its rank 0 over MPI_Bcast). The
+// ncclComm is cached as an MPI attribute of that communicator, so it lives exactly as long as the
+// communicator: the reference's ProductGrid makes a new CommGrid per product and its destructor
+// MPI_Comm_free's the row/column worlds (CommGrid.h:49-56), which runs the delete callback below
+// (ncclCommDestroy). A handle value MPI later reuses for another communicator carries no attribute,
+// so it can never return an ncclComm with the wrong members.
+inline int rccl_comm_delete(MPI_Comm, int, void* attr, void*) {
+  auto* c = static_cast<ncclComm_t*>(attr);
+  (void)hipStreamSynchronize(reinterpret_cast<hipStream_t>(cbh_ctx_stream(context())));
+  ncclCommDestroy(*c);
+  delete c;
+  return MPI_SUCCESS;
+}
+inline int rccl_keyval() {
+  static int kv = [] {
+    int k = MPI_KEYVAL_INVALID;
+    MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, rccl_comm_delete, &k, nullptr);
+    return k;
+  }();
+  return kv;
+}
 inline ncclComm_t rccl_comm_for(MPI_Comm comm) {
-  static std::map<MPI_Comm, ncclComm_t> cache;
-  auto it = cache.find(comm);
-  if (it != cache.end()) return it->second;
+  void* attr = nullptr;
+  int found = 0;
+  MPI_Comm_get_attr(comm, rccl_keyval(), &attr, &found);
+  if (found && attr) return *static_cast<ncclComm_t*>(attr);
   int rank = 0, size = 1;
   MPI_Comm_rank(comm, &rank);
   MPI_Comm_size(comm, &size);
@@ -133,10 +154,10 @@ inline ncclComm_t rccl_comm_for(MPI_Comm comm) {
   if (rank == 0) rccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
   MPI_Bcast(&id, (int)sizeof(id), MPI_BYTE, 0, comm);
   context();  // the context selects this rank's device
-  ncclComm_t c;
-  rccl_check(ncclCommInitRank(&c, size, id, rank), "ncclCommInitRank");
-  cache[comm] = c;
-  return c;
+  auto* c = new ncclComm_t;
+  rccl_check(ncclCommInitRank(c, size, id, rank), "ncclCommInitRank");
+  MPI_Comm_set_attr(comm, rccl_keyval(), c);
+  return *c;
 }
 
 // SpParHelper::BCastMatrix (SpParHelper.cpp:581-599) on device blocks: non-root ranks allocate
@@ -212,6 +233,30 @@ cbh_mat* local_multiply(const cbh_mat* A, const cbh_mat* B) {
   return C;
 }
 
+// MultiwayMerge of any number of device partials (MultiwayMerge.h:411-526 takes any count): one
+// cbh_merge per group of at most kMaxLists (16) lists, the group results merged again until one
+// is left; every input and intermediate is freed. Takes ownership of `parts` (non-empty).
+inline cbh_mat* merge_all(cbh_semiring sr, std::vector<cbh_mat*> parts) {
+  constexpr size_t kGroup = 16;  // cbh_merge's list limit (kMaxLists)
+  while (parts.size() > 1) {
+    std::vector<cbh_mat*> next;
+    for (size_t g = 0; g < parts.size(); g += kGroup) {
+      const size_t k = std::min(kGroup, parts.size() - g);
+      if (k == 1) {
+        next.push_back(parts[g]);
+        continue;
+      }
+      cbh_mat* C = nullptr;
+      int rc = cbh_merge(context(), sr, (int)k, parts.data() + g, &C);
+      if (rc != CBH_OK) die(context(), rc, "cbh_merge");
+      for (size_t i = g; i < g + k; ++i) cbh_mat_free(context(), parts[i]);
+      next.push_back(C);
+    }
+    parts.swap(next);
+  }
+  return parts[0];
+}
+
 // SpParMat<.., SpDCCols> <-> SpParMat<.., SpDCColsDev>: one upload / download of the local block
 template <class IT, class NT>
 combblas::SpParMat<IT, NT, SpDCColsDev<IT, NT>> to_device(combblas::SpParMat<IT, NT, combblas::SpDCCols<IT, NT>>& A) {
@@ -276,10 +321,7 @@ SpParMat<IU, NUO, UDERO> Mult_AnXBn_Synch(SpParMat<IU, NU1, combblas_hip::SpDCCo
   } else if (tomerge.size() == 1) {
     C = tomerge[0];  // one partial: it is the product (no copy round trip)
   } else {
-    int rc = cbh_merge(combblas_hip::context(), combblas_hip::semiring_traits<SR>::code, (int)tomerge.size(),
-                       tomerge.data(), &C);
-    if (rc != CBH_OK) combblas_hip::die(combblas_hip::context(), rc, "cbh_merge");
-    for (cbh_mat* p : tomerge) cbh_mat_free(combblas_hip::context(), p);
+    C = combblas_hip::merge_all(combblas_hip::semiring_traits<SR>::code, tomerge);
   }
   return SpParMat<IU, NUO, UDERO>(new UDERO(C), GridC);
 }

@@ -18,25 +18,27 @@ struct TSymSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 struct TSymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512, U = 8; };
 // mid-size symbolic tasks (kSmallCap < products <= kSymMidCap): one sub-tile in a 16 KB key
 // table, five workgroups per CU, so the per-task setup latency overlaps
-#ifndef CBH_SYMMID
-#define CBH_SYMMID 2048
-#endif
-struct TSymMid { static constexpr int T = 2 * CBH_SYMMID, BS = 256, EMAX = 256, U = 4; };
+constexpr int kSymMid = 2048;  // (1024 / 4096 measured no better)
+struct TSymMid { static constexpr int T = 2 * kSymMid, BS = 256, EMAX = 256, U = 4; };
 struct TNumSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 // (T = 8192 with 1024-thread groups, one per CU: 89.1 vs 98.2 GFLOP/s at scale 22)
 struct TNumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512, U = 8; };
 // mid-size hash tasks (kSmallCap < outputs <= kMidCap) of the library's A^2 path: a quarter of the
 // large kernel's LDS, so four workgroups share a CU and the per-task setup latency overlaps
-#ifndef CBH_MIDCAP
-#define CBH_MIDCAP 1024
-#endif
-struct TNumMid { static constexpr int T = 2 * CBH_MIDCAP, BS = 256, EMAX = 256, U = 4; };
+constexpr int kMidOut = 1024;  // (512 / 2048 measured no better)
+struct TNumMid { static constexpr int T = 2 * kMidOut, BS = 256, EMAX = 256, U = 4; };
 // wider accumulators (user value types) keep the large table within ~50 KB of LDS
 template <class SR>
 struct TNumLargeFor {
   static constexpr int bytes = (int)(sizeof(int32_t) + sizeof(typename SR::acc_t));
   static constexpr int T = bytes <= 12 ? 4096 : (bytes <= 24 ? 2048 : (bytes <= 48 ? 1024 : 512));
   static constexpr int BS = 512, EMAX = 512, U = 8;
+};
+template <class SR>
+struct TNumMidFor {
+  static constexpr int bytes = (int)(sizeof(int32_t) + sizeof(typename SR::acc_t));
+  static constexpr int T = bytes <= 12 ? 2 * kMidOut : (bytes <= 24 ? kMidOut : 512);
+  static constexpr int BS = 256, EMAX = 256, U = 4;
 };
 template <class SR>
 struct TNumSmallFor {
@@ -46,8 +48,8 @@ struct TNumSmallFor {
 };
 constexpr int64_t kChunkMin = 256;  // tasks with more B entries than this keep cursors in HBM
 constexpr int64_t kSmallCap = 256;  // numeric tasks with <= kSmallCap outputs run the small kernel
-constexpr int64_t kMidCap = CBH_MIDCAP;  // ... with <= kMidCap the mid kernel (library numeric pass)
-constexpr int64_t kSymMidCap = CBH_SYMMID;  // symbolic tasks with <= kSymMidCap products: the mid kernel
+constexpr int64_t kMidCap = kMidOut;  // ... with <= kMidCap the mid kernel (library numeric pass)
+constexpr int64_t kSymMidCap = kSymMid;  // symbolic tasks with <= kSymMidCap products: the mid kernel
 static_assert(kChunkMin <= TSymSmall::EMAX && kChunkMin <= TSymMid::EMAX && kChunkMin <= TSymLarge::EMAX &&
                   kChunkMin <= TNumSmall::EMAX && kChunkMin <= TNumMid::EMAX &&
                   kChunkMin <= TNumLarge::EMAX,
@@ -119,19 +121,35 @@ inline TaskArgs numeric_args(const cbh_numeric_plan& p, int64_t cbase, int32_t* 
   return a;
 }
 
-// The numeric pass of a plan for semiring SR: dense tasks (if the plan binned any: built-in,
-// lock-free semirings only), hash tasks of the large and the small kernel, all on the plan's
-// stream. C is the matrix cbh_plan_numeric allocated.
+// The dense (bitmap-rank) kernel accumulates with SR::lds_acc, so it needs a lock-free add, and the
+// library's dense split (cbh_plan_numeric, dense_split_kernel) is computed for the CAPD / NWB
+// layout of 8-byte accumulators: other semirings plan with CBH_PLAN_NO_DENSE.
+template <class SR>
+constexpr bool dense_capable() {
+  return !sr_locked<SR>::value && sizeof(typename SR::acc_t) == 8;
+}
+template <class SR>
+constexpr uint32_t plan_flags() {
+  return dense_capable<SR>() ? 0u : CBH_PLAN_NO_DENSE;
+}
+
+// The numeric pass of a plan for semiring SR: dense tasks (if the plan binned any), hash tasks of
+// the large, mid and small kernels, all on the plan's stream. C is the matrix cbh_plan_numeric
+// allocated with plan_flags<SR>().
 template <class SR>
 hipError_t run_numeric_plan(const cbh_numeric_plan& p, int32_t* Cir, void* Cnum, int64_t ccap) {
   const TaskArgs a = numeric_args(p, 0, Cir, Cnum, ccap);
   hipStream_t s = reinterpret_cast<hipStream_t>(p.stream);
   hipError_t e = hipSuccess;
-  if constexpr (!sr_locked<SR>::value) {
+  if constexpr (dense_capable<SR>()) {
     e = launch_tasks<SR, TNumLarge, MODE_TDENSE>(a, p.dense_first, p.dense_count, s);
     if (e != hipSuccess) return e;
+  } else if (p.dense_count > 0) {
+    return hipErrorInvalidValue;  // planned without CBH_PLAN_NO_DENSE
   }
   e = launch_tasks<SR, TNumLargeFor<SR>, MODE_TNUM>(a, p.large_first, p.large_count, s);
+  if (e != hipSuccess) return e;
+  e = launch_tasks<SR, TNumMidFor<SR>, MODE_TNUM>(a, p.mid_first, p.mid_count, s);
   if (e != hipSuccess) return e;
   return launch_tasks<SR, TNumSmallFor<SR>, MODE_TNUM>(a, p.small_first, p.small_count, s);
 }

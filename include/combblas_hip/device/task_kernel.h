@@ -42,19 +42,20 @@ constexpr int kSymWords = 13312;  // bitmap words of the large symbolic configur
 // numeric sub-tile: planned outputs, in eighths of the T home slots (3/8 and 5/8 measured slower:
 // 97.6 and 93.5 vs 98.6 GFLOP/s at scale 22)
 constexpr int kFill8 = 4;
-// dense numeric sub-tile capacity in quarters of T (build knob for the A/B; 3 = 3072 values)
-#ifndef CBH_CAPD4
-#define CBH_CAPD4 3
-#endif
-// a task runs dense when its dense sub-tiles are at most CBH_DRATIO4/4 of its hash sub-tiles
-#ifndef CBH_DRATIO4
-#define CBH_DRATIO4 5
-#endif
+// dense numeric sub-tile capacity in quarters of T: 3 = 3072 values for T = 4096 (2 and 4
+// measured slower: 98.7 / 104.5 vs 105.3 GFLOP/s at scale 22)
+constexpr int kCapD4 = 3;
+// a task runs dense when its dense sub-tiles are at most kDRatio4/4 of its hash sub-tiles (4, 6,
+// 8 and 12 measured no better)
+constexpr int kDRatio4 = 5;
 
 // Diagnostic build only (-DCBH_STAMPS, libcombblas_hip_stamps.so): thread 0 of every workgroup
 // adds the s_memtime cycles of each kernel phase (delimited by block barriers) into g_stamps.
 #ifdef CBH_STAMPS
-__device__ unsigned long long g_stamps[16];
+// [0..11] phase cycles, [12] workgroups, [13] chunk-subtiles, [14] overflows, [15] products,
+// [16] entry visits, [17] active entry visits, [18] active entries whose segment ends inside the
+// 8-row window (short), [19] products of those, [20] hash sub-tile occupied slots (commit)
+__device__ unsigned long long g_stamps[24];
 #define CBH_STAMP(k)                                    \
   do {                                                  \
     if (threadIdx.x == 0) {                             \
@@ -259,7 +260,7 @@ __host__ __device__ inline int64_t dense_subtiles(int64_t work, int64_t span, in
   int64_t Rd = (work + cd - 1) / cd;
   const int64_t Rw = (span + 32 * nwb - 1) / (32 * nwb);
   Rd = Rd > Rw ? Rd : Rw;
-  return 4 * Rd <= CBH_DRATIO4 * R ? Rd : 0;
+  return 4 * Rd <= kDRatio4 * R ? Rd : 0;
 }
 
 template <class SR, int T, int BS, int EMAX, int U, int MODE>
@@ -287,7 +288,7 @@ struct TaskCfg {
   // output rows are not stored: the commit reads them off the bitmap), then the rest of both
   // tables is the bitmap (NWB words) followed by the int16 prefix popcount of every word --
   // 32*NWB rows per sub-tile (CAPD 3072 and 135 K rows for T = 4096 with f64)
-  static constexpr int CAPD = T / 4 * CBH_CAPD4;
+  static constexpr int CAPD = T / 4 * kCapD4;
   static constexpr size_t o_dvals = o_keys;
   static constexpr size_t o_dbits = al(o_dvals + sizeof(acc_t) * CAPD);
   static constexpr int NWB = NUM ? (int)((o_pos - o_dbits) / 6) / 8 * 8 : 0;
@@ -348,6 +349,7 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
 #ifdef CBH_STAMPS
   uint64_t st_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t t_prev_ = __builtin_amdgcn_s_memtime();
+  unsigned long long dg_active = 0, dg_short = 0, dg_shortp = 0;
 #endif
   if ((int64_t)blockIdx.x >= a.norder) return;
   const int32_t task = a.order[blockIdx.x];
@@ -498,12 +500,18 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
   // then the exclusive scan of the segment lengths; epos becomes the gather base (cursor - offset).
   // Returns the sub-tile's product count P.
   auto segments = [&](int nec, int32_t hi, bool hi_is_end) -> int {
+#ifdef CBH_STAMPS
+    if (tid == 0) atomicAdd(&g_stamps[16], (unsigned long long)nec);
+#endif
     for (int i = tid; i < nec; i += BS) {
       const int32_t nx = enext[i];
       const int64_t p = epos[i];
       int64_t stop = p;
       int32_t nx2 = nx;
       if (nx < hi) {
+#ifdef CBH_STAMPS
+        dg_active++;
+#endif
         const int64_t end = eend[i];
         if (hi_is_end) {
           stop = end;
@@ -516,6 +524,12 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
       }
       eoff[i] = (int32_t)(stop - p);
       enext2[i] = nx2;
+#ifdef CBH_STAMPS
+      if (nx < hi && stop - p < 8) {
+        dg_short++;
+        dg_shortp += (unsigned long long)(stop - p);
+      }
+#endif
     }
     __syncthreads();
     CBH_STAMP(2);
@@ -907,6 +921,9 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
         }
       }
       out_pos += qtot;
+#ifdef CBH_STAMPS
+      if (tid == 0) atomicAdd(&g_stamps[20], (unsigned long long)qtot);
+#endif
     }
     lo = hi;
     w = wnom;
@@ -926,6 +943,9 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
     for (int k = 0; k < 12; ++k) atomicAdd(&g_stamps[k], (unsigned long long)st_[k]);
     atomicAdd(&g_stamps[12], 1ull);
   }
+  if (dg_active) atomicAdd(&g_stamps[17], dg_active);
+  if (dg_short) atomicAdd(&g_stamps[18], dg_short);
+  if (dg_shortp) atomicAdd(&g_stamps[19], dg_shortp);
 #endif
 }
 

@@ -1,0 +1,155 @@
+// Drop-in test of the reference's PHASED and 3D drivers (built by `make -C oracle ref` into
+// oracle/_ref/dropin3d_harness, g++ like the reference). Run under mpirun with 1, 2, 4 or 8 ranks
+// sharing one GPU (each rank its own HIP context; OMP_NUM_THREADS=1).
+//
+// Every case runs the reference's UNCHANGED driver twice on the same R-MAT input: once with
+// PlusTimesSRing<double,double>, whose local kernels COMBBLAS_HIP_INSTANTIATE routes to the gfx950
+// path (LocalSpGEMMHash, LocalSpGEMM, MultiwayMerge, MultiwayMergeHash, through the C-ABI), once
+// with a value-identical semiring that is not specialized (the stock OpenMP kernels):
+//   MemEfficientSpGEMM      ParFriends.h:449-730   (2D, square process counts; hash and heap
+//                           kernels, 1 and 3 phases, with MCLPruneRecoverySelect :185-353)
+//   Mult_AnXBn_SUMMA3D      ParFriends.h:2918-3208 (SpParMat3D, layers from argv; the fiber
+//                           reduce-scatter :3097-3183 merges with MultiwayMergeHash)
+//   MemEfficientSpGEMM3D    ParFriends.h:3214-3705 (hash and heap kernels, 2 phases, prune)
+// The results (Convert2D for the 3D ones) must hold the same entries on every rank. The stock hash
+// kernels leave rows unsorted inside a column (mtSpGEMM.h:624-634, MultiwayMergeHash sorted=false),
+// so each local column is compared as a sorted set; values are R-MAT edge multiplicities, so every
+// double sum is exact.
+//   dropin3d_harness <scale> <layers>  -> "DROPIN3D <case> OK nnz=... ranks=..." lines, exit 0 on success
+#include <mpi.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <memory>
+#include <utility>
+#include <vector>
+
+#include "CombBLAS/CombBLAS.h"
+#include "CombBLAS/CommGrid3D.h"
+#include "CombBLAS/SpParMat3D.h"
+#include "combblas_hip/HipSpGEMM.h"
+
+using namespace combblas;
+
+double cblas_alltoalltime, cblas_allgathertime, cblas_mergeconttime, cblas_transvectime, cblas_localspmvtime;
+double mcl_Abcasttime, mcl_Bbcasttime, mcl_localspgemmtime, mcl_multiwaymergetime, mcl_kselecttime,
+    mcl_prunecolumntime, mcl_symbolictime, mcl3d_conversiontime, mcl3d_symbolictime, mcl3d_Abcasttime,
+    mcl3d_Bbcasttime, mcl3d_SUMMAtime, mcl3d_localspgemmtime, mcl3d_SUMMAmergetime, mcl3d_reductiontime,
+    mcl3d_3dmergetime, mcl3d_kselecttime, mcl3d_totaltime, mcl3d_floptime, mcl3d_proc_flop_mean, mcl3d_proc_flop_std,
+    mcl3d_proc_nnzc_pre_red, mcl3d_proc_nnzc_post_red;
+int64_t mcl_memory, mcl3d_layer_flop, mcl3d_layer_nnzc, mcl3d_nnzc, mcl3d_flop, mcl3d_max_proc_flop,
+    mcl3d_max_proc_nnzc_pre_red, mcl3d_max_proc_nnzc_post_red;
+MTRand GlobalMT(123);
+
+struct CpuPlusTimes {  // PlusTimesSRing<double,double> on the stock path
+  static double id() { return 0; }
+  static bool returnedSAID() { return false; }
+  static MPI_Op mpi_op() { return MPI_SUM; }
+  static double add(const double& a, const double& b) { return a + b; }
+  static double multiply(const double& a, const double& b) { return a * b; }
+  static void axpy(double a, const double& x, double& y) { y += a * x; }
+};
+typedef PlusTimesSRing<double, double> PTDD;
+COMBBLAS_HIP_INSTANTIATE(PTDD, int64_t, double)
+
+typedef SpDCCols<int64_t, double> DCols;
+typedef SpParMat<int64_t, double, DCols> PMat;
+typedef SpParMat3D<int64_t, double, DCols> PMat3D;
+
+// the local block's columns as sorted (row, value) sets
+static std::vector<std::pair<int64_t, std::vector<std::pair<int64_t, double>>>> columns(DCols& M) {
+  std::vector<std::pair<int64_t, std::vector<std::pair<int64_t, double>>>> out;
+  for (auto colit = M.begcol(); colit != M.endcol(); ++colit) {
+    std::vector<std::pair<int64_t, double>> col;
+    for (auto nzit = M.begnz(colit); nzit != M.endnz(colit); ++nzit) col.emplace_back(nzit.rowid(), nzit.value());
+    std::sort(col.begin(), col.end());
+    if (!col.empty()) out.emplace_back(colit.colid(), std::move(col));
+  }
+  return out;
+}
+
+static int report(const char* name, PMat& Ch, PMat& Cc, double hip_s, double cpu_s) {
+  int myrank, nprocs;
+  MPI_Comm_rank(MPI_COMM_WORLD, &myrank);
+  MPI_Comm_size(MPI_COMM_WORLD, &nprocs);
+  int bad = (columns(Ch.seq()) == columns(Cc.seq())) ? 0 : 1;
+  if (Ch.getnrow() != Cc.getnrow() || Ch.getncol() != Cc.getncol()) bad = 1;
+  int anybad = 0;
+  MPI_Allreduce(&bad, &anybad, 1, MPI_INT, MPI_MAX, MPI_COMM_WORLD);
+  const int64_t nnz = Ch.getnnz(), nnzc = Cc.getnnz();  // collective
+  if (nnz != nnzc) anybad = 1;
+  if (myrank == 0) {
+    std::printf("DROPIN3D %s %s nnz=%lld ranks=%d hip_s=%.3f cpu_s=%.3f\n", name, anybad ? "MISMATCH" : "OK",
+                (long long)nnz, nprocs, hip_s, cpu_s);
+    std::fflush(stdout);
+  }
+  return anybad;
+}
+
+static bool is_square(int p) {
+  const int r = (int)std::lround(std::sqrt((double)p));
+  return r * r == p;
+}
+
+int main(int argc, char** argv) {
+  int provided;
+  MPI_Init_thread(&argc, &argv, MPI_THREAD_SERIALIZED, &provided);
+  const int scale = argc > 1 ? std::atoi(argv[1]) : 10;
+  const int layers = argc > 2 ? std::atoi(argv[2]) : 0;
+  int nprocs;
+  MPI_Comm_size(MPI_COMM_WORLD, &nprocs);
+  int bad = 0;
+  {  // every CombBLAS object must be destroyed before MPI_Finalize
+    double init[4] = {.57, .19, .19, .05};
+    DistEdgeList<int64_t>* DEL = new DistEdgeList<int64_t>();
+    DEL->GenGraph500Data(init, scale, 16, true, true);
+    SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>> G(*DEL, false);
+    delete DEL;
+    PMat A(G), B(G);
+    // MCLPruneRecoverySelect parameters: keep entries > 1.5, select the 40 largest per column,
+    // recover up to 60 when the kept mass falls under 90 %
+    const double hard = 1.5, pct = 0.9;
+    const int64_t sel = 40, rec = 60;
+    if (is_square(nprocs)) {
+      for (int kernel : {1, 2})
+        for (int phases : {1, 3}) {
+          char name[96];
+          std::snprintf(name, sizeof(name), "MemEfficientSpGEMM<kernel=%d,phases=%d,prune>", kernel, phases);
+          double t0 = MPI_Wtime();
+          PMat Ch = MemEfficientSpGEMM<PTDD, double, DCols>(A, B, phases, hard, sel, rec, pct, 1, kernel, 0);
+          double t1 = MPI_Wtime();
+          PMat Cc = MemEfficientSpGEMM<CpuPlusTimes, double, DCols>(A, B, phases, hard, sel, rec, pct, 1, kernel, 0);
+          double t2 = MPI_Wtime();
+          bad += report(name, Ch, Cc, t1 - t0, t2 - t1);
+        }
+    }
+    if (layers > 0 && nprocs % layers == 0 && is_square(nprocs / layers)) {
+      PMat3D A3(A, layers, true, false), B3(B, layers, false, false);
+      {
+        double t0 = MPI_Wtime();
+        PMat3D C3h = Mult_AnXBn_SUMMA3D<PTDD, double, DCols, int64_t, double, double, DCols, DCols>(A3, B3);
+        double t1 = MPI_Wtime();
+        PMat3D C3c = Mult_AnXBn_SUMMA3D<CpuPlusTimes, double, DCols, int64_t, double, double, DCols, DCols>(A3, B3);
+        double t2 = MPI_Wtime();
+        PMat Ch = C3h.Convert2D(), Cc = C3c.Convert2D();
+        bad += report("Mult_AnXBn_SUMMA3D", Ch, Cc, t1 - t0, t2 - t1);
+      }
+      for (int kernel : {1, 2}) {
+        char name[96];
+        std::snprintf(name, sizeof(name), "MemEfficientSpGEMM3D<kernel=%d,phases=2,prune>", kernel);
+        double t0 = MPI_Wtime();
+        PMat3D C3h = MemEfficientSpGEMM3D<PTDD, double, DCols, int64_t, double, double, DCols, DCols>(
+            A3, B3, 2, hard, sel, rec, pct, 1, kernel, 0);
+        double t1 = MPI_Wtime();
+        PMat3D C3c = MemEfficientSpGEMM3D<CpuPlusTimes, double, DCols, int64_t, double, double, DCols, DCols>(
+            A3, B3, 2, hard, sel, rec, pct, 1, kernel, 0);
+        double t2 = MPI_Wtime();
+        PMat Ch = C3h.Convert2D(), Cc = C3c.Convert2D();
+        bad += report(name, Ch, Cc, t1 - t0, t2 - t1);
+      }
+    }
+  }
+  MPI_Finalize();
+  return bad ? 1 : 0;
+}

@@ -37,20 +37,44 @@ def _dc(res):
     return H.Dcsc(*res[:2], *res[2:])
 
 
-def _galerkin_worker(rank, world):
+def _backend(kind):
+    """local-block operations: the CPU oracle (this file) or the gfx950 kernels with every rank
+    sharing cuda:0 (tests/test_apps_dist_gpu.py; the collectives stay on gloo)"""
+    if kind == "oracle":
+        return OracleBackend(), None
+    import torch
+
+    import combblas_amd as cb
+    from combblas_amd.backend import HipBackend
+
+    torch.cuda.set_device(0)
+    ctx = cb.Context(0)
+    return HipBackend(ctx), ctx
+
+
+def _close(ctx):
+    if ctx is not None:
+        import torch
+
+        torch.cuda.synchronize()
+        ctx.close()
+
+
+def _galerkin_worker(rank, world, kind="oracle"):
     from combblas_amd import parfriends as pf
     from combblas_amd.commgrid import CommGrid
     from combblas_amd.galerkin import poisson27, prolongation, transpose
     from combblas_amd.semirings import PlusTimesSRing
     from combblas_amd.spparmat import SpParMat
 
-    be, grid = OracleBackend(), CommGrid()
+    (be, ctx), grid = _backend(kind), CommGrid()
     A = SpParMat.distribute(poisson27(8), grid, be)
     T = SpParMat.distribute(prolongation(8), grid, be)
     S = SpParMat.distribute(transpose(prolongation(8)), grid, be)
     AT = pf.PSpGEMM(PlusTimesSRing, A, T)
     SAT = pf.PSpGEMM(PlusTimesSRing, S, AT)
     g = SAT.gather_host()
+    _close(ctx)
     return _out(g) if rank == 0 else None
 
 
@@ -81,13 +105,13 @@ def test_tc_2x2_vs_reference(apps, apps_meta):
     assert int(got.num.sum()) == apps_meta["tc"]["10"]["triangles"] == 78452
 
 
-def _mcl_worker(rank, world, mode, params, phases, ppm=0):
+def _mcl_worker(rank, world, mode, params, phases, ppm=0, kind="oracle"):
     from combblas_amd import parfriends as pf
     from combblas_amd.commgrid import CommGrid, CommGrid3D
     from combblas_amd.semirings import PlusTimesSRing
     from combblas_amd.spparmat import SpParMat, SpParMat3D
 
-    be = OracleBackend()
+    be, ctx = _backend(kind)
     A = _h(H.load_npz(os.path.join(H.GOLDEN, "apps.npz"))["mcl_A"])
     hard, sel, rec, pct = params
     res = []
@@ -103,6 +127,7 @@ def _mcl_worker(rank, world, mode, params, phases, ppm=0):
             dA, dB = SpParMat.distribute(A, grid, be), SpParMat.distribute(A, grid, be)
             C = pf.MemEfficientSpGEMM(PlusTimesSRing, dA, dB, phases=phases, perProcessMemory=ppm, **kw)
         res.append(C.gather_host())
+    _close(ctx)
     return (_out(res[0]), _out(res[1])) if rank == 0 else None
 
 
@@ -112,9 +137,17 @@ def _mcl_worker(rank, world, mode, params, phases, ppm=0):
 @pytest.mark.parametrize("mode,world,phases,ppm", [("2d", 4, 3, 0), ("3d", 8, 2, 0), ("2d", 4, 0, 96 * 1024),
                                                     ("3d", 8, 0, 64 * 1024)])
 def test_mcl_prune_distributed(apps, apps_meta, mode, world, phases, ppm):
+    check_mcl(apps, apps_meta, mode, run_world(_mcl_worker, world, mode, mcl_params(apps_meta), phases, ppm))
+
+
+def mcl_params(apps_meta):
     p = apps_meta["mcl"]["0"]
-    params = (p["hard"], p["select"], p["recover"], p["pct"])
-    raw, pruned = run_world(_mcl_worker, world, mode, params, phases, ppm)
+    return (p["hard"], p["select"], p["recover"], p["pct"])
+
+
+def check_mcl(apps, apps_meta, mode, res):
+    params = mcl_params(apps_meta)
+    raw, pruned = res
     A2, got = _dc(raw), _dc(pruned)
     ref = apps["mcl_A2"]
     assert np.array_equal(A2.jc, ref.jc) and np.array_equal(A2.cp, ref.cp) and np.array_equal(A2.ir, ref.ir)

@@ -1,0 +1,84 @@
+"""GPU regression tests for the two device faults of round 2, each forcing the shipped code path
+that faulted ("What's weak" 2):
+
+1. A large numeric HASH sub-tile that inserts without a probe overflow but occupies more slots
+   than the commit queue holds (WIN = U*BS = 4096 of the TA = 4160 slots). It must be retried with
+   half the row range from the cursors BEFORE the segment scan (fixed in 633d2f2; before, the
+   retry read out of range). Construction, for TNumLarge (T 4096, 512 threads, U 8):
+     one output column with 4101 outputs: rows 64*m (m < 4100) plus one row at 3*X - 1,
+     X = 4100*64 = 262400 -> one task (4101 products <= kTaskFlops) spanning 787200 rows;
+     dense_subtiles(4101, 787200, ...) = 0 (6 bitmap sub-tiles > 5/4 of 3 hash sub-tiles), so it
+     runs on the hash kernel with R = ceil(4101 / 2048) = 3 sub-tiles of 262400 rows; the first
+     holds all 4100 evenly spaced rows (slot = 64*m*4096/262400: at most 2 rows per home slot,
+     probes of 1-2) -> 4100 occupied slots > 4096 queue entries, no probe overflow -> retry.
+   Variants: the column's products from ONE B entry (cursors in LDS) and from 600 B entries
+   (> EMAX = 512: chunked, cursors double-buffered in HBM); f64 and int64 values.
+2. The TC dot-form piece kernels are wave-strided with a capped grid (an AQL dispatch counts
+   work-items in 32 bits; scale 22 overflowed the direct grid, fixed in 2b52875). The test-only
+   CBH_TEST_GRID_CAP lowers the cap to 1 block (4 waves) so that scale 12/14 runs many strides
+   per wave; the result must equal the reference's C (tests/golden/tc.json digests).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+X = 4100 * 64  # rows of the first hash sub-tile
+
+
+def _queue_overflow_operands(nentries, dtype, seed):
+    rng = np.random.default_rng(seed)
+    m = 3 * X
+    rows = np.concatenate([np.arange(4100, dtype=np.int64) * 64, [m - 1]])
+    owner = np.concatenate([np.arange(4100) % nentries, [nentries - 1]])  # A column of each row
+    order = np.lexsort((rows, owner))
+    rows, owner = rows[order], owner[order]
+    vals = rng.integers(1, 9, rows.size).astype(dtype) * (1 if dtype == np.int64 else 0.5)
+    cp = np.searchsorted(owner, np.arange(nentries + 1)).astype(np.int64)
+    A = H.Dcsc(m, nentries, np.arange(nentries, dtype=np.int64), cp, rows.astype(np.int32), vals.astype(dtype))
+    bv = rng.integers(1, 5, nentries).astype(dtype) * (1 if dtype == np.int64 else 0.25)
+    B = H.Dcsc(nentries, 1, np.zeros(1, np.int64), np.array([0, nentries], np.int64),
+               np.arange(nentries, dtype=np.int32), bv.astype(dtype))
+    return A, B
+
+
+@pytest.mark.parametrize("nentries", [1, 600])
+@pytest.mark.parametrize("dtype", [np.float64, np.int64])
+def test_hash_commit_queue_only_overflow(ctx, oracle, nentries, dtype):
+    import combblas_amd as cb
+
+    A, B = _queue_overflow_operands(nentries, dtype, 7 + nentries)
+    dA = cb.SpDCCols.from_host(ctx, cb.HostDcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num))
+    dB = cb.SpDCCols.from_host(ctx, cb.HostDcsc(B.m, B.n, B.jc, B.cp, B.ir, B.num))
+    C = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dA, dB)
+    h = C.to_host()
+    got = H.Dcsc(h.m, h.n, h.jc, h.cp, h.ir, h.num)
+    exp = oracle.spgemm(A, B, "plus_times", "hybrid")
+    assert exp.nnz == 4101
+    H.assert_dcsc_equal(got, exp, msg=f"queue-only overflow, {nentries} B entries, {np.dtype(dtype).name}")
+    for S in (C, dA, dB):
+        S.free()
+
+
+@pytest.mark.parametrize("scale", [12, 14])
+def test_tc_dot_grid_cap_strides(ctx, scale, monkeypatch):
+    from combblas_amd.apps import MaskedSpGEMM, TCLower
+    from combblas_amd.semirings import PlusTimesSRing
+
+    with open(os.path.join(H.GOLDEN, "tc.json")) as f:
+        ref = json.load(f)["scales"][str(scale)]
+    monkeypatch.setenv("CBH_TEST_GRID_CAP", "1")  # 4 waves stride over every piece
+    L, L2 = TCLower(ctx, scale), TCLower(ctx, scale)
+    C = MaskedSpGEMM(PlusTimesSRing, L, L2, L, method="dot")
+    h = C.to_host()
+    c = H.Dcsc(h.m, h.n, h.jc, h.cp, h.ir, h.num)
+    vs, dg = H.digest(c)
+    assert (c.nnz, c.nzc) == (ref["nnzC"], ref["nzcC"])
+    assert int(c.num.sum()) == ref["triangles"] and vs == ref["sumC"] and dg == int(ref["digestC"])
+    for S in (C, L, L2):
+        S.free()

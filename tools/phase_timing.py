@@ -4,7 +4,7 @@
     python tools/phase_timing.py SCALE NCALLS
 
 Prints one "call i: <ms> ms nnz=<n>" line per call and, last, the per-kernel stats of the final
-call as a dict literal (tools/gpu_ab.sh parses it). With CBH_LIB=stamps CBH_DIAG=1 the library
+call as a dict literal (A/B scripts parse it). With CBH_LIB=stamps CBH_DIAG=1 the library
 prints per-sub-bin launch times and phase cycle shares to stderr.
 """
 from __future__ import annotations

@@ -1,5 +1,5 @@
 """Dev tool: per-launch HBM traffic of one kernel from rocprofv3 --pmc passes (one directory per
-pass, as tools/gpu_diag.sh writes them) -> profiles/pmc_<name>.json, read by bench.py for
+pass, as tools/gpu_bins.sh writes them) -> profiles/pmc_<name>.json, read by bench.py for
 roofline.traffic.
 
 Correction (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7): FETCH_SIZE and WRITE_SIZE are
