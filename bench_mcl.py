@@ -2,9 +2,9 @@
 """bench_mcl.py -- BASELINE.json config C5 on one MI355X: HipMCL's expansion A² followed by
 MCLPruneRecoverySelect (Applications/MCL.cpp:574-577 -> ParFriends.h:449-730 with the prune of
 :185-353), on the protein-similarity-like planted-partition input (combblas_amd.mclgen,
-column-stochastic, ~100 nonzeros per column). The config names n = 2^24 on a 2×2×2 grid of 8 GPUs;
-this line runs the same pipeline on one GPU at n = 2^20 by default (host generation of the input
-takes ~50 s there and grows faster than linearly; the 8-GPU path is MemEfficientSpGEMM3D).
+column-stochastic, ~44 nonzeros per column after symmetrisation), generated on the GPU
+(mclgen.planted_partition_device). The config names n = 2^24 on a 2×2×2 grid of 8 GPUs; this line
+runs the same size and pipeline on one GPU (the 8-GPU path is MemEfficientSpGEMM3D).
 
 One step = parfriends.MemEfficientSpGEMM(PlusTimes, A, A, phases = planned from the exact symbolic
 pass, hardThreshold = 1e-4, selectNum = 1100, recoverNum = 1400, recoverPct = 0.9 -- MCL.cpp's
@@ -15,7 +15,12 @@ Check on a sample of columns: the device expansion of those columns against the 
 (oracle/apps_oracle.py, pinned to the reference's MCLPruneRecoverySelect) of the device's own
 unpruned columns (rows exact, values within 1e-12: the phased product and the sampled product may
 split long columns into different chunk sums).
-    python bench_mcl.py [--log2n 20] [--deg 100] [--steps 2] [--warmup 1]
+
+roofline: the task-kernel class with the most HIP-event time over the timed steps (bench.py's
+kernel_roofline). CPU baseline ("reference"): MCL.cpp's own expansion call MemEfficientSpGEMM
+with MCLPruneRecoverySelect (oracle/_ref/ref_harness mclexp, built from the reference sources) on
+every --cpu-stride-th column of the right operand, 1 rank x host cores, median of 3 after a warm-up.
+    python bench_mcl.py [--log2n 24] [--deg 100] [--steps 2] [--warmup 1] [--host-gen]
 """
 from __future__ import annotations
 
@@ -37,13 +42,50 @@ def log(msg):
     print(f"[bench_mcl] {msg}", file=sys.stderr, flush=True)
 
 
+def reference_baseline(A, flops, stride):
+    """MCL.cpp:574-577's expansion MemEfficientSpGEMM(A, A_s) + MCLPruneRecoverySelect by the
+    reference itself (oracle/_ref/ref_harness mclexp) on A's columns c % stride == 0 as the right
+    operand, 1 rank x host cores; None when oracle/_ref is absent"""
+    import subprocess
+    import tempfile
+
+    ref = os.path.join(HERE, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(ref):
+        return None
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    import helpers as H
+
+    if stride <= 0:
+        stride = max(1, int(flops // 3e8))
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        fa = os.path.join(td, "A.cbm")
+        H.write_cbm(fa, H.Dcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num))
+        env = dict(os.environ, OMP_NUM_THREADS=str(cores), LD_LIBRARY_PATH="/usr/lib/x86_64-linux-gnu:/opt/conda/lib")
+        r = subprocess.run([ref, "mclexp", fa, str(stride), "3", str(HARD), str(SELECT), str(RECOVER), str(PCT)],
+                           env=env, cwd="/tmp", capture_output=True, text=True, timeout=900)
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode != 0 or not line:
+        log(f"reference baseline failed rc={r.returncode}: {r.stderr[-300:]}")
+        return None
+    d = json.loads(line[-1])
+    return {"value": round(d["gflops"], 6), "unit": "GFLOP/s", "cores": d["threads"], "kind": "reference",
+            "sample": f"MCL.cpp's expansion MemEfficientSpGEMM(A, A_s) with MCLPruneRecoverySelect (hard {HARD}, "
+                      f"select {SELECT}, recover {RECOVER}/{PCT}; oracle/_ref built from the reference sources, 1 rank x "
+                      f"{d['threads']} threads) on A's {d['cols']} columns c % {stride} == 0 ({d['flops']} multiplies, "
+                      f"{d['nnz_after_prune']} kept): median of {d['reps']} after 1 warm-up = {d['median_s']:.3f} s"}
+
+
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--log2n", type=int, default=20)
+    p.add_argument("--log2n", type=int, default=24)
     p.add_argument("--deg", type=int, default=100)
     p.add_argument("--steps", type=int, default=2)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--check-cols", type=int, default=100)
+    p.add_argument("--host-gen", action="store_true", help="numpy generator (mclgen.planted_partition)")
+    p.add_argument("--cpu-stride", type=int, default=0, help="0: about 3e8 multiplies in the CPU sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
     args = p.parse_args()
     import torch
 
@@ -51,21 +93,26 @@ def main():
     from combblas_amd import parfriends as pf
     from combblas_amd.backend import HipBackend
     from combblas_amd.commgrid import CommGrid
-    from combblas_amd.mclgen import planted_partition
+    from combblas_amd.mclgen import planted_partition, planted_partition_device
     from combblas_amd.spparmat import SpParMat
 
     torch.cuda.set_device(0)
     n = 1 << args.log2n
+    ctx = cb.Context(0)
+    be = HipBackend(ctx)
+    grid = CommGrid()
     t0 = time.perf_counter()
-    A = planted_partition(n, args.deg, 7)
+    if args.host_gen:
+        A = planted_partition(n, args.deg, 7)
+        dA, dB = SpParMat.distribute(A, grid, be), SpParMat.distribute(A, grid, be)
+    else:
+        gA = planted_partition_device(ctx, n, args.deg, 7)
+        dA, dB = SpParMat(gA, grid, be, n, n), SpParMat(gA.clone(), grid, be, n, n)
+        A = gA.to_host()
     log(f"input: n {n}, nnz {A.nnz} ({time.perf_counter() - t0:.1f} s)")
     colnnz = np.zeros(n, np.int64)
     colnnz[A.jc] = np.diff(A.cp)
     flops = int((np.bincount(A.ir, minlength=n).astype(np.int64) * colnnz).sum())  # sum_k nnz(A(:,k)) nnz(A(k,:))
-    ctx = cb.Context(0)
-    be = HipBackend(ctx)
-    grid = CommGrid()
-    dA, dB = SpParMat.distribute(A, grid, be), SpParMat.distribute(A, grid, be)
     rng = np.random.default_rng(11)
     sample = np.sort(rng.choice(n, size=args.check_cols, replace=False))
     got = {}
@@ -93,6 +140,8 @@ def main():
         step(count)
     ctx.synchronize()
     torch.cuda.synchronize()
+    ctx.reset_kernel_stats()
+    ctx.enable_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         kept["nnz"] = 0
@@ -100,6 +149,10 @@ def main():
     ctx.synchronize()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
+    ctx.enable_timing(False)
+    from bench import kernel_roofline
+
+    roofline = kernel_roofline(ctx.kernel_stats())
     log(f"{args.steps} step(s): {dt * 1e3:.1f} ms/step, {phases} phases, nnz after prune {kept['nnz']}")
     step(keep_sample)  # the sampled pruned columns
 
@@ -114,8 +167,8 @@ def main():
     lens = np.array([d.cp[j + 1] - d.cp[j] for j in sample])
     Bs = H.Dcsc(n, args.check_cols, np.arange(args.check_cols), np.concatenate([[0], np.cumsum(lens)]),
                 d.ir[cols], d.num[cols])
-    hA = cb.HostDcsc(d.m, d.n, d.jc, d.cp, d.ir, d.num)
-    dev = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, cb.SpDCCols.from_host(ctx, hA),
+    dAs = dA.seq if not args.host_gen else cb.SpDCCols.from_host(ctx, cb.HostDcsc(d.m, d.n, d.jc, d.cp, d.ir, d.num))
+    dev = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dAs,
                                cb.SpDCCols.from_host(ctx, cb.HostDcsc(Bs.m, Bs.n, Bs.jc, Bs.cp, Bs.ir, Bs.num))).to_host()
     devC = H.Dcsc(dev.m, dev.n, dev.jc, dev.cp, dev.ir, dev.num)
     ora = H.Oracle().spgemm(d, Bs, "plus_times", "hybrid", threads=int(os.environ.get("OMP_NUM_THREADS", "8")))
@@ -137,30 +190,17 @@ def main():
                          "got_not_expected": int(np.setdiff1d(gr, er).size)}
         elif not np.allclose(gv, ev, rtol=1e-12, atol=0):
             badv += 1
-    # CPU baseline: the oracle expansion + prune of the first n/8 columns (OpenMP over the host cores)
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    nb = n // 8
-    e = int(np.searchsorted(d.jc, nb))
-    Bb = H.Dcsc(n, nb, d.jc[:e], d.cp[:e + 1] - d.cp[0], d.ir[d.cp[0]:d.cp[e]], d.num[d.cp[0]:d.cp[e]])
-    bflops = int(colnnz[Bb.ir].sum())
-    t1 = time.perf_counter()
-    Cb = H.Oracle().spgemm(d, Bb, "plus_times", "hybrid", threads=cores)
-    te = time.perf_counter() - t1
-    AO.mcl_prune_recovery_select(Cb, HARD, SELECT, RECOVER, PCT)
-    tb = time.perf_counter() - t1
-    base = {"value": round(2.0 * bflops / tb / 1e9, 6), "unit": "GFLOP/s", "cores": cores, "kind": "port",
-            "sample": f"columns [0, n/8) ({bflops} flops): CPU oracle expansion (restatement of the reference's "
-                      f"LocalHybridSpGEMM, OpenMP over {cores} threads) + the numpy prune restatement, {tb:.2f} s (expansion alone {te:.2f} s = "
-                      f"{2.0 * bflops / te / 1e9:.4f} GFLOP/s)"}
+    base = None if args.no_cpu_baseline else reference_baseline(A, flops, args.cpu_stride)
     out = {"metric": "HipMCL expansion A^2 + MCLPruneRecoverySelect (C5): semiring GFLOP/s of the expansion",
            "value": round(2.0 * flops / dt / 1e9, 3), "unit": "GFLOP/s", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "dtype": "f64",
-           "data": f"synthetic: planted-partition, column-stochastic, n = 2^{args.log2n}, ~{args.deg} nnz/col",
+           "data": f"synthetic: planted-partition ({'host numpy' if args.host_gen else 'generated on the GPU'}), "
+                   f"column-stochastic, n = 2^{args.log2n}, {args.deg} draws/col",
            "config": {"workload": f"mcl_pp{args.log2n}_deg{args.deg}_A2_prune", "n": n, "nnzA": int(A.nnz),
                       "flops": flops, "phases": phases, "nnz_after_prune": int(kept["nnz"]),
                       "prune": {"hard": HARD, "select": SELECT, "recover": RECOVER, "pct": PCT},
                       "parallelism": "1 GPU (config C5 names 2x2x2)"},
-           "cpu_baseline": base,
+           "roofline": roofline, "cpu_baseline": base,
            "check": {"sample_columns": int(args.check_cols), "expansion_matches_oracle": exp_ok,
                      "pruned_row_mismatches": bad,
                      "pruned_value_mismatches": badv, "first_mismatch": first, "ok": exp_ok and bad == 0 and badv == 0}}

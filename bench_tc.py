@@ -7,10 +7,15 @@ j of L for every mask entry, A transposed on the device inside the step) + the t
 (sum of C). Inputs (L and a second copy, TCLower on the device) are resident in HBM before the
 timed region.
 
-Rate: the reference computes the unmasked L*L first (TC.cpp:109), i.e. flops = sum_k nnz(L(:,k)) *
-nnz(L(k,:)) semiring multiplies, then masks; "value" is that work per second (2 flops per
-multiply-add), the reference-equivalent GFLOP/s. The dot form does not enumerate those products:
-`probes` = sum over mask entries of the shorter list, the elements it actually visits.
+Rate: `probes` = sum over mask entries of the shorter of the two lists the dot form intersects
+(the elements it actually visits); "value" is probes per second (G probes/s). The reference instead
+forms the unmasked L*L first (TC.cpp:109): flops = sum_k nnz(L(:,k)) * nnz(L(k,:)) multiplies, reported
+only as a note ("reference_equivalent_gflops"), since this path never forms those products.
+roofline: 8 algorithmic bytes per probe (the shorter list's row id and the longer list's element it
+is decided against) over the step time -- the dot-form kernels are ~90 % of the step.
+CPU baseline ("reference"): TC.cpp's own flow (oracle/_ref/ref_harness tc) at --cpu-scale (its
+unmasked L*L exhausts a 64 GB host from scale 18), expressed in the same unit (that problem's
+probes / the reference's time); the same-size GPU step is timed beside it ("same_size").
 
 Check: the reference's own C at scales 12-16 is pinned in tests/golden/tc.json (GPU tests); here
 a sample of mask columns of the scale-24 C is recomputed on the host by explicit set
@@ -70,6 +75,7 @@ def cpu_baseline(scale):
     import subprocess
 
     import combblas_amd as cb
+    from combblas_amd.apps import TCLower
 
     ref = os.path.join(HERE, "oracle", "_ref", "ref_harness")
     if not os.path.exists(ref):
@@ -82,16 +88,52 @@ def cpu_baseline(scale):
     if r.returncode != 0 or not line:
         return None
     d = json.loads(line[-1])
-    src, dst = cb.rmat_edges(scale)
-    keep = src != dst
-    key = np.unique(np.concatenate([src[keep] << scale | dst[keep], dst[keep] << scale | src[keep]]))
-    deg = np.bincount(key & ((1 << scale) - 1), minlength=1 << scale).astype(np.int64)
-    flops = int((deg * deg).sum())
-    return {"value": round(2.0 * flops / d["tc_s"] / 1e9, 6), "unit": "GFLOP/s", "cores": d["threads"],
+    # the same problem on the GPU: probes, flops, step time
+    ctx = cb.Context(0)
+    L = TCLower(ctx, scale, 16)
+    L2 = TCLower(ctx, scale, 16)
+    flops, probes = work_of(L)
+    C, tri = tc_step(L, L2)
+    C.free()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        C, tri = tc_step(L, L2)
+        C.free()
+    ctx.synchronize()
+    gdt = (time.perf_counter() - t0) / 3
+    for S in (L, L2):
+        S.free()
+    ctx.close()
+    return {"value": round(probes / d["tc_s"] / 1e9, 6), "unit": "Gprobe/s", "cores": d["threads"],
             "kind": "reference",
             "sample": f"TC.cpp's flow at R-MAT scale {scale} (Mult_AnXBn_Synch(L, L) + EWiseMult + Reduce, 1 rank x "
-                      f"{d['threads']} threads, oracle/_ref built from the reference sources): {d['tc_s']:.3f} s for "
-                      f"{flops} unmasked products, triangles {d['triangles']}"}
+                      f"{d['threads']} threads, oracle/_ref built from the reference sources): {d['tc_s']:.3f} s "
+                      f"({flops} unmasked products = {2.0 * flops / d['tc_s'] / 1e9:.4f} GFLOP/s; that problem has "
+                      f"{probes} dot-form probes), triangles {d['triangles']}",
+            "same_size": {"scale": scale, "gpu_ms_per_step": round(gdt * 1e3, 3), "gpu_triangles": tri,
+                          "ref_triangles": d["triangles"], "speedup": round(d["tc_s"] / gdt, 1)}}
+
+
+def work_of(L):
+    """(unmasked multiplies of L*L, dot-form probes) of TC's L (symmetric pattern)"""
+    import torch
+
+    cp, jc, ir, _ = L.tensors()
+    deg = torch.zeros(L.n, dtype=torch.int64, device=cp.device)
+    deg[jc] = cp[1:] - cp[:-1]
+    flops = int((deg * deg).sum().item())  # symmetric pattern: nnz(L(:,k)) = nnz(L(k,:))
+    colof = torch.repeat_interleave(jc, cp[1:] - cp[:-1])
+    probes = int(torch.minimum(deg[ir.long()], deg[colof]).sum().item())
+    return flops, probes
+
+
+def tc_step(L, L2):
+    from combblas_amd.apps import MaskedSpGEMM
+    from combblas_amd.semirings import PlusTimesSRing
+
+    C = MaskedSpGEMM(PlusTimesSRing, L, L2, L, method="dot")
+    return C, int(C.tensors()[3].sum().item())
 
 
 def main():
@@ -107,8 +149,7 @@ def main():
     import torch
 
     import combblas_amd as cb
-    from combblas_amd.apps import MaskedSpGEMM, TCLower
-    from combblas_amd.semirings import PlusTimesSRing
+    from combblas_amd.apps import TCLower
 
     torch.cuda.set_device(0)
     ctx = cb.Context(0)
@@ -117,18 +158,10 @@ def main():
     L2 = TCLower(ctx, args.scale, args.edgefactor)
     ctx.synchronize()
     log(f"L built on the device: nnz {L.nnz}, {time.perf_counter() - t0:.1f} s")
-    cp, jc, ir, _ = L.tensors()
-    deg = torch.zeros(L.n, dtype=torch.int64, device=cp.device)
-    deg[jc] = cp[1:] - cp[:-1]
-    flops = int((deg * deg).sum().item())  # symmetric pattern: nnz(L(:,k)) = nnz(L(k,:))
-    colof = torch.repeat_interleave(jc, cp[1:] - cp[:-1])
-    probes = int(torch.minimum(deg[ir.long()], deg[colof]).sum().item())
-    del colof
+    flops, probes = work_of(L)
 
     def step():
-        C = MaskedSpGEMM(PlusTimesSRing, L, L2, L, method="dot")
-        tri = int(C.tensors()[3].sum().item())
-        return C, tri
+        return tc_step(L, L2)
 
     for _ in range(args.warmup):
         C, tri = step()
@@ -146,19 +179,31 @@ def main():
     log(f"{args.steps} step(s): {dt * 1e3:.1f} ms/step, triangles {tri}, nnzC {C.nnz}")
     checked, bad = host_check(L, C, args.check_cols)
     vsum, dig = C.checksum()
-    out = {"metric": "TC (L*L).*L on R-MAT: reference-equivalent semiring GFLOP/s (C4)",
-           "value": round(2.0 * flops / dt / 1e9, 3), "unit": "GFLOP/s", "n_gpus": 1, "steps": args.steps,
+    nnzL = L.nnz
+    for S in (L, L2):
+        S.free()
+    ach = 8.0 * probes / dt / 1e9
+    out = {"metric": "TC (L*L).*L on R-MAT (C4): G probes/s of the dot-form masked SpGEMM",
+           "value": round(probes / dt / 1e9, 3), "unit": "Gprobe/s", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "dtype": "int64",
            "data": "synthetic: packed Graph500 R-MAT (seed 0xDECAFBAD), TC.cpp's L built on the device",
            "config": {"workload": f"tc_rmat{args.scale}_ef{args.edgefactor}_masked_LxL_PlusTimes_i64",
-                      "scale": args.scale, "nnzL": L.nnz, "flops_unmasked": flops, "probes": probes,
-                      "probes_per_s": round(probes / dt, 1), "method": "dot"},
+                      "scale": args.scale, "nnzL": nnzL, "flops_unmasked": flops, "probes": probes,
+                      "method": "dot", "wall_s_per_step": round(dt, 4),
+                      "reference_equivalent_gflops": round(2.0 * flops / dt / 1e9, 3),
+                      "reference_equivalent_note": "2 x the unmasked L*L multiplies the reference would form, per "
+                                                   "second; this path never forms them (not the headline)"},
+           "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": 8000.0, "unit": "GB/s",
+                        "frac": round(ach / 8000.0, 4), "traffic": None,
+                        "kernel": "whole step (dot-form classify + thread/wave intersection + collect)",
+                        "alg_bytes_per_step": 8 * probes,
+                        "note": "8 B per probe: the shorter list's row id and the longer-list element it is decided "
+                                "against"},
            "cpu_baseline": None if args.no_cpu_baseline else cpu_baseline(args.cpu_scale),
            "check": {"triangles": tri, "nnzC": C.nnz, "value_sum": vsum, "digest": str(dig),
                      "sampled_columns": checked, "sampled_mismatches": bad, "ok": bad == 0 and vsum == tri}}
     print(json.dumps(out), flush=True)
-    for S in (C, L, L2):
-        S.free()
+    C.free()
     ctx.close()
 
 

@@ -1001,7 +1001,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   const double sb_m = 4.0 * bl.units[1] + 16.0 * bl.mid_count;
   if (diag_enabled()) CBH_TRY((launch_task_diag<Dummy, TSymLarge, MODE_TSYM>(ctx, a, bl, "symbolic")));
   else CBH_TRY((launch_task<Dummy, TSymLarge, MODE_TSYM>(ctx, a, bl.large_first, bl.large_count, CBH_K_SYM_LARGE, sb_l)));
-  CBH_TRY((launch_task<Dummy, TSymMid, MODE_TSYM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_SYM_SMALL, sb_m)));
+  CBH_TRY((launch_task<Dummy, TSymMid, MODE_TSYM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_SYM_MID, sb_m)));
   CBH_TRY((launch_task<Dummy, TSymSmall, MODE_TSYM>(ctx, a, bl.small_first, bl.small_count, CBH_K_SYM_SMALL, sb_s)));
   // task offsets -> column pointers of C
   CBH_TRY(exclusive_scan_i64(ctx, S, P.tcnt, P.toff, P.ntasks + 1));
@@ -1062,7 +1062,7 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
     CBH_TRY((launch_task<SR, TNumLarge, MODE_TDENSE>(ctx, a, bd.large_first, bd.large_count, CBH_K_NUM_DENSE, nb_d)));
     CBH_TRY((launch_task<SR, TNumLarge, MODE_TNUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
   }
-  CBH_TRY((launch_task<SR, TNumMid, MODE_TNUM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_NUM_SMALL, nb_m)));
+  CBH_TRY((launch_task<SR, TNumMid, MODE_TNUM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_NUM_MID, nb_m)));
   CBH_TRY((launch_task<SR, TNumSmall, MODE_TNUM>(ctx, a, bl.small_first, bl.small_count, CBH_K_NUM_SMALL, nb_s)));
   if (launches) *launches += (bd.large_count > 0);
   if (launches) *launches += (bl.large_count > 0) + (bl.mid_count > 0) + (bl.small_count > 0);

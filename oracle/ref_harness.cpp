@@ -20,6 +20,13 @@
 //   tc    <scale> <L.cbm> <C.cbm>                     Applications/TC.cpp:62-121 on one rank (C = (L*L).*L)
 //   mcl   <A.cbm> <out.cbm> <hard> <select> <recover> <pct>
 //                                                     MCLPruneRecoverySelect (ParFriends.h:185-353)
+//   galerkin <A.cbm> <R.cbm> <stride> <reps>          CPU baseline of C3: GalerkinNew.cpp:99-106's
+//                                                     S = R', AT = PSpGEMM(A, R_s), SAT = PSpGEMM(S, AT)
+//                                                     with R_s = R's columns c % stride == 0; JSON
+//   mclexp <A.cbm> <stride> <reps> <hard> <select> <recover> <pct>
+//                                                     CPU baseline of C5: MCL.cpp:574-577's expansion
+//                                                     MemEfficientSpGEMM(A, A_s) with the prune, A_s =
+//                                                     A's columns c % stride == 0; JSON
 // sr: pt_f64 | pt_i64 | max_i64 | min_i64 | bool ; kernel: hybrid | hash | hashu | heap
 #include <mpi.h>
 #include <omp.h>
@@ -381,6 +388,130 @@ static int do_mcl(const std::string& fa, const std::string& fo, double hard, int
   return 0;
 }
 
+// keeps the columns c % stride == 0 of d (all n columns kept, as a ColSplit piece)
+static cbm::Dcsc column_sample(const cbm::Dcsc& d, int64_t stride) {
+  cbm::Dcsc o;
+  o.vtype = d.vtype;
+  o.m = d.m;
+  o.n = d.n;
+  o.cp.push_back(0);
+  for (int64_t i = 0; i < d.nzc(); ++i) {
+    if (d.jc[i] % stride != 0) continue;
+    o.jc.push_back(d.jc[i]);
+    for (int64_t p = d.cp[i]; p < d.cp[i + 1]; ++p) {
+      o.ir.push_back(d.ir[p]);
+      if (d.vtype == cbm::F64) o.vf.push_back(d.vf[p]);
+      else o.vi.push_back(d.vi[p]);
+    }
+    o.cp.push_back((int64_t)o.ir.size());
+  }
+  return o;
+}
+
+// semiring multiplies of X*Y on one rank: sum over Y's entries (k, j) of nnz(X(:, k))
+template <class NT>
+static int64_t local_flops(const SpDCCols<int64_t, NT>& X, const SpDCCols<int64_t, NT>& Y) {
+  if (X.getnnz() == 0 || Y.getnnz() == 0) return 0;
+  std::vector<int64_t> cn(X.getncol(), 0);
+  const Dcsc<int64_t, NT>* dx = X.GetDCSC();
+  for (int64_t i = 0; i < dx->nzc; ++i) cn[dx->jc[i]] = dx->cp[i + 1] - dx->cp[i];
+  const Dcsc<int64_t, NT>* dy = Y.GetDCSC();
+  int64_t f = 0;
+  for (int64_t p = 0; p < dy->nz; ++p) f += cn[dy->ir[p]];
+  return f;
+}
+
+static int nthreads_of() {
+  int nthreads = 1;
+#ifdef THREADED
+#pragma omp parallel
+  {
+#pragma omp master
+    nthreads = omp_get_num_threads();
+  }
+#endif
+  return nthreads;
+}
+
+// GalerkinNew.cpp:99-106 on one rank: S = T' (Transpose), AT = PSpGEMM<PTDD>(A, T), SAT =
+// PSpGEMM<PTDD>(S, AT), on the column sample T_s of T (SAT(:, J) = S * (A * T(:, J)) exactly).
+// One untimed warm-up, then `reps` timed pairs of products; prints the median.
+static int do_galerkin(const std::string& fa, const std::string& fr, int64_t stride, int reps) {
+  typedef PlusTimesSRing<double, double> PTDD;
+  typedef SpDCCols<int64_t, double> DER;
+  typedef SpParMat<int64_t, double, DER> Mat;
+  std::shared_ptr<CommGrid> grid(new CommGrid(MPI_COMM_WORLD, 0, 0));
+  cbm::Dcsc a = cbm::read(fa), r = cbm::read(fr);
+  Mat A(to_spdccols<double>(a), grid);
+  Mat T(to_spdccols<double>(r), grid);
+  Mat Ts(to_spdccols<double>(column_sample(r, stride)), grid);
+  Mat S = T;
+  S.Transpose();
+  std::vector<double> ts;
+  int64_t f1 = 0, f2 = 0, nnz_at = 0, nnz_sat = 0;
+  double vsum = 0;
+  for (int it = -1; it < reps; ++it) {
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double t0 = now();
+    Mat AT = PSpGEMM<PTDD>(A, Ts);
+    Mat SAT = PSpGEMM<PTDD>(S, AT);
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double dt = now() - t0;
+    if (it >= 0) ts.push_back(dt);
+    f1 = local_flops<double>(A.seq(), Ts.seq());
+    f2 = local_flops<double>(S.seq(), AT.seq());
+    nnz_at = AT.getnnz();
+    nnz_sat = SAT.getnnz();
+    vsum = 0;
+    if (SAT.seq().getnnz()) {
+      const Dcsc<int64_t, double>* d = SAT.seq().GetDCSC();
+      for (int64_t p = 0; p < d->nz; ++p) vsum += d->numx[p];
+    }
+  }
+  std::sort(ts.begin(), ts.end());
+  const double med = ts[ts.size() / 2];
+  std::printf("{\"flops\": %lld, \"flops_AR\": %lld, \"flops_RtAR\": %lld, \"nnzAT\": %lld, \"nnzSAT\": %lld, "
+              "\"value_sum\": %.17g, \"median_s\": %.6f, \"min_s\": %.6f, \"reps\": %d, \"gflops\": %.6f, "
+              "\"threads\": %d, \"stride\": %lld, \"cols\": %lld}\n",
+              (long long)(f1 + f2), (long long)f1, (long long)f2, (long long)nnz_at, (long long)nnz_sat, vsum, med,
+              ts.front(), reps, 2.0 * (f1 + f2) / med / 1e9, nthreads_of(), (long long)stride,
+              (long long)Ts.seq().getnzc());
+  return 0;
+}
+
+// MCL.cpp:574-577 (layers == 1) on one rank: the expansion MemEfficientSpGEMM<PTFF>(A, A_s, phases
+// = 1, prunelimit, select, recover_num, recover_pct, kselectVersion 1, hash kernel) with its
+// MCLPruneRecoverySelect, on the column sample A_s of the right operand.
+static int do_mclexp(const std::string& fa, int64_t stride, int reps, double hard, int64_t sel, int64_t rec,
+                     double pct) {
+  typedef PlusTimesSRing<double, double> PTFF;
+  typedef SpDCCols<int64_t, double> DER;
+  typedef SpParMat<int64_t, double, DER> Mat;
+  std::shared_ptr<CommGrid> grid(new CommGrid(MPI_COMM_WORLD, 0, 0));
+  cbm::Dcsc a = cbm::read(fa);
+  Mat A(to_spdccols<double>(a), grid);
+  Mat B(to_spdccols<double>(column_sample(a, stride)), grid);
+  const int64_t flops = local_flops<double>(A.seq(), B.seq());
+  std::vector<double> ts;
+  int64_t nnzc = 0;
+  for (int it = -1; it < reps; ++it) {
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double t0 = now();
+    Mat C = MemEfficientSpGEMM<PTFF, double, DER>(A, B, 1, hard, (int64_t)sel, (int64_t)rec, pct, 1, 1, (int64_t)0);
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double dt = now() - t0;
+    if (it >= 0) ts.push_back(dt);
+    nnzc = C.getnnz();
+  }
+  std::sort(ts.begin(), ts.end());
+  const double med = ts[ts.size() / 2];
+  std::printf("{\"flops\": %lld, \"nnz_after_prune\": %lld, \"median_s\": %.6f, \"min_s\": %.6f, \"reps\": %d, "
+              "\"gflops\": %.6f, \"threads\": %d, \"stride\": %lld, \"cols\": %lld}\n",
+              (long long)flops, (long long)nnzc, med, ts.front(), reps, 2.0 * flops / med / 1e9, nthreads_of(),
+              (long long)stride, (long long)B.seq().getnzc());
+  return 0;
+}
+
 #define DISPATCH_SR(sr, CALL)                                                   \
   if (sr == "pt_f64") {                                                         \
     typedef PlusTimesSRing<double, double> SR;                                  \
@@ -435,6 +566,10 @@ static int run(int argc, char** argv) {
   if (mode == "tc" && argc == 5) return do_tc(std::atoi(argv[2]), argv[3], argv[4]);
   if (mode == "mcl" && argc == 8)
     return do_mcl(argv[2], argv[3], std::atof(argv[4]), std::atoll(argv[5]), std::atoll(argv[6]), std::atof(argv[7]));
+  if (mode == "galerkin" && argc == 6) return do_galerkin(argv[2], argv[3], std::atoll(argv[4]), std::atoi(argv[5]));
+  if (mode == "mclexp" && argc == 9)
+    return do_mclexp(argv[2], std::atoll(argv[3]), std::atoi(argv[4]), std::atof(argv[5]), std::atoll(argv[6]),
+                     std::atoll(argv[7]), std::atof(argv[8]));
   std::fprintf(stderr, "bad arguments\n");
   return 2;
 }

@@ -145,12 +145,14 @@ def mcl_params(apps_meta):
     return (p["hard"], p["select"], p["recover"], p["pct"])
 
 
-def check_mcl(apps, apps_meta, mode, res):
+def check_mcl(apps, apps_meta, mode, res, rtol=0.0):
+    """rtol: the device accumulates non-dyadic f64 sums in LDS-atomic arrival order, so the pruned run
+    and the unpruned run of the same product may differ in the last bits (north_star's 1e-12)"""
     params = mcl_params(apps_meta)
     raw, pruned = res
     A2, got = _dc(raw), _dc(pruned)
     ref = apps["mcl_A2"]
     assert np.array_equal(A2.jc, ref.jc) and np.array_equal(A2.cp, ref.cp) and np.array_equal(A2.ir, ref.ir)
     np.testing.assert_allclose(A2.num, ref.num, rtol=1e-12, atol=0)
-    H.assert_dcsc_equal(got, AO.mcl_prune_recovery_select(A2, *params), msg=f"MCL prune {mode}")
+    H.assert_dcsc_equal(got, AO.mcl_prune_recovery_select(A2, *params), rtol=rtol, msg=f"MCL prune {mode}")
     assert got.nnz == pytest.approx(apps["mcl_out0"].nnz, rel=0.01)

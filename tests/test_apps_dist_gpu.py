@@ -8,7 +8,8 @@ every rank owns its GPU and the same driver code runs over RCCL.
   C5 MCL       MemEfficientSpGEMM + MCLPruneRecoverySelect on 2x2 and MemEfficientSpGEMM3D on
                2x2x2 (ParFriends.h:449-730, 3214-3705; prune :185-353), fixed phases and phases=0
                (planned from the exact symbolic pass under a small per-process budget) -> the
-               reference's expanded matrix mcl_A2 (1e-12) and the oracle prune of it, exactly
+               reference's expanded matrix mcl_A2 (1e-12) and the oracle prune of it (structure exact,
+               values 1e-12: the pruned and the unpruned device runs sum in LDS-atomic order)
 (the CPU twin of this file, with the oracle backend: tests/test_apps_dist_cpu.py)
 """
 import pytest
@@ -29,4 +30,4 @@ def test_gpu_galerkin_2x2_vs_reference(apps):
                                                     ("3d", 8, 0, 64 * 1024)])
 def test_gpu_mcl_prune_distributed(apps, apps_meta, mode, world, phases, ppm):
     res = run_world(_mcl_worker, world, mode, mcl_params(apps_meta), phases, ppm, "hip", timeout=200)
-    check_mcl(apps, apps_meta, mode, res)
+    check_mcl(apps, apps_meta, mode, res, rtol=1e-12)
