@@ -720,14 +720,19 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
     // hash numeric: occupied slots per wave (slot ranges of SPW) -> every wave's queue offset and
     // the total; a sub-tile whose occupied slots exceed the commit queue is retried like an overflow
     constexpr int SPW = ((TA + NW - 1) / NW + 63) / 64 * 64;
+    constexpr int NBW = SPW / 64;  // occupancy ballots per wave
     int qbase = 0, qtot = 0;
+    // occupancy masks of this wave's slot range, kept for the queue compaction of the commit
+    uint64_t occm[NUM && !dense ? NBW : 1];
     if constexpr (NUM && !dense) {
       const int sb = wid * SPW < TA ? wid * SPW : TA;
       const int se = sb + SPW < TA ? sb + SPW : TA;
       int wc = 0;
-      for (int s0 = sb; s0 < se; s0 += 64) {
-        const int sl = s0 + lane;
-        wc += __popcll(__ballot(sl < se && keys[sl] != kEmpty));
+#pragma unroll
+      for (int b = 0; b < NBW; ++b) {
+        const int sl = sb + 64 * b + lane;
+        occm[b] = __ballot(sl < se && keys[sl] != kEmpty);
+        wc += __popcll(occm[b]);
       }
       if (lane == 0) red[NW + wid] = wc;
       __syncthreads();
@@ -858,14 +863,12 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
       int16_t* Q = reinterpret_cast<int16_t*>(own);
       {
         const int sb = wid * SPW < TA ? wid * SPW : TA;
-        const int se = sb + SPW < TA ? sb + SPW : TA;
         const uint64_t lt = (1ull << lane) - 1ull;
         int qo = qbase;
-        for (int s0 = sb; s0 < se; s0 += 64) {
-          const int sl = s0 + lane;
-          const bool occ = sl < se && keys[sl] != kEmpty;
-          const uint64_t mask = __ballot(occ);
-          if (occ) Q[qo + __popcll(mask & lt)] = (int16_t)sl;
+#pragma unroll
+        for (int b = 0; b < NBW; ++b) {
+          const uint64_t mask = occm[b];
+          if ((mask >> lane) & 1ull) Q[qo + __popcll(mask & lt)] = (int16_t)(sb + 64 * b + lane);
           qo += __popcll(mask);
         }
       }
@@ -887,12 +890,21 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
         const int rs = below ? 63 - __clzll(below) : -1;  // run start lane (-1: before the batch)
         const int re = above ? __ffsll((long long)above) - 1 : 64;  // run end lane (64: after it)
         const int lo_l = rs < 0 ? 0 : rs, hi_l = re > 63 ? 63 : re;
+        // keys of the run inside the batch: four shuffles in flight per exit test (runs average
+        // 2.5 slots, but the batch's longest -- about 11 at fill 1/2 -- sets the trip count)
         int rank = 0;
-        for (int j = 0;; ++j) {
-          const bool act = valid && lo_l + j <= hi_l;
-          if (__ballot(act) == 0ull) break;
-          const int32_t kj = __shfl(key, (lo_l + j) & 63);
-          rank += (act && kj < key) ? 1 : 0;
+        for (int j = 0;; j += 4) {
+          if (__ballot(valid && lo_l + j <= hi_l) == 0ull) break;
+          const int32_t k0 = __shfl(key, (lo_l + j) & 63);
+          const int32_t k1 = __shfl(key, (lo_l + j + 1) & 63);
+          const int32_t k2 = __shfl(key, (lo_l + j + 2) & 63);
+          const int32_t k3 = __shfl(key, (lo_l + j + 3) & 63);
+          if (valid) {
+            rank += (lo_l + j <= hi_l && k0 < key) ? 1 : 0;
+            rank += (lo_l + j + 1 <= hi_l && k1 < key) ? 1 : 0;
+            rank += (lo_l + j + 2 <= hi_l && k2 < key) ? 1 : 0;
+            rank += (lo_l + j + 3 <= hi_l && k3 < key) ? 1 : 0;
+          }
         }
         int rstart = b0 + lo_l;
         if (valid && rs < 0) {  // the run began in an earlier batch

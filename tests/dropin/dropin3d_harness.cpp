@@ -11,7 +11,7 @@
 //   Mult_AnXBn_SUMMA3D      ParFriends.h:2918-3208 (SpParMat3D, layers from argv; the fiber
 //                           reduce-scatter :3097-3183 merges with MultiwayMergeHash)
 //   MemEfficientSpGEMM3D    ParFriends.h:3214-3705 (hash and heap kernels, 2 phases, prune)
-// The results (Convert2D for the 3D ones) must hold the same entries on every rank. The stock hash
+// The results must hold the same entries on every rank (3D ones compared block by block). The stock hash
 // kernels leave rows unsorted inside a column (mtSpGEMM.h:624-634, MultiwayMergeHash sorted=false),
 // so each local column is compared as a sorted set; values are R-MAT edge multiplicities, so every
 // double sum is exact.
@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -87,9 +88,72 @@ static int report(const char* name, PMat& Ch, PMat& Cc, double hip_s, double cpu
   return anybad;
 }
 
+// 3D results compared block by block (both runs distribute C the same way): Convert2D builds a
+// square 2D grid of the world, which 2 and 8 ranks do not have
+static int report3d(const char* name, PMat3D& Ch, PMat3D& Cc, double hip_s, double cpu_s) {
+  int myrank, nprocs;
+  MPI_Comm_rank(MPI_COMM_WORLD, &myrank);
+  MPI_Comm_size(MPI_COMM_WORLD, &nprocs);
+  int bad = (columns(*Ch.seqptr()) == columns(*Cc.seqptr())) ? 0 : 1;
+  if (Ch.seqptr()->getnrow() != Cc.seqptr()->getnrow() || Ch.seqptr()->getncol() != Cc.seqptr()->getncol()) bad = 1;
+  int64_t loc[2] = {Ch.seqptr()->getnnz(), Cc.seqptr()->getnnz()}, tot[2] = {0, 0};
+  MPI_Allreduce(loc, tot, 2, MPI_INT64_T, MPI_SUM, MPI_COMM_WORLD);
+  int anybad = 0;
+  MPI_Allreduce(&bad, &anybad, 1, MPI_INT, MPI_MAX, MPI_COMM_WORLD);
+  if (tot[0] != tot[1]) anybad = 1;
+  if (myrank == 0) {
+    std::printf("DROPIN3D %s %s nnz=%lld ranks=%d hip_s=%.3f cpu_s=%.3f\n", name, anybad ? "MISMATCH" : "OK",
+                (long long)tot[0], nprocs, hip_s, cpu_s);
+    std::fflush(stdout);
+  }
+  return anybad;
+}
+
 static bool is_square(int p) {
   const int r = (int)std::lround(std::sqrt((double)p));
   return r * r == p;
+}
+
+// The R-MAT input on a gr x gc grid of MPI_COMM_WORLD. DistEdgeList and SpParMat(DEL) need a square
+// world (CommGrid.cpp:45-52 aborts otherwise), so for 2 or 8 ranks every rank generates the whole
+// matrix on MPI_COMM_SELF and keeps its block (SpParMat::Owner's split: m/gr rows per block, the
+// last one taking the remainder; local ids) -- the 3D drivers then redistribute it by tuples
+// (SpParMat3D's non-special constructor takes any 2D grid shape).
+static PMat make_input(int scale, int gr, int gc) {
+  double init[4] = {.57, .19, .19, .05};
+  if (gr == gc) {
+    DistEdgeList<int64_t>* DEL = new DistEdgeList<int64_t>();
+    DEL->GenGraph500Data(init, scale, 16, true, true);
+    SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>> G(*DEL, false);
+    delete DEL;
+    return PMat(G);
+  }
+  MPI_Comm self = MPI_COMM_SELF;
+  DistEdgeList<int64_t>* DEL = new DistEdgeList<int64_t>(self);
+  DEL->GenGraph500Data(init, scale, 16, true, true);
+  SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>> G(*DEL, false);
+  delete DEL;
+  int myrank;
+  MPI_Comm_rank(MPI_COMM_WORLD, &myrank);
+  const int64_t m = G.getnrow(), n = G.getncol();
+  const int pr = myrank / gc, pc = myrank % gc;
+  const int64_t rper = m / gr, cper = n / gc;
+  const int64_t r0 = pr * rper, r1 = pr == gr - 1 ? m : r0 + rper;
+  const int64_t c0 = pc * cper, c1 = pc == gc - 1 ? n : c0 + cper;
+  std::vector<std::tuple<int64_t, int64_t, double>> t;
+  auto& S = G.seq();
+  for (auto colit = S.begcol(); colit != S.endcol(); ++colit) {
+    const int64_t c = colit.colid();
+    if (c < c0 || c >= c1) continue;
+    for (auto nzit = S.begnz(colit); nzit != S.endnz(colit); ++nzit)
+      if (nzit.rowid() >= r0 && nzit.rowid() < r1)
+        t.emplace_back(nzit.rowid() - r0, c - c0, (double)nzit.value());
+  }
+  auto* owned = new std::tuple<int64_t, int64_t, double>[t.size()];  // SpTuples delete[]s its array
+  std::copy(t.begin(), t.end(), owned);
+  SpTuples<int64_t, double> tup((int64_t)t.size(), r1 - r0, c1 - c0, owned, true);
+  std::shared_ptr<CommGrid> grid(new CommGrid(MPI_COMM_WORLD, gr, gc));
+  return PMat(new DCols(tup, false), grid);
 }
 
 int main(int argc, char** argv) {
@@ -101,12 +165,12 @@ int main(int argc, char** argv) {
   MPI_Comm_size(MPI_COMM_WORLD, &nprocs);
   int bad = 0;
   {  // every CombBLAS object must be destroyed before MPI_Finalize
-    double init[4] = {.57, .19, .19, .05};
-    DistEdgeList<int64_t>* DEL = new DistEdgeList<int64_t>();
-    DEL->GenGraph500Data(init, scale, 16, true, true);
-    SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>> G(*DEL, false);
-    delete DEL;
-    PMat A(G), B(G);
+    int gr = (int)std::lround(std::sqrt((double)nprocs)), gc = gr;
+    if (gr * gc != nprocs) {  // 2 -> 1 x 2, 8 -> 2 x 4
+      gr = (int)std::lround(std::sqrt((double)(nprocs / 2)));
+      gc = nprocs / gr;
+    }
+    PMat A = make_input(scale, gr, gc), B = make_input(scale, gr, gc);
     // MCLPruneRecoverySelect parameters: keep entries > 1.5, select the 40 largest per column,
     // recover up to 60 when the kept mass falls under 90 %
     const double hard = 1.5, pct = 0.9;
@@ -132,8 +196,7 @@ int main(int argc, char** argv) {
         double t1 = MPI_Wtime();
         PMat3D C3c = Mult_AnXBn_SUMMA3D<CpuPlusTimes, double, DCols, int64_t, double, double, DCols, DCols>(A3, B3);
         double t2 = MPI_Wtime();
-        PMat Ch = C3h.Convert2D(), Cc = C3c.Convert2D();
-        bad += report("Mult_AnXBn_SUMMA3D", Ch, Cc, t1 - t0, t2 - t1);
+        bad += report3d("Mult_AnXBn_SUMMA3D", C3h, C3c, t1 - t0, t2 - t1);
       }
       for (int kernel : {1, 2}) {
         char name[96];
@@ -145,8 +208,7 @@ int main(int argc, char** argv) {
         PMat3D C3c = MemEfficientSpGEMM3D<CpuPlusTimes, double, DCols, int64_t, double, double, DCols, DCols>(
             A3, B3, 2, hard, sel, rec, pct, 1, kernel, 0);
         double t2 = MPI_Wtime();
-        PMat Ch = C3h.Convert2D(), Cc = C3c.Convert2D();
-        bad += report(name, Ch, Cc, t1 - t0, t2 - t1);
+        bad += report3d(name, C3h, C3c, t1 - t0, t2 - t1);
       }
     }
   }
