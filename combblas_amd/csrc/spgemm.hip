@@ -56,7 +56,7 @@ struct cbh_ctx {
   std::multimap<size_t, void*> cache;
   std::unordered_map<void*, size_t> live;
   size_t cached_bytes = 0;
-  size_t cache_cap = size_t(64) << 30;  // CBH_CACHE_CAP_GB; above it the cache is released
+  size_t cache_cap = size_t(128) << 30;  // CBH_CACHE_CAP_GB; above it the cache is released
   bool poison = false;  // CBH_ALLOC_POISON=1: freed blocks are filled with 0xFF and never reused
   std::vector<void*> quarantine;
   std::vector<hipEvent_t> evpool;
@@ -746,15 +746,30 @@ __global__ void add_i64_kernel(const int64_t* __restrict__ x, const int64_t* __r
   if (i < n) o[i] = x[i] + y[i];
 }
 
+// Stored row bitmaps (TaskArgs::bmp): words of every dense CANDIDATE, a large-symbolic task that
+// the dense split could choose by its flop estimate (the outputs the split decides on are at most
+// the flops, and dense_subtiles only grows with the work), else 0. The symbolic pass writes the
+// candidates' bitmaps while it counts; the dense kernel reads them instead of marking rows again.
+__global__ void bmp_count_kernel(const int64_t* __restrict__ twork, const int32_t* __restrict__ tlo,
+                                 const int32_t* __restrict__ thi, int64_t n, int64_t T, int64_t capd, int64_t nwb,
+                                 int64_t minwork, int64_t* __restrict__ words) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int64_t w = twork[t], span = (int64_t)thi[t] - tlo[t];
+  words[t] = (w > minwork && span > 0 && dense_subtiles(w, span, T, capd, nwb) > 0) ? (span + 31) / 32 : 0;
+}
+
 // numeric tasks split between the dense (bitmap-rank) and the hash kernels: wd / wh = the task's
-// output count in the kernel it goes to, 0 in the other
+// output count in the kernel it goes to, 0 in the other. Dense needs a stored bitmap (boff).
 __global__ void dense_split_kernel(const int64_t* __restrict__ tcnt, const int32_t* __restrict__ tlo,
-                                   const int32_t* __restrict__ thi, int64_t n, int64_t T, int64_t capd, int64_t nwb,
-                                   int64_t smallcap, int enable, int64_t* __restrict__ wd, int64_t* __restrict__ wh) {
+                                   const int32_t* __restrict__ thi, const int64_t* __restrict__ boff, int64_t n,
+                                   int64_t T, int64_t capd, int64_t nwb, int64_t smallcap, int enable,
+                                   int64_t* __restrict__ wd, int64_t* __restrict__ wh) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   const int64_t w = tcnt[t];
-  const bool d = enable && w > smallcap && dense_subtiles(w, (int64_t)thi[t] - tlo[t], T, capd, nwb) > 0;
+  const bool d = enable && boff != nullptr && boff[t + 1] > boff[t] && w > smallcap &&
+                 dense_subtiles(w, (int64_t)thi[t] - tlo[t], T, capd, nwb) > 0;
   wd[t] = d ? w : 0;
   wh[t] = d ? 0 : w;
 }
@@ -765,6 +780,21 @@ static bool kDenseEnabled() {
     return e ? std::atoi(e) : 1;
   }();
   return v != 0;
+}
+// share of the free HBM the phase workspace of cbh_spgemm_phased takes (CBH_PHASE_FRAC)
+static double phase_frac() {
+  static double v = [] {
+    const char* e = std::getenv("CBH_PHASE_FRAC");
+    return e ? std::atof(e) : 0.5;
+  }();
+  return v;
+}
+static double bmp_frac() {
+  static double v = [] {
+    const char* e = std::getenv("CBH_BMP_FRAC");
+    return e ? std::atof(e) : 0.4;
+  }();
+  return v;
 }
 
 // task_kernel launch with optional HIP-event timing (kernel configurations: device/numeric.h;
@@ -861,6 +891,8 @@ struct Plan {  // device arrays describing C = A*B (B's nonzero column slots, ta
   int32_t* trk = nullptr;     // per task: row block of its middle row (launch order key)
   int32_t* gnx0 = nullptr;    // row at each committed cursor (double-buffered like gcur)
   int32_t* gnx1 = nullptr;
+  int64_t* boff = nullptr;    // ntasks + 1: stored-bitmap word offsets (see bmp_count_kernel)
+  uint32_t* bmp = nullptr;    // null: no stored bitmaps (dense kernel off)
   int64_t total_flops = 0, total_nnz = 0;
 };
 
@@ -893,6 +925,8 @@ static TaskArgs task_args(const cbh_mat* A, const cbh_mat* B, const Plan& P, cbh
   a.gend = P.gend;
   a.gnx0 = P.gnx0;
   a.gnx1 = P.gnx1;
+  a.boff = P.bmp ? P.boff : nullptr;
+  a.bmp = P.bmp;
   return a;
 }
 
@@ -988,6 +1022,29 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
       P.goff = nullptr;
     }
   }
+  {  // stored row bitmaps of the dense candidates, within CBH_BMP_FRAC (default 0.4) of the HBM
+    using CD = TaskCfg<PlusTimesD<double>, TNumLarge::T, TNumLarge::BS, TNumLarge::EMAX, TNumLarge::U, MODE_TDENSE>;
+    int64_t* bw;
+    CBH_TRY(S.get(&bw, nt + 1));
+    CBH_TRY(S.get(&P.boff, nt + 1));
+    hipLaunchKernelGGL(bmp_count_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.twork, P.tlo, P.thi,
+                       P.ntasks, (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSymMidCap, bw);
+    CBH_HIP(ctx, hipGetLastError());
+    CBH_HIP(ctx, hipMemsetAsync(bw + P.ntasks, 0, sizeof(int64_t), ctx->stream));
+    CBH_TRY(exclusive_scan_i64(ctx, S, bw, P.boff, P.ntasks + 1));
+    int64_t words = 0;
+    CBH_HIP(ctx, hipMemcpyAsync(&words, P.boff + P.ntasks, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    size_t freeb = 0, totb = 0;
+    CBH_HIP(ctx, hipMemGetInfo(&freeb, &totb));
+    // within a fraction of the device (not of what is free: later calls find the earlier call's
+    // bitmaps in the block cache and the phase workspace resident)
+    if (words > 0 && kDenseEnabled() && (double)words * 4.0 <= bmp_frac() * (double)totb &&
+        (size_t)words * 4 < freeb + ctx->cached_bytes)
+      CBH_TRY(S.get(&P.bmp, (size_t)words));
+    if (diag_enabled())
+      std::fprintf(stderr, "[cbh diag] stored bitmaps: %.3f GB (%s)\n", words * 4e-9, P.bmp ? "kept" : "over budget: no dense");
+  }
   CBH_HIP(ctx, hipMemsetAsync(P.tcnt, 0, sizeof(int64_t) * (nt + 1), ctx->stream));
   BinLists bl;
   CBH_TRY(make_bins(ctx, S, P.twork, P.ntasks, 0, P.order, &bl, BinCaps{kSmallCap, kSymMidCap}, P.tunits, P.trk));
@@ -1032,7 +1089,7 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
   CBH_TRY(S.get(&wd, nt));
   CBH_TRY(S.get(&wh, nt));
   hipLaunchKernelGGL(dense_split_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.tcnt + t0, P.tlo + t0,
-                     P.thi + t0, nt, (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSmallCap,
+                     P.thi + t0, P.bmp ? P.boff + t0 : nullptr, nt, (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSmallCap,
                      kDenseEnabled() ? 1 : 0, wd, wh);
   CBH_HIP(ctx, hipGetLastError());
   BinLists bd, bl;
@@ -1056,6 +1113,31 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
   const double nb_s = eb * bl.units[0] + 16.0 * bl.small_count;
   const double nb_m = eb * bl.units[1] + 16.0 * bl.mid_count;
   if (diag_enabled()) {
+    {  // task-class totals of this numeric range (profiling aid)
+      std::vector<int64_t> hd(nt), hc(nt), hw(nt);
+      std::vector<int32_t> hlo(nt), hhi(nt), hcol(nt);
+      CBH_HIP(ctx, hipMemcpyAsync(hd.data(), wd, nt * 8, hipMemcpyDeviceToHost, ctx->stream));
+      CBH_HIP(ctx, hipMemcpyAsync(hc.data(), P.tcnt + t0, nt * 8, hipMemcpyDeviceToHost, ctx->stream));
+      CBH_HIP(ctx, hipMemcpyAsync(hw.data(), P.twork + t0, nt * 8, hipMemcpyDeviceToHost, ctx->stream));
+      CBH_HIP(ctx, hipMemcpyAsync(hlo.data(), P.tlo + t0, nt * 4, hipMemcpyDeviceToHost, ctx->stream));
+      CBH_HIP(ctx, hipMemcpyAsync(hhi.data(), P.thi + t0, nt * 4, hipMemcpyDeviceToHost, ctx->stream));
+      CBH_HIP(ctx, hipMemcpyAsync(hcol.data(), P.tcol + t0, nt * 4, hipMemcpyDeviceToHost, ctx->stream));
+      CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      double s[2][5] = {{0}};  // tasks, span, outputs, flops, columns
+      int64_t lastc[2] = {-1, -1};
+      for (int64_t t = 0; t < nt; ++t) {
+        const int k = hd[t] > 0 ? 1 : 0;
+        if (hc[t] <= kSmallCap && !k) continue;
+        s[k][0] += 1;
+        s[k][1] += (double)(hhi[t] - hlo[t]);
+        s[k][2] += (double)hc[t];
+        s[k][3] += (double)hw[t];
+        if (hcol[t] != lastc[k]) s[k][4] += 1, lastc[k] = hcol[t];
+      }
+      for (int k = 0; k < 2; ++k)
+        std::fprintf(stderr, "[cbh diag] %s tasks %.0f cols %.0f span %.4g (bitmap %.3f GB) outputs %.4g flops %.4g\n",
+                     k ? "dense" : "hash>256", s[k][0], s[k][4], s[k][1], s[k][1] / 8e9, s[k][2], s[k][3]);
+    }
     CBH_TRY((launch_task_diag<SR, TNumLarge, MODE_TDENSE>(ctx, a, bd, "numeric dense")));
     CBH_TRY((launch_task_diag<SR, TNumLarge, MODE_TNUM>(ctx, a, bl, "numeric hash")));
   } else {
@@ -1510,7 +1592,7 @@ int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh
       } else {
         size_t freeb = 0, totb = 0;
         CBH_HIP(ctx, hipMemGetInfo(&freeb, &totb));
-        budget_bytes = (int64_t)(freeb / 2);
+        budget_bytes = (int64_t)(freeb * phase_frac());
       }
     }
     int64_t budget = std::max<int64_t>(1, std::min<int64_t>(budget_bytes / (int64_t)esz, P.total_nnz));
@@ -1714,7 +1796,8 @@ int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t
   int64_t *wd, *wh;
   CBH_TRY(p->S.get(&wd, nt));
   CBH_TRY(p->S.get(&wh, nt));
-  hipLaunchKernelGGL(dense_split_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.tcnt, P.tlo, P.thi, nt,
+  hipLaunchKernelGGL(dense_split_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.tcnt, P.tlo, P.thi,
+                     P.bmp ? P.boff : nullptr, nt,
                      (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSmallCap,
                      (kDenseEnabled() && !(flags & CBH_PLAN_NO_DENSE)) ? 1 : 0, wd, wh);
   CBH_HIP(ctx, hipGetLastError());
@@ -1746,6 +1829,8 @@ int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t
   out->gend = P.gend;
   out->gnx0 = P.gnx0;
   out->gnx1 = P.gnx1;
+  out->boff = P.bmp ? P.boff : nullptr;
+  out->bmp = P.bmp;
   out->err = ctx->d_err;
   out->nnzA = A->nnz;
   out->ncolA = A->n;

@@ -111,6 +111,11 @@ struct TaskArgs {
   // only when it is active
   int32_t* gnx0;
   int32_t* gnx1;
+  // stored row bitmaps of the dense candidates (bmp_count_kernel): task t owns words
+  // [boff[t], boff[t+1]) of bmp, bit x of word w = row tlo[t] + 32 w + x. The large symbolic kernel
+  // writes them while it counts; the dense numeric kernel reads them instead of a marking pass.
+  const int64_t* boff;
+  uint32_t* bmp;
   // merge mode (MultiwayMerge of k partial lists): entry l of output column slot c is list l's
   // segment [mstart[c*nl+l], +mlen[c*nl+l]) of lir[l] / lnum[l]; no multiply
   const int64_t* mstart;
@@ -370,32 +375,31 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
   const int64_t span = (int64_t)thi - tlo;
   const bool chunked = ne > EMAX;
   const int nchunks = chunked ? (int)((ne + EMAX - 1) / EMAX) : 1;
-  // sub-tile plan (uniform in rows). Numeric sub-tiles are DENSE when a bitmap over the
-  // sub-tile's rows fits LDS without more sub-tiles than the hash needs: distinct rows are marked
-  // in the bitmap first, its prefix popcounts then give every row its output rank directly, so
-  // values accumulate in row order and the commit is a straight copy (no hashing, no probing, no
-  // rank search). Sparse row ranges use the order-preserving hash.
+  // sub-tile plan of the hash and symbolic kernels (uniform in rows). Tasks whose output rows are
+  // dense enough run the DENSE kernel instead (windows of the stored row bitmap, below): their
+  // bitmap's prefix popcounts give every row its output rank directly, so values accumulate in
+  // row order and the commit is a straight copy (no hashing, no probing, no rank search).
   bool bitmap = false;
   constexpr bool dense = C::DENSE;
-  int64_t R;
-  {
+  // symbolic: a dense candidate's bitmap is stored for the dense numeric kernel (word-aligned
+  // sub-tiles, always the bitmap form)
+  const bool store = !NUM && a.bmp != nullptr && a.boff[task + 1] > a.boff[task];
+  int64_t R = 1;
+  if constexpr (!dense) {
     constexpr int64_t cap = NUM ? (int64_t)T * kFill8 / 8 : T / 2;  // outputs (keys) per sub-tile
     R = (work + cap - 1) / cap;
     if constexpr (!NUM) {
       const int64_t Rb = (span + 32ll * TA - 1) / (32ll * TA);
-      if (Rb <= R) {
+      if (Rb <= R || store) {
         bitmap = true;
         R = Rb;
       }
-    } else if constexpr (dense) {  // the binning chose this kernel with the same plan
-      const int64_t Rd = dense_subtiles(work, span, T, C::CAPD, C::NWB);
-      const int64_t Rw = (span + 32ll * C::NWB - 1) / (32ll * C::NWB);
-      R = Rd > Rw ? Rd : Rw;
     }
     if (R > span) R = span;
     if (R < 1) R = 1;
   }
-  const int64_t wnom = (span + R - 1) / R;
+  int64_t wnom = (span + R - 1) / R;
+  if (store) wnom = (wnom + 31) & ~int64_t(31);  // <= 32*TA: R >= span / (32*TA)
 
   // violated bounds guards are recorded in a register and reported once at the end: a guard_fail
   // (global atomics with return values) inside a hot loop makes the compiler drain vmcnt there
@@ -489,7 +493,7 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
       eend[i] = cend;
       const int32_t nx = pos < cend ? kUnknownRow : kNoRow;
       enext[i] = nx;
-      if (chunked) {  // the first sub-tile's cursors are committed state too (dense value pass)
+      if (chunked) {  // the first sub-tile's cursors are committed state too
         a.gend[go + first + i] = cend;
         (par ? a.gcur1 : a.gcur0)[go + first + i] = pos;
         (par ? a.gnx1 : a.gnx0)[go + first + i] = nx;
@@ -602,8 +606,126 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
   int my_count = 0;  // symbolic hash: keys this thread inserted first
 
   int32_t lo = tlo;
+  if constexpr (dense) {
+    // DENSE numeric sub-tiles are windows of the task's row bitmap, stored by the symbolic pass
+    // (TaskArgs::bmp), cut where the window's popcount would pass CAPD: the word prefix popcounts
+    // give every row its output rank before any product is gathered, so one value pass
+    // accumulates the products at their ranks, nothing overflows, windows without outputs are
+    // skipped, and the commit walks the bitmap (no row ids stored).
+    const int64_t bw0 = a.boff[task];
+    const int64_t nwt = a.boff[task + 1] - bw0;
+    if (a.bmp == nullptr || nwt != (span + 31) / 32) {
+      if (tid == 0) guard_fail(a.err, 10, c, task, nwt, span);
+      return;
+    }
+    const uint32_t* __restrict__ tb = a.bmp + bw0;
+    __shared__ int32_t s_cut;
+    constexpr int KW = (C::NWB + BS - 1) / BS;
+    bool inited = !chunked;  // chunked: HBM entry state is written by the first processed window
+    int64_t w0 = 0;
+    while (w0 < nwt) {
+      const int wl = (int)((nwt - w0) < C::NWB ? (nwt - w0) : C::NWB);
+      for (int x = tid; x < wl; x += BS) dwords[x] = tb[w0 + x];
+      if (tid == 0) {
+        s_cut = wl;
+        __hip_atomic_store(&s_ovf, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // sweep() reads it
+      }
+      __syncthreads();
+      // exclusive popcount prefix per word (thread-consecutive words; stride KW is odd: no bank
+      // conflicts), clamped to int16 past the cut, and the word where the prefix passes CAPD
+      int tsum = 0;
+      for (int k = 0; k < KW; ++k) {
+        const int x = tid * KW + k;
+        tsum += x < wl ? __popc(dwords[x]) : 0;
+      }
+      int wtotal = 0;
+      int ex = block_excl_sum<BS>(tsum, red, wtotal);
+      for (int k = 0; k < KW; ++k) {
+        const int x = tid * KW + k;
+        if (x < wl) {
+          const int pc = __popc(dwords[x]);
+          dpre[x] = (int16_t)(ex < 32767 ? ex : 32767);
+          if (ex <= C::CAPD && ex + pc > C::CAPD) s_cut = x;
+          ex += pc;
+        }
+      }
+      __syncthreads();
+      CBH_STAMP(1);
+      const int cut = s_cut;
+      const int dtotal = cut < wl ? (int)dpre[cut] : wtotal;
+      lo = (int32_t)(tlo + 32 * w0);
+      const int64_t hcut = tlo + 32 * (w0 + cut);
+      const int32_t hi = (int32_t)(hcut < thi ? hcut : thi);
+      const uint32_t tw = (uint32_t)(hi - lo);
+      if (dtotal > 0) {
+        auto place = [&](int u) {
+          const uint32_t d = (uint32_t)(r[u] - lo);
+          if (d >= tw) {
+            bad |= 1 << 8;
+            return;
+          }
+          const uint32_t wv = dwords[d >> 5];
+          if (!((wv >> (d & 31)) & 1u)) bad |= 1 << 11;  // a product row the symbolic pass did not mark
+          const int slot = dpre[d >> 5] + __popc(wv & ((1u << (d & 31)) - 1u));
+          SR::lds_acc(&vals[slot], av[u]);
+        };
+        for (int ch = 0; ch < nchunks; ++ch) {
+          int nec = (int)ne;
+          if (chunked) {
+            const int64_t first = (int64_t)ch * EMAX;
+            nec = (int)((ne - first) < EMAX ? (ne - first) : EMAX);
+            load_entries(first, nec, lo, hi, lo == tlo && (full & 1), inited);
+            __syncthreads();
+          }
+          const int P = segments(nec, hi, hi == thi);
+          CBH_STAMP(3);
+          if (chunked) {  // this chunk's cursors after the window, into the other buffer
+            int64_t* gn = par ? a.gcur0 : a.gcur1;
+            int32_t* gx = par ? a.gnx0 : a.gnx1;
+            for (int i = tid; i < nec; i += BS) {
+              gn[go + (int64_t)ch * EMAX + i] = epos[i] + eoff[i + 1];
+              gx[go + (int64_t)ch * EMAX + i] = enext2[i];
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the stores land before the next barrier
+          }
+          sweep(nec, P, true, place);  // ends with a barrier: the entry state may be reloaded
+        }
+        // commit: values are in row order; word x's set bits are ranks dpre[x]..
+        for (int x = tid; x < cut; x += BS) {
+          uint32_t wv = dwords[x];
+          int rk = dpre[x];
+          while (wv) {
+            const int b = __builtin_ctz(wv);
+            wv &= wv - 1u;
+            const int64_t pos = out_pos + rk;
+            if (pos >= out_end || pos >= a.ccap) {
+              bad |= 1 << 5;
+            } else {
+              a.Cir[pos] = lo + 32 * x + b;
+              reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(vals[rk]);
+            }
+            vals[rk] = SR::identity();
+            ++rk;
+          }
+        }
+        out_pos += dtotal;
+        if (chunked) {
+          par ^= 1;
+          inited = true;
+        } else {
+          for (int i = tid; i < (int)ne; i += BS) {
+            epos[i] += eoff[i + 1];
+            enext[i] = enext2[i];
+          }
+        }
+      }
+      w0 += cut;
+      __syncthreads();
+      CBH_STAMP(6);
+    }
+  }
   int64_t w = wnom;
-  while (lo < thi) {
+  while (!dense && lo < thi) {
     const int32_t hi = (int32_t)(((int64_t)lo + w < thi) ? lo + w : thi);
     const bool hi_is_end = hi == thi;  // entry ends are clamped to the task (load_entries)
     const uint32_t tw = (uint32_t)(hi - lo);
@@ -611,8 +733,6 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
     const int nwd = (int)((tw + 31) >> 5);
     if (!NUM && bitmap) {
       for (int s = tid; s < nwd; s += BS) words[s] = 0u;
-    } else if constexpr (dense) {
-      for (int s = tid; s < nwd; s += BS) dwords[s] = 0u;
     } else {
       for (int s = tid; s < (NUM ? TA : T); s += BS) {
         keys[s] = kEmpty;
@@ -645,12 +765,6 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
           const uint32_t d = (uint32_t)(r[u] - lo);
           if (d >= tw) bad |= 1 << 8;
           else atomicOr(&words[d >> 5], 1u << (d & 31));
-        });
-      } else if constexpr (dense) {
-        sweep(nec, P, false, [&](int u) {
-          const uint32_t d = (uint32_t)(r[u] - lo);
-          if (d >= tw) bad |= 1 << 8;
-          else atomicOr(&dwords[d >> 5], 1u << (d & 31));
         });
       } else if constexpr (NUM) {
         sweep(nec, P, true, [&](int u) {
@@ -716,15 +830,14 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
         __syncthreads();  // entry state is reloaded by the next chunk
       }
     }
-    int dtotal = 0;
     // hash numeric: occupied slots per wave (slot ranges of SPW) -> every wave's queue offset and
     // the total; a sub-tile whose occupied slots exceed the commit queue is retried like an overflow
     constexpr int SPW = ((TA + NW - 1) / NW + 63) / 64 * 64;
     constexpr int NBW = SPW / 64;  // occupancy ballots per wave
     int qbase = 0, qtot = 0;
     // occupancy masks of this wave's slot range, kept for the queue compaction of the commit
-    uint64_t occm[NUM && !dense ? NBW : 1];
-    if constexpr (NUM && !dense) {
+    uint64_t occm[NUM ? NBW : 1];
+    if constexpr (NUM) {
       const int sb = wid * SPW < TA ? wid * SPW : TA;
       const int se = sb + SPW < TA ? sb + SPW : TA;
       int wc = 0;
@@ -743,71 +856,12 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
         qtot += rr;
       }
     }
-    if constexpr (NUM && dense) {
-      if (dense && !__hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-        // output rank of every word's first row: exclusive scan of the bitmap's popcounts
-        constexpr int KW = (C::NWB + BS - 1) / BS;
-        int tsum = 0;
-        for (int k = 0; k < KW; ++k) {
-          const int x = tid * KW + k;
-          tsum += x < nwd ? __popc(dwords[x]) : 0;
-        }
-        int ex = block_excl_sum<BS>(tsum, red, dtotal);
-        for (int k = 0; k < KW; ++k) {
-          const int x = tid * KW + k;
-          if (x < nwd) {
-            dpre[x] = (int16_t)ex;
-            ex += __popc(dwords[x]);
-          }
-        }
-        if (dtotal > C::CAPD) {
-          if (tid == 0) set_ovf();
-        }
-        __syncthreads();
-      }
-      if (dense && !__hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-        auto place = [&](int u) {
-          const val_t vv = av[u];
-          const uint32_t d = (uint32_t)(r[u] - lo);
-          if (d >= tw) return;
-          const uint32_t wv = dwords[d >> 5];
-          const int slot = dpre[d >> 5] + __popc(wv & ((1u << (d & 31)) - 1u));
-          SR::lds_acc(&vals[slot], vv);
-        };
-        {
-          // value pass over the same products again (second gather, mostly cache hits): the
-          // segments are known -- LDS (one chunk) or the two HBM cursor buffers (chunked). Keeping
-          // one-window sub-tiles' products in registers instead measured slower (96.2 vs 97.7).
-          for (int ch = 0; ch < nchunks; ++ch) {
-            int nec = (int)ne;
-            if (chunked) {
-              const int64_t first = (int64_t)ch * EMAX;
-              nec = (int)((ne - first) < EMAX ? (ne - first) : EMAX);
-              const int64_t* gc = par ? a.gcur1 : a.gcur0;
-              const int64_t* gn = par ? a.gcur0 : a.gcur1;
-              for (int i = tid; i < nec; i += BS) {
-                const int64_t p0 = gc[go + first + i];
-                const int32_t len = (int32_t)(gn[go + first + i] - p0);
-                epos[i] = p0;
-                eoff[i] = len;
-                if (len > 0) escale[i] = reinterpret_cast<const b_t*>(a.Bnum)[e0 + first + i];
-              }
-              __syncthreads();
-              block_scan_excl<BS>(eoff, nec, red);
-              for (int i = tid; i < nec; i += BS) epos[i] -= eoff[i];
-            }
-            sweep(nec, eoff[nec], true, place);
-          }
-        }
-        __syncthreads();
-      }
-    }
     const bool ovf_now = __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (qtot > WIN || ovf_now) {  // table could not hold the sub-tile: halve the row range, redo
-      // restore the cursors segments() moved, unless the insertion overflow already did (hash
-      // tables only: the dense passes never raise it during the sweep). A hash sub-tile that
-      // inserted fine but occupies more slots than the commit queue holds lands here unrestored.
-      if (!chunked && (dense || !ovf_now))
+      // restore the cursors segments() moved, unless the insertion overflow already did. A hash
+      // sub-tile that inserted fine but occupies more slots than the commit queue holds lands
+      // here unrestored.
+      if (!chunked && !ovf_now)
         for (int i = tid; i < (int)ne; i += BS) epos[i] += eoff[i];
       __syncthreads();
       my_count = count_before;
@@ -830,27 +884,11 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
       }
     CBH_STAMP(9);
     if (!NUM && bitmap) {
-      for (int s = tid; s < nwd; s += BS) my_count += __popc(words[s]);
-    } else if constexpr (dense) {
-      if constexpr (NUM) {  // values are already in row order; word x's set bits are ranks dpre[x]..
-        for (int x = tid; x < nwd; x += BS) {
-          uint32_t wv = dwords[x];
-          int rk = dpre[x];
-          while (wv) {
-            const int b = __builtin_ctz(wv);
-            wv &= wv - 1u;
-            const int64_t pos = out_pos + rk;
-            if (pos >= out_end || pos >= a.ccap) {
-              bad |= 1 << 5;
-            } else {
-              a.Cir[pos] = lo + 32 * x + b;
-              reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(vals[rk]);
-            }
-            vals[rk] = SR::identity();
-            ++rk;
-          }
-        }
-        out_pos += dtotal;
+      uint32_t* sb = store ? a.bmp + a.boff[task] + ((lo - tlo) >> 5) : nullptr;
+      for (int s = tid; s < nwd; s += BS) {
+        const uint32_t wv = words[s];
+        my_count += __popc(wv);
+        if (store) sb[s] = wv;
       }
     } else if constexpr (NUM) {
       // rank commit. The occupied slots are compacted in slot order into a queue Q (the owner
