@@ -750,26 +750,50 @@ __global__ void add_i64_kernel(const int64_t* __restrict__ x, const int64_t* __r
 // the dense split could choose by its flop estimate (the outputs the split decides on are at most
 // the flops, and dense_subtiles only grows with the work), else 0. The symbolic pass writes the
 // candidates' bitmaps while it counts; the dense kernel reads them instead of marking rows again.
-__global__ void bmp_count_kernel(const int64_t* __restrict__ twork, const int32_t* __restrict__ tlo,
-                                 const int32_t* __restrict__ thi, int64_t n, int64_t T, int64_t capd, int64_t nwb,
-                                 int64_t minwork, int64_t* __restrict__ words) {
+// When they do not all fit the budget, the candidates with the highest flop density are kept
+// (quarter-octave density classes: words per class, then a class threshold).
+constexpr int kBmpClasses = 96;
+__device__ __forceinline__ int bmp_class(int64_t w, int64_t span) {
+  const float x = (float)w * 65536.0f / (float)span;  // flops per 2^16 rows
+  const int b = (int)(4.0f * log2f(x > 1.0f ? x : 1.0f));
+  return b < kBmpClasses ? b : kBmpClasses - 1;
+}
+__global__ __launch_bounds__(256) void bmp_count_kernel(const int64_t* __restrict__ twork, const int32_t* __restrict__ tlo,
+                                                        const int32_t* __restrict__ thi, int64_t n, int64_t T,
+                                                        int64_t capd, int64_t nwb, int64_t minwork, int64_t dr4,
+                                                        int min_class, int64_t* __restrict__ words,
+                                                        unsigned long long* __restrict__ class_words) {
+  __shared__ unsigned long long h[kBmpClasses];
+  for (int i = threadIdx.x; i < kBmpClasses; i += blockDim.x) h[i] = 0;
+  __syncthreads();
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const int64_t w = twork[t], span = (int64_t)thi[t] - tlo[t];
-  words[t] = (w > minwork && span > 0 && dense_subtiles(w, span, T, capd, nwb) > 0) ? (span + 31) / 32 : 0;
+  if (t < n) {
+    const int64_t w = twork[t], span = (int64_t)thi[t] - tlo[t];
+    int64_t nw = (w > minwork && span > 0 && dense_subtiles(w, span, T, capd, nwb, dr4) > 0) ? (span + 31) / 32 : 0;
+    if (nw > 0) {
+      const int b = bmp_class(w, span);
+      if (b < min_class) nw = 0;
+      else if (class_words) atomicAdd(&h[b], (unsigned long long)nw);
+    }
+    words[t] = nw;
+  }
+  __syncthreads();
+  if (class_words)
+    for (int i = threadIdx.x; i < kBmpClasses; i += blockDim.x)
+      if (h[i]) atomicAdd(&class_words[i], h[i]);
 }
 
 // numeric tasks split between the dense (bitmap-rank) and the hash kernels: wd / wh = the task's
 // output count in the kernel it goes to, 0 in the other. Dense needs a stored bitmap (boff).
 __global__ void dense_split_kernel(const int64_t* __restrict__ tcnt, const int32_t* __restrict__ tlo,
                                    const int32_t* __restrict__ thi, const int64_t* __restrict__ boff, int64_t n,
-                                   int64_t T, int64_t capd, int64_t nwb, int64_t smallcap, int enable,
+                                   int64_t T, int64_t capd, int64_t nwb, int64_t dr4, int64_t smallcap, int enable,
                                    int64_t* __restrict__ wd, int64_t* __restrict__ wh) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   const int64_t w = tcnt[t];
   const bool d = enable && boff != nullptr && boff[t + 1] > boff[t] && w > smallcap &&
-                 dense_subtiles(w, (int64_t)thi[t] - tlo[t], T, capd, nwb) > 0;
+                 dense_subtiles(w, (int64_t)thi[t] - tlo[t], T, capd, nwb, dr4) > 0;
   wd[t] = d ? w : 0;
   wh[t] = d ? 0 : w;
 }
@@ -786,6 +810,14 @@ static double phase_frac() {
   static double v = [] {
     const char* e = std::getenv("CBH_PHASE_FRAC");
     return e ? std::atof(e) : 0.5;
+  }();
+  return v;
+}
+// dense split rule (dense_subtiles): dense sub-tiles at most CBH_DRATIO4/4 of the hash ones (A/B switch)
+static int64_t dratio4() {
+  static int64_t v = [] {
+    const char* e = std::getenv("CBH_DRATIO4");
+    return e ? (int64_t)std::atoi(e) : (int64_t)kDRatio4;
   }();
   return v;
 }
@@ -1025,25 +1057,39 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   {  // stored row bitmaps of the dense candidates, within CBH_BMP_FRAC (default 0.4) of the HBM
     using CD = TaskCfg<PlusTimesD<double>, TNumLarge::T, TNumLarge::BS, TNumLarge::EMAX, TNumLarge::U, MODE_TDENSE>;
     int64_t* bw;
+    unsigned long long* cw;
     CBH_TRY(S.get(&bw, nt + 1));
+    CBH_TRY(S.get(&cw, kBmpClasses));
     CBH_TRY(S.get(&P.boff, nt + 1));
+    CBH_HIP(ctx, hipMemsetAsync(cw, 0, sizeof(unsigned long long) * kBmpClasses, ctx->stream));
     hipLaunchKernelGGL(bmp_count_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.twork, P.tlo, P.thi,
-                       P.ntasks, (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSymMidCap, bw);
+                       P.ntasks, (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSymMidCap, dratio4(), 0,
+                       bw, cw);
     CBH_HIP(ctx, hipGetLastError());
-    CBH_HIP(ctx, hipMemsetAsync(bw + P.ntasks, 0, sizeof(int64_t), ctx->stream));
-    CBH_TRY(exclusive_scan_i64(ctx, S, bw, P.boff, P.ntasks + 1));
-    int64_t words = 0;
-    CBH_HIP(ctx, hipMemcpyAsync(&words, P.boff + P.ntasks, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    unsigned long long hc[kBmpClasses];
+    CBH_HIP(ctx, hipMemcpyAsync(hc, cw, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream));
     CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
     size_t freeb = 0, totb = 0;
     CBH_HIP(ctx, hipMemGetInfo(&freeb, &totb));
     // within a fraction of the device (not of what is free: later calls find the earlier call's
-    // bitmaps in the block cache and the phase workspace resident)
-    if (words > 0 && kDenseEnabled() && (double)words * 4.0 <= bmp_frac() * (double)totb &&
-        (size_t)words * 4 < freeb + ctx->cached_bytes)
-      CBH_TRY(S.get(&P.bmp, (size_t)words));
-    if (diag_enabled())
-      std::fprintf(stderr, "[cbh diag] stored bitmaps: %.3f GB (%s)\n", words * 4e-9, P.bmp ? "kept" : "over budget: no dense");
+    // bitmaps in the block cache and the phase workspace resident), densest classes first
+    const double cap_words = std::min(bmp_frac() * (double)totb, 0.9 * (double)(freeb + ctx->cached_bytes)) / 4.0;
+    double words = 0;
+    int min_class = kBmpClasses;
+    while (min_class > 0 && words + (double)hc[min_class - 1] <= cap_words) words += (double)hc[--min_class];
+    if (min_class > 0 && words > 0)  // drop the classes that did not fit
+      hipLaunchKernelGGL(bmp_count_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.twork, P.tlo, P.thi,
+                         P.ntasks, (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSymMidCap, dratio4(),
+                         min_class, bw, nullptr);
+    CBH_HIP(ctx, hipMemsetAsync(bw + P.ntasks, 0, sizeof(int64_t), ctx->stream));
+    CBH_TRY(exclusive_scan_i64(ctx, S, bw, P.boff, P.ntasks + 1));
+    if (words > 0 && kDenseEnabled()) CBH_TRY(S.get(&P.bmp, (size_t)words));
+    if (diag_enabled()) {
+      double all = 0;
+      for (int i = 0; i < kBmpClasses; ++i) all += (double)hc[i];
+      std::fprintf(stderr, "[cbh diag] stored bitmaps: %.3f of %.3f GB (density classes >= %d)\n", words * 4e-9,
+                   all * 4e-9, min_class);
+    }
   }
   CBH_HIP(ctx, hipMemsetAsync(P.tcnt, 0, sizeof(int64_t) * (nt + 1), ctx->stream));
   BinLists bl;
@@ -1089,7 +1135,7 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
   CBH_TRY(S.get(&wd, nt));
   CBH_TRY(S.get(&wh, nt));
   hipLaunchKernelGGL(dense_split_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.tcnt + t0, P.tlo + t0,
-                     P.thi + t0, P.bmp ? P.boff + t0 : nullptr, nt, (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSmallCap,
+                     P.thi + t0, P.bmp ? P.boff + t0 : nullptr, nt, (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, dratio4(), kSmallCap,
                      kDenseEnabled() ? 1 : 0, wd, wh);
   CBH_HIP(ctx, hipGetLastError());
   BinLists bd, bl;
@@ -1798,7 +1844,7 @@ int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t
   CBH_TRY(p->S.get(&wh, nt));
   hipLaunchKernelGGL(dense_split_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.tcnt, P.tlo, P.thi,
                      P.bmp ? P.boff : nullptr, nt,
-                     (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSmallCap,
+                     (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, dratio4(), kSmallCap,
                      (kDenseEnabled() && !(flags & CBH_PLAN_NO_DENSE)) ? 1 : 0, wd, wh);
   CBH_HIP(ctx, hipGetLastError());
   BinLists bd, bl;

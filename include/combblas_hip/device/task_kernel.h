@@ -257,7 +257,8 @@ __device__ __forceinline__ int block_excl_sum(int v, int* red, int& total) {
 // most 15/16 of CAPD outputs each) are not more than 5/4 of the hash sub-tiles (T/2 outputs;
 // 4/4, 8/4 and 12/4 measured slower). Returns the dense sub-tile count, or 0 when the task stays
 // on the hash.
-__host__ __device__ inline int64_t dense_subtiles(int64_t work, int64_t span, int64_t T, int64_t capd, int64_t nwb) {
+__host__ __device__ inline int64_t dense_subtiles(int64_t work, int64_t span, int64_t T, int64_t capd, int64_t nwb,
+                                                  int64_t dratio4 = kDRatio4) {
   if (work <= 0 || span <= 0) return 0;
   const int64_t cap = T / 2;
   const int64_t R = (work + cap - 1) / cap;
@@ -265,7 +266,7 @@ __host__ __device__ inline int64_t dense_subtiles(int64_t work, int64_t span, in
   int64_t Rd = (work + cd - 1) / cd;
   const int64_t Rw = (span + 32 * nwb - 1) / (32 * nwb);
   Rd = Rd > Rw ? Rd : Rw;
-  return 4 * Rd <= kDRatio4 * R ? Rd : 0;
+  return 4 * Rd <= dratio4 * R ? Rd : 0;
 }
 
 template <class SR, int T, int BS, int EMAX, int U, int MODE>
@@ -289,16 +290,16 @@ struct TaskCfg {
   static constexpr size_t o_keys = 0;
   static constexpr size_t o_vals = al(o_keys + sizeof(int32_t) * TA);
   static constexpr size_t o_pos = al(o_vals + (NUM ? sizeof(acc_t) * TA : 0));
-  // dense numeric sub-tiles (MODE_TDENSE) lay the two tables out differently: CAPD values (the
-  // output rows are not stored: the commit reads them off the bitmap), then the rest of both
-  // tables is the bitmap (NWB words) followed by the int16 prefix popcount of every word --
-  // 32*NWB rows per sub-tile (CAPD 3072 and 135 K rows for T = 4096 with f64)
+  // dense numeric windows (MODE_TDENSE) share the two tables' LDS [0, o_pos) between values (from
+  // the bottom; the output rows are not stored: the commit reads them off the bitmap) and the
+  // window's bitmap words with their int16 prefix popcounts (6 B per word, from the top). The
+  // plan (dense_subtiles, the stored-bitmap candidates) prices a task with the split at the
+  // widest window: CAPD values and NWB words (3072 and 4224 = 135 K rows for T = 4096 with f64).
   static constexpr int CAPD = T / 4 * kCapD4;
   static constexpr size_t o_dvals = o_keys;
   static constexpr size_t o_dbits = al(o_dvals + sizeof(acc_t) * CAPD);
   static constexpr int NWB = NUM ? (int)((o_pos - o_dbits) / 6) / 8 * 8 : 0;
-  static constexpr size_t o_dpre = al(o_dbits + sizeof(uint32_t) * NWB);
-  static_assert(!DENSE || o_dpre + sizeof(int16_t) * NWB <= o_pos, "dense bitmap and prefix fit the tables");
+  static_assert(!DENSE || o_dbits + 6 * NWB <= o_pos, "dense bitmap and prefix fit the tables");
   static constexpr size_t o_end = al(o_pos + sizeof(int64_t) * EMAX);
   static constexpr size_t o_scale = al(o_end + sizeof(int64_t) * EMAX);
   static constexpr size_t o_next = al(o_scale + (NUM ? sizeof(b_t) * EMAX : 0));
@@ -587,14 +588,6 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
   if (!chunked) {
     load_entries(0, (int)ne, tlo, thi, (full & 1) != 0, false);
   }
-  uint32_t* dwords = words;  // dense: bitmap words and their int16 prefix past the CAPD values
-  int16_t* dpre = nullptr;
-  if constexpr (NUM) {
-    dwords = reinterpret_cast<uint32_t*>(smem + C::o_dbits);
-    dpre = reinterpret_cast<int16_t*>(smem + C::o_dpre);
-    if constexpr (dense)  // dense accumulators start at the identity; every commit resets what it read
-      for (int s = tid; s < C::CAPD; s += BS) vals[s] = SR::identity();
-  }
   __syncthreads();
   CBH_STAMP(0);
 
@@ -608,10 +601,13 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
   int32_t lo = tlo;
   if constexpr (dense) {
     // DENSE numeric sub-tiles are windows of the task's row bitmap, stored by the symbolic pass
-    // (TaskArgs::bmp), cut where the window's popcount would pass CAPD: the word prefix popcounts
-    // give every row its output rank before any product is gathered, so one value pass
-    // accumulates the products at their ranks, nothing overflows, windows without outputs are
-    // skipped, and the commit walks the bitmap (no row ids stored).
+    // (TaskArgs::bmp): the word prefix popcounts give every row its output rank before any product
+    // is gathered, so one value pass accumulates the products at their ranks, nothing overflows,
+    // windows without outputs are skipped, and the commit walks the bitmap (no row ids stored).
+    // The two hash tables' LDS (TB bytes) holds the values from the bottom and the window's words
+    // and prefixes (6 B per word) from the top: a window loads as many words as the task's output
+    // density says fill the values, and is cut where its outputs would overrun them -- dense
+    // columns get wide windows (5760 values at 18 % density), sparse ones long bitmaps.
     const int64_t bw0 = a.boff[task];
     const int64_t nwt = a.boff[task + 1] - bw0;
     if (a.bmp == nullptr || nwt != (span + 31) / 32) {
@@ -620,53 +616,62 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
     }
     const uint32_t* __restrict__ tb = a.bmp + bw0;
     __shared__ int32_t s_cut;
-    constexpr int KW = (C::NWB + BS - 1) / BS;
+    constexpr int64_t TB = (int64_t)C::o_pos;
+    int64_t wdes = TB * nwt / ((int64_t)sizeof(acc_t) * work + 6 * nwt);  // words whose outputs fill the rest
+    wdes = wdes < 64 ? 64 : (wdes > C::NWB ? C::NWB : wdes);
     bool inited = !chunked;  // chunked: HBM entry state is written by the first processed window
     int64_t w0 = 0;
     while (w0 < nwt) {
-      const int wl = (int)((nwt - w0) < C::NWB ? (nwt - w0) : C::NWB);
-      for (int x = tid; x < wl; x += BS) dwords[x] = tb[w0 + x];
+      const int wl = (int)((nwt - w0) < wdes ? (nwt - w0) : wdes);
+      const int dbase = (int)((TB - 6 * wl) & ~int64_t(15));
+      uint32_t* dw = reinterpret_cast<uint32_t*>(smem + dbase);
+      int16_t* dp = reinterpret_cast<int16_t*>(smem + dbase + 4 * wl);
+      const int capv = dbase / (int)sizeof(acc_t);
+      const int kw = (wl + BS - 1) / BS;
+      for (int x = tid; x < wl; x += BS) dw[x] = tb[w0 + x];
       if (tid == 0) {
         s_cut = wl;
         __hip_atomic_store(&s_ovf, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // sweep() reads it
       }
       __syncthreads();
-      // exclusive popcount prefix per word (thread-consecutive words; stride KW is odd: no bank
-      // conflicts), clamped to int16 past the cut, and the word where the prefix passes CAPD
+      // exclusive popcount prefix per word (thread-consecutive words), clamped to int16 past the
+      // cut, and the word where the prefix passes the value capacity
       int tsum = 0;
-      for (int k = 0; k < KW; ++k) {
-        const int x = tid * KW + k;
-        tsum += x < wl ? __popc(dwords[x]) : 0;
+      for (int k = 0; k < kw; ++k) {
+        const int x = tid * kw + k;
+        tsum += x < wl ? __popc(dw[x]) : 0;
       }
       int wtotal = 0;
       int ex = block_excl_sum<BS>(tsum, red, wtotal);
-      for (int k = 0; k < KW; ++k) {
-        const int x = tid * KW + k;
+      for (int k = 0; k < kw; ++k) {
+        const int x = tid * kw + k;
         if (x < wl) {
-          const int pc = __popc(dwords[x]);
-          dpre[x] = (int16_t)(ex < 32767 ? ex : 32767);
-          if (ex <= C::CAPD && ex + pc > C::CAPD) s_cut = x;
+          const int pc = __popc(dw[x]);
+          dp[x] = (int16_t)(ex < 32767 ? ex : 32767);
+          if (ex <= capv && ex + pc > capv) s_cut = x;
           ex += pc;
         }
       }
       __syncthreads();
       CBH_STAMP(1);
       const int cut = s_cut;
-      const int dtotal = cut < wl ? (int)dpre[cut] : wtotal;
+      const int dtotal = cut < wl ? (int)dp[cut] : wtotal;
       lo = (int32_t)(tlo + 32 * w0);
       const int64_t hcut = tlo + 32 * (w0 + cut);
       const int32_t hi = (int32_t)(hcut < thi ? hcut : thi);
       const uint32_t tw = (uint32_t)(hi - lo);
       if (dtotal > 0) {
+        // the window's accumulators (LDS below dbase; an earlier window's words may have been there)
+        for (int x = tid; x < dtotal; x += BS) vals[x] = SR::identity();
         auto place = [&](int u) {
           const uint32_t d = (uint32_t)(r[u] - lo);
           if (d >= tw) {
             bad |= 1 << 8;
             return;
           }
-          const uint32_t wv = dwords[d >> 5];
+          const uint32_t wv = dw[d >> 5];
           if (!((wv >> (d & 31)) & 1u)) bad |= 1 << 11;  // a product row the symbolic pass did not mark
-          const int slot = dpre[d >> 5] + __popc(wv & ((1u << (d & 31)) - 1u));
+          const int slot = dp[d >> 5] + __popc(wv & ((1u << (d & 31)) - 1u));
           SR::lds_acc(&vals[slot], av[u]);
         };
         for (int ch = 0; ch < nchunks; ++ch) {
@@ -690,22 +695,20 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
           }
           sweep(nec, P, true, place);  // ends with a barrier: the entry state may be reloaded
         }
-        // commit: values are in row order; word x's set bits are ranks dpre[x]..
-        for (int x = tid; x < cut; x += BS) {
-          uint32_t wv = dwords[x];
-          int rk = dpre[x];
-          while (wv) {
-            const int b = __builtin_ctz(wv);
-            wv &= wv - 1u;
-            const int64_t pos = out_pos + rk;
-            if (pos >= out_end || pos >= a.ccap) {
-              bad |= 1 << 5;
-            } else {
-              a.Cir[pos] = lo + 32 * x + b;
-              reinterpret_cast<val_t*>(a.Cnum)[pos] = SR::finalize(vals[rk]);
+        // commit: values are in row order (rank q = output out_pos + q: coalesced); the rows are
+        // read off the bitmap, word x's set bits being ranks dp[x]..
+        if (out_pos + dtotal > out_end || out_pos + dtotal > a.ccap) {
+          bad |= 1 << 5;
+        } else {
+          for (int q = tid; q < dtotal; q += BS)
+            reinterpret_cast<val_t*>(a.Cnum)[out_pos + q] = SR::finalize(vals[q]);
+          for (int x = tid; x < cut; x += BS) {
+            uint32_t wv = dw[x];
+            int32_t* cr = a.Cir + out_pos + dp[x];
+            while (wv) {
+              *cr++ = lo + 32 * x + __builtin_ctz(wv);
+              wv &= wv - 1u;
             }
-            vals[rk] = SR::identity();
-            ++rk;
           }
         }
         out_pos += dtotal;
