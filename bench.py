@@ -41,9 +41,11 @@ KERNELS = {"num_large": "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 51
 # every task-kernel class of the f64 PlusTimes product (the application lines pick their dominant one)
 ALL_KERNELS = dict(KERNELS, **{
     "num_mid": "cbh::task_kernel<cbh::PlusTimesD<double>, 2048, 256, 256, 4, 1, false>",
-    "num_small": "cbh::task_kernel<cbh::PlusTimesD<double>, 512, 128, 256, 4, 1, false>",
+    # one task per wave (wave_kernel.h); numeric tasks a wave table rejects rerun on
+    # task_kernel<PlusTimesD<double>, 512, 128, 256, 4, 1> inside the same timed launch
+    "num_small": "cbh::wave_kernel<cbh::PlusTimesD<double>, 512, 4, 4, 1>",
     "sym_mid": "cbh::task_kernel<cbh::PlusTimesD<long>, 4096, 256, 256, 4, 0, false>",
-    "sym_small": "cbh::task_kernel<cbh::PlusTimesD<long>, 512, 128, 256, 4, 0, false>"})
+    "sym_small": "cbh::wave_kernel<cbh::PlusTimesD<long>, 2048, 4, 4, 0>"})
 
 
 def kernel_roofline(ks, kernels=None):

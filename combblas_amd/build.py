@@ -14,7 +14,8 @@ LIB = os.path.join(HERE, "libcombblas_hip.so")
 SOURCES = ["spgemm.hip", "rmat.cpp"]
 HEADERS = ["apps.h", "convert.h", "host_util.h"] + [os.path.join("..", "..", "include", h) for h in (
     "combblas_hip.h", "combblas_hip/device/semiring.h", "combblas_hip/device/block_ops.h",
-    "combblas_hip/device/task_kernel.h", "combblas_hip/device/numeric.h")]
+    "combblas_hip/device/task_kernel.h", "combblas_hip/device/wave_kernel.h",
+    "combblas_hip/device/numeric.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("CBH_OFFLOAD_ARCH", "gfx950")
 

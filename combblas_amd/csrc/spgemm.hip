@@ -832,16 +832,15 @@ static double bmp_frac() {
 // task_kernel launch with optional HIP-event timing (kernel configurations: device/numeric.h;
 // measured at scale 22: a 1024-thread workgroup with an 8192-slot table, half the sub-tiles, ran
 // 28 % slower than two 512-thread workgroups per CU with 4096 slots)
-template <class SR, class CFG, int MODE, bool MERGE = false>
-static int launch_task(cbh_ctx* ctx, const TaskArgs& args, int64_t first, int64_t count, int kind = -1,
-                       double bytes = 0) {
-  if (count <= 0) return CBH_OK;
+// `launch` (a hipError_t-returning callable) between two timing events of kernel class `kind`
+template <class F>
+static int timed_launch(cbh_ctx* ctx, int kind, double bytes, F&& launch) {
   size_t e0 = (size_t)-1;
   if (ctx->timing && kind >= 0) {
     e0 = next_event(ctx);
     if (e0 != (size_t)-1) (void)hipEventRecord(ctx->evpool[e0], ctx->stream);
   }
-  CBH_HIP(ctx, (launch_tasks<SR, CFG, MODE, MERGE>(args, first, count, ctx->stream)));
+  CBH_HIP(ctx, launch());
   if (e0 != (size_t)-1) {
     const size_t e1 = next_event(ctx);
     if (e1 != (size_t)-1) {
@@ -850,6 +849,12 @@ static int launch_task(cbh_ctx* ctx, const TaskArgs& args, int64_t first, int64_
     }
   }
   return CBH_OK;
+}
+template <class SR, class CFG, int MODE, bool MERGE = false>
+static int launch_task(cbh_ctx* ctx, const TaskArgs& args, int64_t first, int64_t count, int kind = -1,
+                       double bytes = 0) {
+  if (count <= 0) return CBH_OK;
+  return timed_launch(ctx, kind, bytes, [&] { return launch_tasks<SR, CFG, MODE, MERGE>(args, first, count, ctx->stream); });
 }
 
 // CBH_DIAG=1: every large sub-bin launched separately with its time printed (profiling aid only)
@@ -1093,7 +1098,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   }
   CBH_HIP(ctx, hipMemsetAsync(P.tcnt, 0, sizeof(int64_t) * (nt + 1), ctx->stream));
   BinLists bl;
-  CBH_TRY(make_bins(ctx, S, P.twork, P.ntasks, 0, P.order, &bl, BinCaps{kSmallCap, kSymMidCap}, P.tunits, P.trk));
+  CBH_TRY(make_bins(ctx, S, P.twork, P.ntasks, 0, P.order, &bl, BinCaps{kSymWaveCap, kSymMidCap}, P.tunits, P.trk));
   TaskArgs a = task_args(A, B, P, ctx);
   a.twork = P.twork;
   a.cnt = P.tcnt;
@@ -1105,7 +1110,11 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   if (diag_enabled()) CBH_TRY((launch_task_diag<Dummy, TSymLarge, MODE_TSYM>(ctx, a, bl, "symbolic")));
   else CBH_TRY((launch_task<Dummy, TSymLarge, MODE_TSYM>(ctx, a, bl.large_first, bl.large_count, CBH_K_SYM_LARGE, sb_l)));
   CBH_TRY((launch_task<Dummy, TSymMid, MODE_TSYM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_SYM_MID, sb_m)));
-  CBH_TRY((launch_task<Dummy, TSymSmall, MODE_TSYM>(ctx, a, bl.small_first, bl.small_count, CBH_K_SYM_SMALL, sb_s)));
+  if (bl.small_count > 0)  // one task per wave (wave_kernel.h)
+    CBH_TRY(timed_launch(ctx, CBH_K_SYM_SMALL, sb_s, [&] {
+      return launch_waves<Dummy, WSymSmall::TW, WSymSmall::WPB, WSymSmall::U, MODE_TSYM>(a, bl.small_first, bl.small_count,
+                                                                                        ctx->stream, nullptr, nullptr);
+    }));
   // task offsets -> column pointers of C
   CBH_TRY(exclusive_scan_i64(ctx, S, P.tcnt, P.toff, P.ntasks + 1));
   hipLaunchKernelGGL(gather_i64_kernel, dim3(blocks_for(n + 1, 256)), dim3(256), 0, ctx->stream, P.toff, P.tstart,
@@ -1191,7 +1200,15 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
     CBH_TRY((launch_task<SR, TNumLarge, MODE_TNUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
   }
   CBH_TRY((launch_task<SR, TNumMid, MODE_TNUM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_NUM_MID, nb_m)));
-  CBH_TRY((launch_task<SR, TNumSmall, MODE_TNUM>(ctx, a, bl.small_first, bl.small_count, CBH_K_NUM_SMALL, nb_s)));
+  if (bl.small_count > 0) {  // one task per wave; the tasks a wave table rejects rerun on the workgroup kernel
+    int32_t* ovf;
+    int* novf;
+    CBH_TRY(S.get(&ovf, bl.small_count));
+    CBH_TRY(S.get(&novf, 1));
+    CBH_TRY(timed_launch(ctx, CBH_K_NUM_SMALL, nb_s, [&] {
+      return launch_small_numeric<SR, TNumSmall>(a, bl.small_first, bl.small_count, ctx->stream, ovf, novf);
+    }));
+  }
   if (launches) *launches += (bd.large_count > 0);
   if (launches) *launches += (bl.large_count > 0) + (bl.mid_count > 0) + (bl.small_count > 0);
   return CBH_OK;
@@ -1890,6 +1907,10 @@ int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t
   out->small_count = bl.small_count;
   out->mid_first = nd + bl.mid_first;
   out->mid_count = bl.mid_count;
+  if (bl.small_count > 0) {  // the wave kernel's rejected small tasks (device/numeric.h launch_small_numeric)
+    CBH_TRY(p->S.get(&out->wave_ovf, bl.small_count));
+    CBH_TRY(p->S.get(&out->wave_novf, 1));
+  }
   return CBH_OK;
 }
 

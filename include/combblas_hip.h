@@ -218,6 +218,7 @@ typedef struct cbh_numeric_plan {
   void* stream;                                              /* hipStream_t of the context        */
   int64_t mid_first, mid_count;                              /* mid-size hash tasks (<= 1024 out) */
   const int64_t* boff; uint32_t* bmp;                        /* stored row bitmaps of dense tasks */
+  int32_t* wave_ovf; int* wave_novf;                         /* small tasks a wave table rejected */
 } cbh_numeric_plan;
 /* bin every task for the hash kernels: the dense (bitmap-rank) kernel needs a lock-free SR::add
  * and 8-byte accumulators, the layout the plan's dense split is computed for (numeric.h

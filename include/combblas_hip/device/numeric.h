@@ -10,6 +10,7 @@
 
 #include "../../combblas_hip.h"
 #include "task_kernel.h"
+#include "wave_kernel.h"
 
 namespace cbh {
 
@@ -46,6 +47,17 @@ struct TNumSmallFor {
   static constexpr int T = bytes <= 48 ? 512 : 256;
   static constexpr int BS = 128, EMAX = 256, U = 4;
 };
+// one task per wavefront (wave_kernel.h) for the small bins: numeric tasks of <= kSmallCap outputs
+// in a 512-slot order-preserving table, symbolic tasks of <= kSymWaveCap products in a key hash of
+// twice that; four waves (four tasks) per workgroup
+struct WNumSmall { static constexpr int TW = 512, WPB = 4, U = 4; };
+constexpr int kSymWaveCap = 1024;
+struct WSymSmall { static constexpr int TW = 2 * kSymWaveCap, WPB = 4, U = 4; };
+// user value types: the wave table while a wave's LDS stays within ~16 KB
+template <class SR>
+constexpr bool wave_numeric_ok() {
+  return sizeof(typename SR::acc_t) <= 16 && sizeof(typename sr_b_type<SR>::type) <= 16;
+}
 constexpr int64_t kChunkMin = 256;  // tasks with more B entries than this keep cursors in HBM
 constexpr int64_t kSmallCap = 256;  // numeric tasks with <= kSmallCap outputs run the small kernel
 constexpr int64_t kMidCap = kMidOut;  // ... with <= kMidCap the mid kernel (library numeric pass)
@@ -135,6 +147,31 @@ constexpr uint32_t plan_flags() {
   return dense_capable<SR>() ? 0u : CBH_PLAN_NO_DENSE;
 }
 
+// Numeric tasks of the small bin: one per wave; the tasks whose wave table overflowed are rerun on
+// the workgroup kernel CFG (needs ovf = int32[count] and novf = one int of device scratch; the
+// count is read back once). Without scratch, or for wide value types, the workgroup kernel only.
+template <class SR, class CFG>
+hipError_t launch_small_numeric(const TaskArgs& a, int64_t first, int64_t count, hipStream_t s, int32_t* ovf,
+                                int* novf) {
+  if (count <= 0) return hipSuccess;
+  if constexpr (wave_numeric_ok<SR>()) {
+    if (ovf && novf) {
+      hipError_t e = hipMemsetAsync(novf, 0, sizeof(int), s);
+      if (e != hipSuccess) return e;
+      e = launch_waves<SR, WNumSmall::TW, WNumSmall::WPB, WNumSmall::U, MODE_TNUM>(a, first, count, s, ovf, novf);
+      if (e != hipSuccess) return e;
+      int h = 0;
+      e = hipMemcpyAsync(&h, novf, sizeof(int), hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e != hipSuccess || h == 0) return e;
+      TaskArgs b = a;
+      b.order = ovf;
+      return launch_tasks<SR, CFG, MODE_TNUM>(b, 0, h, s);
+    }
+  }
+  return launch_tasks<SR, CFG, MODE_TNUM>(a, first, count, s);
+}
+
 // The numeric pass of a plan for semiring SR: dense tasks (if the plan binned any), hash tasks of
 // the large, mid and small kernels, all on the plan's stream. C is the matrix cbh_plan_numeric
 // allocated with plan_flags<SR>().
@@ -153,7 +190,7 @@ hipError_t run_numeric_plan(const cbh_numeric_plan& p, int32_t* Cir, void* Cnum,
   if (e != hipSuccess) return e;
   e = launch_tasks<SR, TNumMidFor<SR>, MODE_TNUM>(a, p.mid_first, p.mid_count, s);
   if (e != hipSuccess) return e;
-  return launch_tasks<SR, TNumSmallFor<SR>, MODE_TNUM>(a, p.small_first, p.small_count, s);
+  return launch_small_numeric<SR, TNumSmallFor<SR>>(a, p.small_first, p.small_count, s, p.wave_ovf, p.wave_novf);
 }
 
 }  // namespace cbh

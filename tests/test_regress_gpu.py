@@ -82,3 +82,46 @@ def test_tc_dot_grid_cap_strides(ctx, scale, monkeypatch):
     assert int(c.num.sum()) == ref["triangles"] and vs == ref["sumC"] and dg == int(ref["digestC"])
     for S in (C, L, L2):
         S.free()
+
+
+def _wave_overflow_operands(dtype, seed):
+    """Small tasks (<= 256 outputs: the one-task-per-wave kernel) whose rows cluster: 202 rows, 200
+    of them consecutive, over a 10^6-row span -> the 512-slot order-preserving table maps the 200
+    consecutive rows to one home slot, probing passes kPmax and the wave hands the task to the
+    workgroup kernel (wave_kernel.h); every other column stays on the wave path."""
+    rng = np.random.default_rng(seed)
+    m, n = 1_000_000, 60
+    cols, rows = [], []
+    for c in range(n):
+        if c % 3 == 0:
+            r = np.concatenate([[0], 500_000 + 300 * c + np.arange(200), [m - 1]])
+        else:
+            r = np.sort(rng.choice(m, 40, replace=False))
+        rows.append(r)
+        cols.append(np.full(r.size, c))
+    rows, cols = np.concatenate(rows), np.concatenate(cols)
+    cp = np.searchsorted(cols, np.arange(n + 1)).astype(np.int64)
+    av = rng.integers(1, 9, rows.size).astype(dtype) * (1 if dtype == np.int64 else 0.5)
+    A = H.Dcsc(m, n, np.arange(n, dtype=np.int64), cp, rows.astype(np.int32), av)
+    nb = n // 2
+    bv = rng.integers(1, 5, n).astype(dtype) * (1 if dtype == np.int64 else 0.25)
+    B = H.Dcsc(n, nb, np.arange(nb, dtype=np.int64), np.arange(0, n + 1, 2, dtype=np.int64),
+               np.arange(n, dtype=np.int32), bv)
+    return A, B
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.int64])
+def test_wave_table_overflow_reruns_on_workgroup(ctx, oracle, dtype):
+    import combblas_amd as cb
+
+    A, B = _wave_overflow_operands(dtype, 5)
+    dA = cb.SpDCCols.from_host(ctx, cb.HostDcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num))
+    dB = cb.SpDCCols.from_host(ctx, cb.HostDcsc(B.m, B.n, B.jc, B.cp, B.ir, B.num))
+    C = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dA, dB)
+    h = C.to_host()
+    got = H.Dcsc(h.m, h.n, h.jc, h.cp, h.ir, h.num)
+    exp = oracle.spgemm(A, B, "plus_times", "hybrid")
+    assert np.diff(exp.cp).max() <= 256  # every column is a small (wave) task
+    H.assert_dcsc_equal(got, exp, msg=f"wave overflow, {np.dtype(dtype).name}")
+    for S in (C, dA, dB):
+        S.free()
