@@ -26,6 +26,7 @@
 #include "../../include/combblas_hip/device/numeric.h"
 #include "apps.h"
 #include "convert.h"
+#include "blocks.h"
 
 using namespace cbh;
 
@@ -1113,7 +1114,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   if (bl.small_count > 0)  // one task per wave (wave_kernel.h)
     CBH_TRY(timed_launch(ctx, CBH_K_SYM_SMALL, sb_s, [&] {
       return launch_waves<Dummy, WSymSmall::TW, WSymSmall::WPB, WSymSmall::U, MODE_TSYM>(a, bl.small_first, bl.small_count,
-                                                                                        ctx->stream, nullptr, nullptr);
+                                                                                        ctx->stream);
     }));
   // task offsets -> column pointers of C
   CBH_TRY(exclusive_scan_i64(ctx, S, P.tcnt, P.toff, P.ntasks + 1));
@@ -1200,15 +1201,10 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
     CBH_TRY((launch_task<SR, TNumLarge, MODE_TNUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
   }
   CBH_TRY((launch_task<SR, TNumMid, MODE_TNUM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_NUM_MID, nb_m)));
-  if (bl.small_count > 0) {  // one task per wave; the tasks a wave table rejects rerun on the workgroup kernel
-    int32_t* ovf;
-    int* novf;
-    CBH_TRY(S.get(&ovf, bl.small_count));
-    CBH_TRY(S.get(&novf, 1));
+  if (bl.small_count > 0)  // one task per wave (wave_kernel.h)
     CBH_TRY(timed_launch(ctx, CBH_K_NUM_SMALL, nb_s, [&] {
-      return launch_small_numeric<SR, TNumSmall>(a, bl.small_first, bl.small_count, ctx->stream, ovf, novf);
+      return launch_small_numeric<SR, TNumSmall>(a, bl.small_first, bl.small_count, ctx->stream);
     }));
-  }
   if (launches) *launches += (bd.large_count > 0);
   if (launches) *launches += (bl.large_count > 0) + (bl.mid_count > 0) + (bl.small_count > 0);
   return CBH_OK;
@@ -1907,10 +1903,6 @@ int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t
   out->small_count = bl.small_count;
   out->mid_first = nd + bl.mid_first;
   out->mid_count = bl.mid_count;
-  if (bl.small_count > 0) {  // the wave kernel's rejected small tasks (device/numeric.h launch_small_numeric)
-    CBH_TRY(p->S.get(&out->wave_ovf, bl.small_count));
-    CBH_TRY(p->S.get(&out->wave_novf, 1));
-  }
   return CBH_OK;
 }
 
@@ -2586,7 +2578,175 @@ int cbh_prune_columns(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, cbh_
   return CBH_OK;
 }
 
+// ---------------------------------------------------------------------------- block column ops
+int cbh_mat_col_slice(cbh_ctx* ctx, const cbh_mat* M, int64_t c0, int64_t c1, cbh_mat** out) {
+  if (!ctx || !M || !out) return fail(ctx, CBH_E_ARG, "null argument");
+  if (c0 < 0 || c1 < c0 || c1 > M->n) return fail(ctx, CBH_E_ARG, "column range outside the block");
+  *out = nullptr;
+  if (M->nzc == 0) {
+    CBH_TRY(new_mat(ctx, M->m, c1 - c0, 0, 0, M->dtype, out, M->vbytes));
+    CBH_HIP(ctx, hipMemsetAsync((*out)->cp, 0, sizeof(int64_t), ctx->stream));
+    return CBH_OK;
+  }
+  Scratch S(ctx);
+  int64_t* d;
+  CBH_TRY(S.get(&d, 4));
+  hipLaunchKernelGGL(col_range_kernel, dim3(1), dim3(64), 0, ctx->stream, M->jc, M->cp, M->nzc, c0, c1, d);
+  CBH_HIP(ctx, hipGetLastError());
+  int64_t h[4];
+  CBH_HIP(ctx, hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  const int64_t nzc = h[1] - h[0], nnz = h[3] - h[2];
+  cbh_mat* C;
+  CBH_TRY(new_mat(ctx, M->m, c1 - c0, nnz, nzc, M->dtype, &C, M->vbytes));
+  hipLaunchKernelGGL(add_const_i64_kernel, dim3(blocks_for(nzc + 1, 256)), dim3(256), 0, ctx->stream, M->cp + h[0],
+                     nzc + 1, -h[2], C->cp);
+  if (nzc > 0)
+    hipLaunchKernelGGL(add_const_i64_kernel, dim3(blocks_for(nzc, 256)), dim3(256), 0, ctx->stream, M->jc + h[0], nzc,
+                       -c0, C->jc);
+  if (nnz > 0) {
+    CBH_HIP(ctx, hipMemcpyAsync(C->ir, M->ir + h[2], sizeof(int32_t) * nnz, hipMemcpyDeviceToDevice, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(C->num, static_cast<const char*>(M->num) + h[2] * M->vbytes, (size_t)(nnz * M->vbytes),
+                                hipMemcpyDeviceToDevice, ctx->stream));
+  }
+  CBH_HIP(ctx, hipGetLastError());
+  *out = C;
+  return CBH_OK;
+}
+
+int cbh_mat_col_concat(cbh_ctx* ctx, int k, const cbh_mat* const* parts, cbh_mat** out) {
+  if (!ctx || !out || k < 1 || !parts) return fail(ctx, CBH_E_ARG, "bad concat arguments");
+  *out = nullptr;
+  int64_t m = 0, n = 0, nnz = 0, nzc = 0;
+  for (int i = 0; i < k; ++i) {
+    if (!parts[i]) return fail(ctx, CBH_E_ARG, "null block");
+    if (parts[i]->dtype != parts[0]->dtype || parts[i]->vbytes != parts[0]->vbytes)
+      return fail(ctx, CBH_E_ARG, "blocks of different value types");
+    m = std::max(m, parts[i]->m);
+    n += parts[i]->n;
+    nnz += parts[i]->nnz;
+    nzc += parts[i]->nzc;
+  }
+  cbh_mat* C;
+  CBH_TRY(new_mat(ctx, m, n, nnz, nzc, parts[0]->dtype, &C, parts[0]->vbytes));
+  const int64_t vb = parts[0]->vbytes;
+  int64_t coff = 0, eoff = 0, zoff = 0;
+  for (int i = 0; i < k; ++i) {
+    const cbh_mat* P = parts[i];
+    if (P->nzc > 0) {
+      hipLaunchKernelGGL(add_const_i64_kernel, dim3(blocks_for(P->nzc, 256)), dim3(256), 0, ctx->stream, P->cp, P->nzc,
+                         eoff, C->cp + zoff);
+      hipLaunchKernelGGL(add_const_i64_kernel, dim3(blocks_for(P->nzc, 256)), dim3(256), 0, ctx->stream, P->jc, P->nzc,
+                         coff, C->jc + zoff);
+    }
+    if (P->nnz > 0) {
+      CBH_HIP(ctx, hipMemcpyAsync(C->ir + eoff, P->ir, sizeof(int32_t) * P->nnz, hipMemcpyDeviceToDevice, ctx->stream));
+      CBH_HIP(ctx, hipMemcpyAsync(static_cast<char*>(C->num) + eoff * vb, P->num, (size_t)(P->nnz * vb),
+                                  hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    coff += P->n;
+    eoff += P->nnz;
+    zoff += P->nzc;
+  }
+  CBH_HIP(ctx, hipMemcpyAsync(C->cp + nzc, &nnz, sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // nnz is a host local
+  CBH_HIP(ctx, hipGetLastError());
+  *out = C;
+  return CBH_OK;
+}
+
 }  // extern "C"
+
+// ---------------------------------------------------------------------------- MCLPruneRecoverySelect
+// Kselect1 of the flagged columns into thresh (see cbh_mcl_prune_recovery_select)
+static int mcl_kselect(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const int64_t* flag, const double* tot, int64_t k,
+                       cbh_allreduce_fn colsum, void* user, double* thresh) {
+  const int64_t n = A->n;
+  int64_t* pos;
+  int32_t* aidx;
+  CBH_TRY(S.get(&pos, n + 1));
+  CBH_TRY(S.get(&aidx, n));
+  CBH_TRY(exclusive_scan_i64(ctx, S, flag, pos, n + 1));
+  int64_t nact = 0;
+  CBH_HIP(ctx, hipMemcpyAsync(&nact, pos + n, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (nact == 0) return CBH_OK;
+  hipLaunchKernelGGL(active_index_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, n, flag, pos, aidx);
+  double *kth, *totact;
+  CBH_TRY(S.get(&kth, nact));
+  CBH_TRY(S.get(&totact, nact));
+  if (!colsum) {  // columns held whole: one launch, columns staged in LDS
+    const double dmin = 2.2250738585072014e-308;
+    hipLaunchKernelGGL(fill_f64_kernel, dim3(blocks_for(nact, 256)), dim3(256), 0, ctx->stream, kth, nact, dmin);
+    CBH_TRY(cbh_kselect_cols(ctx, A, aidx, nact, k, kth));
+    hipLaunchKernelGGL(kselect_scatter_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, n, aidx, kth,
+                       (const double*)nullptr, thresh);
+  } else {  // 8 radix passes, digit histograms summed over the processor column
+    int64_t* rank;
+    uint64_t* prefix;
+    uint32_t* hist;
+    CBH_TRY(S.get(&rank, nact));
+    CBH_TRY(S.get(&prefix, nact));
+    CBH_TRY(S.get(&hist, 256 * nact));
+    hipLaunchKernelGGL(kselect_rank_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, n, aidx, tot, k, rank,
+                       prefix, totact);
+    for (int shift = 56; shift >= 0; shift -= 8) {
+      CBH_TRY(cbh_kselect_hist(ctx, A, aidx, nact, prefix, shift, hist));
+      const int rc = colsum(user, hist, 256 * nact, CBH_REDUCE_U32);
+      if (rc != 0) return fail(ctx, rc, "processor-column reduction of the Kselect histograms failed");
+      CBH_TRY(cbh_kselect_pick(ctx, nact, hist, prefix, rank, shift));
+    }
+    CBH_TRY(cbh_kselect_value(ctx, nact, prefix, kth));
+    hipLaunchKernelGGL(kselect_scatter_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, n, aidx, kth, totact,
+                       thresh);
+  }
+  CBH_HIP(ctx, hipGetLastError());
+  return CBH_OK;
+}
+
+extern "C" int cbh_mcl_prune_recovery_select(cbh_ctx* ctx, const cbh_mat* A, double hardThreshold, int64_t selectNum,
+                                             int64_t recoverNum, double recoverPct, cbh_allreduce_fn colsum,
+                                             void* user, cbh_mat** C) {
+  CBH_TRY(need_f64(ctx, A));
+  if (!C) return fail(ctx, CBH_E_ARG, "null output");
+  *C = nullptr;
+  const int64_t n = A->n;
+  if (n == 0) return empty_result(ctx, A->m, A->n, A->dtype, C);
+  Scratch S(ctx);
+  double *st, *thresh, *kept;
+  int64_t *rec, *sel, *s2;
+  CBH_TRY(S.get(&st, 3 * n));  // cnt | cntp | sump, reduced in one call
+  CBH_TRY(S.get(&thresh, n));
+  CBH_TRY(S.get(&kept, 2 * n));
+  CBH_TRY(S.get(&rec, n + 1));
+  CBH_TRY(S.get(&sel, n + 1));
+  CBH_TRY(S.get(&s2, n + 1));
+  double *cnt = st, *cntp = st + n, *sump = st + 2 * n;
+  CBH_TRY(cbh_col_stats(ctx, A, hardThreshold, cnt, cntp, sump));
+  if (colsum) {
+    const int rc = colsum(user, st, 3 * n, CBH_REDUCE_F64);
+    if (rc != 0) return fail(ctx, rc, "processor-column reduction of the column statistics failed");
+  }
+  hipLaunchKernelGGL(mcl_flags_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, n, cnt, cntp, sump,
+                     hardThreshold, selectNum, recoverNum, recoverPct, thresh, rec, sel);
+  CBH_HIP(ctx, hipGetLastError());
+  // recovery: the recoverNum-th largest of the UNPRUNED column (A.Kselect, ParFriends.h:221-236)
+  if (recoverNum > 0) CBH_TRY(mcl_kselect(ctx, S, A, rec, cnt, recoverNum, colsum, user, thresh));
+  if (selectNum > 0) {  // selection (:239-270), then recovery of what selection left too thin (:272-330)
+    CBH_TRY(mcl_kselect(ctx, S, A, sel, cnt, selectNum, colsum, user, thresh));
+    if (recoverNum > 0) {
+      CBH_TRY(cbh_col_stats_kept(ctx, A, thresh, kept, kept + n));
+      if (colsum) {
+        const int rc = colsum(user, kept, 2 * n, CBH_REDUCE_F64);
+        if (rc != 0) return fail(ctx, rc, "processor-column reduction of the kept statistics failed");
+      }
+      hipLaunchKernelGGL(mcl_recheck_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, n, sel, kept,
+                         kept + n, recoverNum, recoverPct, s2);
+      CBH_TRY(mcl_kselect(ctx, S, A, s2, cnt, recoverNum, colsum, user, thresh));
+    }
+  }
+  return cbh_prune_columns(ctx, A, thresh, C);  // PruneColumn(pruneCols, less, true) (:343)
+}
 
 // ============================================================================ format conversions
 // SURVEY.md §8(f)3 (kernels in convert.h): the SpTuples -> SpDCCols build and back, on the device.

@@ -218,7 +218,6 @@ typedef struct cbh_numeric_plan {
   void* stream;                                              /* hipStream_t of the context        */
   int64_t mid_first, mid_count;                              /* mid-size hash tasks (<= 1024 out) */
   const int64_t* boff; uint32_t* bmp;                        /* stored row bitmaps of dense tasks */
-  int32_t* wave_ovf; int* wave_novf;                         /* small tasks a wave table rejected */
 } cbh_numeric_plan;
 /* bin every task for the hash kernels: the dense (bitmap-rank) kernel needs a lock-free SR::add
  * and 8-byte accumulators, the layout the plan's dense split is computed for (numeric.h
@@ -290,6 +289,28 @@ int cbh_kselect_cols(cbh_ctx* ctx, const cbh_mat* A, const int32_t* active_index
                      double* out);
 int cbh_prune_columns(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, cbh_mat** C);
 int cbh_col_stats_kept(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, double* cntk, double* sumk);
+
+/* Whole-block MCLPruneRecoverySelect (ParFriends.h:185-353) on the device: column statistics,
+ * recovery / selection Kselect1 (recoverNum-th / selectNum-th largest), the recovery check after
+ * selection, then PruneColumn -- C is the pruned block (a new matrix; A is kept). Where the block's
+ * columns are split over a processor column, `colsum` (non-NULL) sums a device buffer over it in
+ * place (MPI_Allreduce / ncclAllReduce, the reference's Reduce(Column, ...) and Kselect1 gathers):
+ * count values of type CBH_REDUCE_F64 (double) or CBH_REDUCE_U32 (uint32 histograms), queued on
+ * the context stream; a nonzero return aborts with that code. NULL: columns held whole.          */
+#define CBH_REDUCE_F64 0
+#define CBH_REDUCE_U32 1
+typedef int (*cbh_allreduce_fn)(void* user, void* dev_buf, int64_t count, int type);
+int cbh_mcl_prune_recovery_select(cbh_ctx* ctx, const cbh_mat* A, double hardThreshold, int64_t selectNum,
+                                  int64_t recoverNum, double recoverPct, cbh_allreduce_fn colsum, void* user,
+                                  cbh_mat** C);
+
+/* ---------------------------------------------------------------- block column operations
+ *   cbh_mat_col_slice   columns [c0, c1) of M as a new m x (c1-c0) block, ids rebased
+ *                       (one piece of SpDCCols::ColSplit, SpDCCols.cpp:936-1012)
+ *   cbh_mat_col_concat  the k blocks side by side (SpDCCols::ColConcatenate, SpDCCols.cpp:1014-1090):
+ *                       rows = the largest m, columns offset by the earlier blocks' n            */
+int cbh_mat_col_slice(cbh_ctx* ctx, const cbh_mat* M, int64_t c0, int64_t c1, cbh_mat** out);
+int cbh_mat_col_concat(cbh_ctx* ctx, int k, const cbh_mat* const* parts, cbh_mat** out);
 
 /* ---------------------------------------------------------------- format conversions (device)
  *   cbh_tuples_to_dcsc  device COO (rows, cols, vals; any order, duplicates allowed) -> a DCSC block:

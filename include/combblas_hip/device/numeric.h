@@ -48,7 +48,7 @@ struct TNumSmallFor {
   static constexpr int BS = 128, EMAX = 256, U = 4;
 };
 // one task per wavefront (wave_kernel.h) for the small bins: numeric tasks of <= kSmallCap outputs
-// in a 512-slot order-preserving table, symbolic tasks of <= kSymWaveCap products in a key hash of
+// in a 512-slot key hash (counting commit), symbolic tasks of <= kSymWaveCap products in a key hash of
 // twice that; four waves (four tasks) per workgroup
 struct WNumSmall { static constexpr int TW = 512, WPB = 4, U = 4; };
 constexpr int kSymWaveCap = 1024;
@@ -147,28 +147,13 @@ constexpr uint32_t plan_flags() {
   return dense_capable<SR>() ? 0u : CBH_PLAN_NO_DENSE;
 }
 
-// Numeric tasks of the small bin: one per wave; the tasks whose wave table overflowed are rerun on
-// the workgroup kernel CFG (needs ovf = int32[count] and novf = one int of device scratch; the
-// count is read back once). Without scratch, or for wide value types, the workgroup kernel only.
+// Numeric tasks of the small bin: one per wave (wave_kernel.h); wide user value types keep the
+// workgroup kernel CFG.
 template <class SR, class CFG>
-hipError_t launch_small_numeric(const TaskArgs& a, int64_t first, int64_t count, hipStream_t s, int32_t* ovf,
-                                int* novf) {
+hipError_t launch_small_numeric(const TaskArgs& a, int64_t first, int64_t count, hipStream_t s) {
   if (count <= 0) return hipSuccess;
-  if constexpr (wave_numeric_ok<SR>()) {
-    if (ovf && novf) {
-      hipError_t e = hipMemsetAsync(novf, 0, sizeof(int), s);
-      if (e != hipSuccess) return e;
-      e = launch_waves<SR, WNumSmall::TW, WNumSmall::WPB, WNumSmall::U, MODE_TNUM>(a, first, count, s, ovf, novf);
-      if (e != hipSuccess) return e;
-      int h = 0;
-      e = hipMemcpyAsync(&h, novf, sizeof(int), hipMemcpyDeviceToHost, s);
-      if (e == hipSuccess) e = hipStreamSynchronize(s);
-      if (e != hipSuccess || h == 0) return e;
-      TaskArgs b = a;
-      b.order = ovf;
-      return launch_tasks<SR, CFG, MODE_TNUM>(b, 0, h, s);
-    }
-  }
+  if constexpr (wave_numeric_ok<SR>())
+    return launch_waves<SR, WNumSmall::TW, WNumSmall::WPB, WNumSmall::U, MODE_TNUM>(a, first, count, s);
   return launch_tasks<SR, CFG, MODE_TNUM>(a, first, count, s);
 }
 
@@ -190,7 +175,7 @@ hipError_t run_numeric_plan(const cbh_numeric_plan& p, int32_t* Cir, void* Cnum,
   if (e != hipSuccess) return e;
   e = launch_tasks<SR, TNumMidFor<SR>, MODE_TNUM>(a, p.mid_first, p.mid_count, s);
   if (e != hipSuccess) return e;
-  return launch_small_numeric<SR, TNumSmallFor<SR>>(a, p.small_first, p.small_count, s, p.wave_ovf, p.wave_novf);
+  return launch_small_numeric<SR, TNumSmallFor<SR>>(a, p.small_first, p.small_count, s);
 }
 
 }  // namespace cbh

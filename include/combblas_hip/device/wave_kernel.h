@@ -9,11 +9,13 @@
 // update. Tasks come from the small bins, so one table holds the whole task (no sub-tiles):
 //   symbolic (MODE_TSYM): multiplicative key hash of TW >= 2 x products slots (never fills), the
 //            count of first insertions -> cnt[task]                       [estimateNNZ_Hash]
-//   numeric  (MODE_TNUM): the order-preserving table of task_kernel.h (slot = (row-lo)*TW/span,
-//            forward probing, kGuard slots past TW) with TW >= 2 x outputs, then the same rank
-//            commit (rank_commit_batch) over the wave's queue of occupied slots. A task whose
-//            probing overflows (clustered rows) writes nothing and is appended to `ovf`; the host
-//            reruns those tasks on the workgroup kernel, which splits sub-tiles.
+//   numeric  (MODE_TNUM): the same key hash (TW >= 2 x outputs) with SR::add(SR::multiply(a,b))
+//            into the slot's accumulator, then a COUNTING commit: the occupied keys are compacted
+//            into a list and every key's output position is the number of smaller keys in it
+//            (broadcast LDS reads, no dependent chains; <= TW/2 keys). The workgroup kernels'
+//            order-preserving slot map (slot = (row-lo)*T/span) is not used here: short columns of
+//            structured matrices (C3's stencil x prolongation) cluster their rows in a few narrow
+//            bands, which it maps to a few home slots -- probe chains of ~25 CAS per product.
 #pragma once
 #include "task_kernel.h"
 
@@ -32,18 +34,19 @@ struct WaveCfg {
   static constexpr bool NUM = MODE == MODE_TNUM;
   using acc_t = typename SR::acc_t;
   using b_t = typename sr_b_type<SR>::type;
-  static constexpr int TA = NUM ? TW + kGuard : TW;
+  static constexpr int NOUT = TW / 2;  // outputs (keys) a task may have
   static constexpr size_t al(size_t x) { return (x + 15) & ~size_t(15); }
   static constexpr size_t o_keys = 0;
-  static constexpr size_t o_vals = al(sizeof(int32_t) * TA);
-  static constexpr size_t o_base = al(o_vals + (NUM ? sizeof(acc_t) * TA : 0));  // 64 gather bases
+  static constexpr size_t o_vals = al(sizeof(int32_t) * TW);
+  static constexpr size_t o_base = al(o_vals + (NUM ? sizeof(acc_t) * TW : 0));  // 64 gather bases
   static constexpr size_t o_scale = al(o_base + sizeof(int64_t) * 64);           // 64 B values
-  static constexpr size_t o_q = al(o_scale + (NUM ? sizeof(b_t) * 64 : 0));       // commit queue
-  static constexpr size_t bytes = al(o_q + (NUM ? sizeof(int16_t) * TA : 0));    // per wave
+  static constexpr size_t o_klist = al(o_scale + (NUM ? sizeof(b_t) * 64 : 0));   // commit: keys (+4 pad)
+  static constexpr size_t o_q = al(o_klist + (NUM ? sizeof(int32_t) * (NOUT + 4) : 0));  // their slots
+  static constexpr size_t bytes = al(o_q + (NUM ? sizeof(int16_t) * NOUT : 0));  // per wave
 };
 
 template <class SR, int TW, int WPB, int U, int MODE>
-__global__ __launch_bounds__(64 * WPB) void wave_kernel(TaskArgs a, int32_t* __restrict__ ovf, int* __restrict__ novf) {
+__global__ __launch_bounds__(64 * WPB) void wave_kernel(TaskArgs a) {
   using C = WaveCfg<SR, TW, MODE>;
   using val_t = typename SR::val_t;
   using acc_t = typename SR::acc_t;
@@ -51,7 +54,6 @@ __global__ __launch_bounds__(64 * WPB) void wave_kernel(TaskArgs a, int32_t* __r
   using b_t = typename C::b_t;
   constexpr bool NUM = C::NUM;
   constexpr bool LOCKED = sr_locked<SR>::value;
-  constexpr int TA = C::TA;
   static_assert((TW & (TW - 1)) == 0 && TW >= 64, "table size must be a power of two");
   static_assert(MODE == MODE_TSYM || MODE == MODE_TNUM, "wave kernel: symbolic or numeric hash");
 
@@ -64,6 +66,7 @@ __global__ __launch_bounds__(64 * WPB) void wave_kernel(TaskArgs a, int32_t* __r
   acc_t* vals = reinterpret_cast<acc_t*>(wb + C::o_vals);
   int64_t* ebase = reinterpret_cast<int64_t*>(wb + C::o_base);
   b_t* escale = reinterpret_cast<b_t*>(wb + C::o_scale);
+  int32_t* klist = reinterpret_cast<int32_t*>(wb + C::o_klist);
   int16_t* Q = reinterpret_cast<int16_t*>(wb + C::o_q);
   const int32_t* __restrict__ rowsA = a.Air;
 
@@ -82,14 +85,12 @@ __global__ __launch_bounds__(64 * WPB) void wave_kernel(TaskArgs a, int32_t* __r
     if (!NUM && lane == 0) a.cnt[task] = 0;
     return;
   }
-  for (int s = lane; s < TA; s += 64) {
+  for (int s = lane; s < TW; s += 64) {
     keys[s] = kEmpty;
     if constexpr (NUM && !LOCKED) vals[s] = SR::identity();
   }
   const uint32_t tw = (uint32_t)(thi - tlo);
-  const uint64_t scale = ((uint64_t)TW << 32) / (uint64_t)tw;  // numeric order-preserving slot map
   int my_count = 0;  // symbolic: keys this lane inserted first
-  bool ovf_lane = false;
   int bad = 0;
   wave_lds_sync();
 
@@ -152,33 +153,22 @@ __global__ __launch_bounds__(64 * WPB) void wave_kernel(TaskArgs a, int32_t* __r
           bad |= 1 << 8;
           continue;
         }
-        if constexpr (NUM) {
-          uint32_t s = (uint32_t)(((uint64_t)d * scale) >> 32);
-          bool ok = false;
-          if constexpr (LOCKED) {
-            for (int probe = 0; probe < kPmax && s < (uint32_t)TA; ++probe, ++s)
-              if (locked_insert<SR>(&keys[s], &vals[s], r[u], av[u])) {
-                ok = true;
-                break;
-              }
+        // key hash with wrap-around probing: at most TW/2 distinct keys, so a free slot is always
+        // found (the bins guarantee the bound; a key past it is a count mismatch below)
+        constexpr int LG = __builtin_ctz(TW);
+        uint32_t s = ((uint32_t)r[u] * 0x9E3779B1u) >> (32 - LG);
+        for (int probe = 0; probe < TW; ++probe, s = (s + 1) & (TW - 1)) {
+          if constexpr (NUM && LOCKED) {
+            if (locked_insert<SR>(&keys[s], &vals[s], r[u], av[u])) break;
           } else {
-            for (int probe = 0; probe < kPmax && s < (uint32_t)TA; ++probe, ++s) {
-              const int32_t k = atomicCAS(&keys[s], kEmpty, r[u]);
-              if (k == kEmpty || k == r[u]) {
-                SR::lds_acc(&vals[s], av[u]);
-                ok = true;
-                break;
-              }
-            }
-          }
-          if (!ok) ovf_lane = true;
-        } else {
-          constexpr int LG = __builtin_ctz(TW);
-          uint32_t s = ((uint32_t)r[u] * 0x9E3779B1u) >> (32 - LG);
-          for (int probe = 0; probe < TW; ++probe, s = (s + 1) & (TW - 1)) {
             const int32_t k = atomicCAS(&keys[s], kEmpty, r[u]);
-            if (k == kEmpty) ++my_count;
-            if (k == kEmpty || k == r[u]) break;
+            if constexpr (!NUM) {
+              if (k == kEmpty) ++my_count;
+            }
+            if (k == kEmpty || k == r[u]) {
+              if constexpr (NUM) SR::lds_acc(&vals[s], av[u]);
+              break;
+            }
           }
         }
       }
@@ -192,38 +182,66 @@ __global__ __launch_bounds__(64 * WPB) void wave_kernel(TaskArgs a, int32_t* __r
     for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
     if (lane == 0) a.cnt[task] = t;
   } else {
-    if (__ballot(ovf_lane) != 0ull) {  // rerun on the workgroup kernel (sub-tiles)
-      if (lane == 0) ovf[atomicAdd(novf, 1)] = task;
-      return;
-    }
-    // queue of the occupied slots in slot order (ballot + popcount), then the rank commit
+    // occupied keys (and their slots) compacted into a list; a key's output position is the
+    // number of smaller keys in the list (keys are distinct rows): 4 keys per lane, the list read
+    // by broadcast in 16-byte groups
     const uint64_t lt = (1ull << lane) - 1ull;
-    int qo = 0;
-    for (int b = 0; b < (TA + 63) / 64; ++b) {
+    int n = 0;
+    for (int b = 0; b < TW / 64; ++b) {
       const int sl = 64 * b + lane;
-      const uint64_t m = __ballot(sl < TA && keys[sl] != kEmpty);
-      if ((m >> lane) & 1ull) Q[qo + __popcll(m & lt)] = (int16_t)sl;
-      qo += __popcll(m);
+      const int32_t k = keys[sl];
+      const uint64_t m = __ballot(k != kEmpty);
+      const int at = n + __popcll(m & lt);
+      if (k != kEmpty && at < C::NOUT) {
+        klist[at] = k;
+        Q[at] = (int16_t)sl;
+      }
+      n += __popcll(m);
     }
-    wave_lds_sync();
     const int64_t out_pos = a.toff[task] - a.cbase;
     const int64_t out_end = a.toff[task + 1] - a.cbase;
-    if (out_pos + qo != out_end) {
+    if (n > C::NOUT || out_pos + n != out_end) {
       if (lane == 0) atomicAdd(&a.err[0], 1);  // count mismatch with the symbolic pass
     } else {
-      for (int b0 = 0; b0 < qo; b0 += 64)
-        bad |= rank_commit_batch<SR>(keys, vals, Q, qo, b0, out_pos, out_end, a.ccap, a.Cir,
-                                     reinterpret_cast<val_t*>(a.Cnum));
+      if (lane < 4) klist[n + lane] = kNoRow;  // pad of the 16-byte groups (> every row)
+      wave_lds_sync();
+      constexpr int NK = C::NOUT / 64;
+      int32_t key[NK];
+      int rank[NK];
+#pragma unroll
+      for (int i = 0; i < NK; ++i) {
+        key[i] = 64 * i + lane < n ? klist[64 * i + lane] : kNoRow;
+        rank[i] = 0;
+      }
+      const int nk = (n + 63) / 64;
+      for (int t = 0; t < n; t += 4) {
+        const int4 v = *reinterpret_cast<const int4*>(&klist[t]);
+#pragma unroll
+        for (int i = 0; i < NK; ++i)
+          if (i < nk) rank[i] += (v.x < key[i]) + (v.y < key[i]) + (v.z < key[i]) + (v.w < key[i]);
+      }
+      val_t* __restrict__ Cnum = reinterpret_cast<val_t*>(a.Cnum);
+#pragma unroll
+      for (int i = 0; i < NK; ++i) {
+        const int q = 64 * i + lane;
+        if (q < n) {
+          const int64_t pos = out_pos + rank[i];
+          if (pos >= out_end || pos >= a.ccap) {
+            bad |= 1 << 5;
+          } else {
+            a.Cir[pos] = key[i];
+            Cnum[pos] = SR::finalize(vals[Q[q]]);
+          }
+        }
+      }
     }
   }
   if (bad) guard_fail(a.err, 31 - __clz(bad), c, bad, task);
 }
 
 // Launches wave_kernel over order[first, first+count) in grid slices below 2^32 work-items.
-// Numeric: tasks that overflowed are appended to ovf (novf counts them; zeroed by the caller).
 template <class SR, int TW, int WPB, int U, int MODE>
-hipError_t launch_waves(const TaskArgs& args, int64_t first, int64_t count, hipStream_t stream, int32_t* ovf,
-                        int* novf) {
+hipError_t launch_waves(const TaskArgs& args, int64_t first, int64_t count, hipStream_t stream) {
   if (count <= 0) return hipSuccess;
   using C = WaveCfg<SR, TW, MODE>;
   auto kern = wave_kernel<SR, TW, WPB, U, MODE>;
@@ -240,7 +258,7 @@ hipError_t launch_waves(const TaskArgs& args, int64_t first, int64_t count, hipS
     TaskArgs b = args;
     b.order = args.order + first + off;
     b.norder = n;
-    hipLaunchKernelGGL(kern, dim3((unsigned)((n + WPB - 1) / WPB)), dim3(64 * WPB), C::bytes * WPB, stream, b, ovf, novf);
+    hipLaunchKernelGGL(kern, dim3((unsigned)((n + WPB - 1) / WPB)), dim3(64 * WPB), C::bytes * WPB, stream, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

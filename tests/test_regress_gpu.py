@@ -86,9 +86,8 @@ def test_tc_dot_grid_cap_strides(ctx, scale, monkeypatch):
 
 def _wave_overflow_operands(dtype, seed):
     """Small tasks (<= 256 outputs: the one-task-per-wave kernel) whose rows cluster: 202 rows, 200
-    of them consecutive, over a 10^6-row span -> the 512-slot order-preserving table maps the 200
-    consecutive rows to one home slot, probing passes kPmax and the wave hands the task to the
-    workgroup kernel (wave_kernel.h); every other column stays on the wave path."""
+    of them consecutive, over a 10^6-row span (an order-preserving slot map would put the 200 rows
+    on one home slot; the wave kernel's key hash and counting commit must order them)."""
     rng = np.random.default_rng(seed)
     m, n = 1_000_000, 60
     cols, rows = [], []
@@ -111,7 +110,7 @@ def _wave_overflow_operands(dtype, seed):
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.int64])
-def test_wave_table_overflow_reruns_on_workgroup(ctx, oracle, dtype):
+def test_wave_clustered_rows(ctx, oracle, dtype):
     import combblas_amd as cb
 
     A, B = _wave_overflow_operands(dtype, 5)
@@ -122,6 +121,6 @@ def test_wave_table_overflow_reruns_on_workgroup(ctx, oracle, dtype):
     got = H.Dcsc(h.m, h.n, h.jc, h.cp, h.ir, h.num)
     exp = oracle.spgemm(A, B, "plus_times", "hybrid")
     assert np.diff(exp.cp).max() <= 256  # every column is a small (wave) task
-    H.assert_dcsc_equal(got, exp, msg=f"wave overflow, {np.dtype(dtype).name}")
+    H.assert_dcsc_equal(got, exp, msg=f"wave clustered rows, {np.dtype(dtype).name}")
     for S in (C, dA, dB):
         S.free()
