@@ -1,0 +1,399 @@
+// ParFriendsDev.h -- the reference's PHASED and 3D SpGEMM drivers for device-resident blocks.
+//
+// Overloads, for SpParMat / SpParMat3D over SpDCColsDev (more specialized than the reference's
+// templates, so HipMCL's own calls -- Applications/MCL.cpp:574-577 -- resolve to them):
+//   MCLPruneRecoverySelect   ParFriends.h:185-353   whole local block on the device
+//                                                   (cbh_mcl_prune_recovery_select), column
+//                                                   statistics and Kselect histograms summed over
+//                                                   the processor column with ncclAllReduce
+//   EstPerProcessNnzSUMMA    ParFriends.h:1243-1340 stage broadcasts + device symbolic pass
+//   MemEfficientSpGEMM       ParFriends.h:449-730   B's block cut in `phases` column pieces
+//                                                   (ColSplit), per phase the device SUMMA
+//                                                   (summa_blocks) and MCLPruneRecoverySelect, the
+//                                                   pruned pieces concatenated (ColConcatenate)
+//   Mult_AnXBn_SUMMA3D       ParFriends.h:2918-3208 layer SUMMA, then the fiber reduce-scatter
+//                                                   (:3097-3183) as device column pieces exchanged
+//                                                   with grouped ncclSend / ncclRecv and merged
+//   MemEfficientSpGEMM3D     ParFriends.h:3214-3705 B's layer block cut in `layers` chunks, each in
+//                                                   `phases` pieces; phase p = piece p of every
+//                                                   chunk: layer SUMMA, fiber reduce-scatter,
+//                                                   prune on the layer grid, concatenation
+// Every block, stage partial and piece stays in HBM; only sizes (essentials) cross the host.
+// COMBBLAS_HIP_COMM=mpi stages the exchanges through host MPI instead of RCCL (test rehearsal of
+// several ranks sharing one GPU).
+#pragma once
+
+#include <cmath>
+
+#include "CombBLAS/CommGrid3D.h"
+#include "CombBLAS/SpParMat3D.h"
+#include "SpParMatDev.h"
+
+namespace combblas_hip {
+
+inline cbh_mat* col_slice(const cbh_mat* M, int64_t c0, int64_t c1) {
+  cbh_mat* out = nullptr;
+  int rc = cbh_mat_col_slice(context(), M, c0, c1, &out);
+  if (rc != CBH_OK) die(context(), rc, "cbh_mat_col_slice");
+  return out;
+}
+// ColConcatenate of the blocks (freed)
+inline cbh_mat* col_concat(std::vector<cbh_mat*>& parts) {
+  cbh_mat* out = nullptr;
+  int rc = cbh_mat_col_concat(context(), (int)parts.size(), parts.data(), &out);
+  if (rc != CBH_OK) die(context(), rc, "cbh_mat_col_concat");
+  for (cbh_mat* p : parts) cbh_mat_free(context(), p);
+  parts.clear();
+  return out;
+}
+inline std::vector<int64_t> essentials(const cbh_mat* M) {  // {nnz, m, n, nzc}
+  int64_t m = 0, n = 0, nnz = 0, nzc = 0;
+  cbh_mat_info(M, &m, &n, &nnz, &nzc, nullptr);
+  return {nnz, m, n, nzc};
+}
+// SpDCCols::ColSplit(parts) cuts: (i+1) * (n/parts), the last piece takes the remainder
+inline std::vector<int64_t> colsplit_cuts(int64_t n, int parts) {
+  std::vector<int64_t> c{0};
+  for (int i = 1; i < parts; ++i) c.push_back(i * (n / parts));
+  c.push_back(n);
+  return c;
+}
+
+// in-place sum of a device buffer over an MPI communicator (the cbh_allreduce_fn of
+// cbh_mcl_prune_recovery_select): ncclAllReduce on the mirrored RCCL communicator, or host staged
+inline int comm_allreduce_sum(void* user, void* buf, int64_t count, int type) {
+  MPI_Comm comm = *static_cast<MPI_Comm*>(user);
+  hipStream_t s = reinterpret_cast<hipStream_t>(cbh_ctx_stream(context()));
+  const size_t esz = type == CBH_REDUCE_F64 ? sizeof(double) : sizeof(uint32_t);
+  if (use_mpi_transport()) {
+    std::vector<char> h(esz * (size_t)count);
+    if (hipMemcpyAsync(h.data(), buf, h.size(), hipMemcpyDeviceToHost, s) != hipSuccess) return CBH_E_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return CBH_E_HIP;
+    MPI_Allreduce(MPI_IN_PLACE, h.data(), (int)count, type == CBH_REDUCE_F64 ? MPI_DOUBLE : MPI_UINT32_T, MPI_SUM, comm);
+    if (hipMemcpyAsync(buf, h.data(), h.size(), hipMemcpyHostToDevice, s) != hipSuccess) return CBH_E_HIP;
+    return hipStreamSynchronize(s) == hipSuccess ? 0 : CBH_E_HIP;
+  }
+  ncclComm_t nc = rccl_comm_for(comm);
+  return ncclAllReduce(buf, buf, (size_t)count, type == CBH_REDUCE_F64 ? ncclFloat64 : ncclUint32, ncclSum, nc, s) ==
+                 ncclSuccess
+             ? 0
+             : CBH_E_HIP;
+}
+
+// MCLPruneRecoverySelect of a device block whose columns are split over `colworld`
+inline cbh_mat* mcl_prune_block(const cbh_mat* A, MPI_Comm colworld, double hard, int64_t selectNum,
+                                int64_t recoverNum, double recoverPct) {
+  int size = 1;
+  MPI_Comm_size(colworld, &size);
+  MPI_Comm comm = colworld;
+  cbh_mat* C = nullptr;
+  int rc = cbh_mcl_prune_recovery_select(context(), A, hard, selectNum, recoverNum, recoverPct,
+                                         size > 1 ? comm_allreduce_sum : nullptr, &comm, &C);
+  if (rc != CBH_OK) die(context(), rc, "cbh_mcl_prune_recovery_select");
+  return C;
+}
+
+// The fiber reduce-scatter of Mult_AnXBn_SUMMA3D (ParFriends.h:3097-3183) on device blocks: the
+// layer partial P is cut into column pieces of widths div[0..L) (ids rebased), piece j goes to
+// fiber rank j -- essentials by MPI_Alltoall, the arrays by grouped ncclSend / ncclRecv (host
+// staged with COMBBLAS_HIP_COMM=mpi) -- and the L pieces of this rank's chunk are merged
+// (MultiwayMergeHash there; the device merge keeps rows sorted). P is freed.
+inline cbh_mat* fiber_reduce_scatter(cbh_semiring sr, cbh_mat* P, const std::vector<int64_t>& div, MPI_Comm fiber,
+                                     int dtype, int64_t vbytes) {
+  int L = 1, me = 0;
+  MPI_Comm_size(fiber, &L);
+  MPI_Comm_rank(fiber, &me);
+  std::vector<cbh_mat*> send(L), recv(L, nullptr);
+  int64_t c0 = 0;
+  for (int j = 0; j < L; ++j) {
+    send[j] = col_slice(P, c0, c0 + div[j]);
+    c0 += div[j];
+  }
+  cbh_mat_free(context(), P);
+  std::vector<int64_t> sess(4 * (size_t)L), ress(4 * (size_t)L);
+  for (int j = 0; j < L; ++j) {
+    const auto e = essentials(send[j]);
+    std::copy(e.begin(), e.end(), sess.begin() + 4 * j);
+  }
+  MPI_Alltoall(sess.data(), 4, MPI_INT64_T, ress.data(), 4, MPI_INT64_T, fiber);
+  recv[me] = send[me];
+  for (int j = 0; j < L; ++j) {
+    if (j == me) continue;
+    int rc = cbh_mat_create(context(), ress[4 * j + 1], ress[4 * j + 2], ress[4 * j], ress[4 * j + 3], (cbh_dtype)dtype,
+                            vbytes, &recv[j]);
+    if (rc != CBH_OK) die(context(), rc, "cbh_mat_create");
+  }
+  struct Arrs {
+    void* p[4];
+    size_t b[4];
+  };
+  auto arrays = [&](cbh_mat* M) {
+    const int64_t *cp, *jc;
+    const int32_t* ir;
+    const void* num;
+    cbh_mat_device_arrays(M, &cp, &jc, &ir, &num);
+    const auto e = essentials(M);
+    return Arrs{{const_cast<int64_t*>(cp), const_cast<int64_t*>(jc), const_cast<int32_t*>(ir), const_cast<void*>(num)},
+                {sizeof(int64_t) * (size_t)(e[3] + 1), sizeof(int64_t) * (size_t)e[3], sizeof(int32_t) * (size_t)e[0],
+                 (size_t)vbytes * (size_t)e[0]}};
+  };
+  hipStream_t s = reinterpret_cast<hipStream_t>(cbh_ctx_stream(context()));
+  if (use_mpi_transport()) {  // host-staged pairwise exchange
+    for (int d = 1; d < L; ++d) {
+      const int to = (me + d) % L, from = (me - d + L) % L;
+      const Arrs a = arrays(send[to]), b = arrays(recv[from]);
+      for (int k = 0; k < 4; ++k) {
+        std::vector<char> hs(a.b[k]), hr(b.b[k]);
+        if (a.b[k]) {
+          (void)hipMemcpyAsync(hs.data(), a.p[k], a.b[k], hipMemcpyDeviceToHost, s);
+          (void)hipStreamSynchronize(s);
+        }
+        MPI_Sendrecv(hs.data(), (int)a.b[k], MPI_BYTE, to, k, hr.data(), (int)b.b[k], MPI_BYTE, from, k, fiber,
+                     MPI_STATUS_IGNORE);
+        if (b.b[k]) {
+          (void)hipMemcpyAsync(b.p[k], hr.data(), b.b[k], hipMemcpyHostToDevice, s);
+          (void)hipStreamSynchronize(s);
+        }
+      }
+    }
+  } else {
+    ncclComm_t nc = rccl_comm_for(fiber);
+    rccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (int j = 0; j < L; ++j) {
+      if (j == me) continue;
+      const Arrs a = arrays(send[j]), b = arrays(recv[j]);
+      for (int k = 0; k < 4; ++k) {
+        if (a.b[k]) rccl_check(ncclSend(a.p[k], a.b[k], ncclUint8, j, nc, s), "ncclSend");
+        if (b.b[k]) rccl_check(ncclRecv(b.p[k], b.b[k], ncclUint8, j, nc, s), "ncclRecv");
+      }
+    }
+    rccl_check(ncclGroupEnd(), "ncclGroupEnd");
+  }
+  for (int j = 0; j < L; ++j)
+    if (j != me) cbh_mat_free(context(), send[j]);
+  std::vector<cbh_mat*> nonempty;
+  for (int j = 0; j < L; ++j) {
+    if (essentials(recv[j])[0] > 0) nonempty.push_back(recv[j]);
+    else cbh_mat_free(context(), recv[j]);
+  }
+  if (nonempty.empty()) {
+    cbh_mat* C = nullptr;
+    int rc = cbh_mat_create(context(), ress[4 * me + 1], div[me], 0, 0, (cbh_dtype)dtype, vbytes, &C);
+    if (rc != CBH_OK) die(context(), rc, "cbh_mat_create");
+    return C;
+  }
+  if (nonempty.size() == 1) return nonempty[0];
+  return merge_all(sr, nonempty);
+}
+
+// the product 3D grid of C (ParFriends.h:3200-3203 / 3700: a fresh CommGrid3D of A's shape)
+template <class IU, class NU1, class DER>
+std::shared_ptr<combblas::CommGrid3D> product_grid3d(combblas::SpParMat3D<IU, NU1, DER>& A) {
+  auto g = A.getcommgrid3D();
+  return std::shared_ptr<combblas::CommGrid3D>(new combblas::CommGrid3D(g->GetWorld(), g->GetGridLayers(),
+                                                                          g->GetGridRows(), g->GetGridCols(),
+                                                                          A.isSpecial()));
+}
+
+// SpParMat3D<.., SpDCCols> -> SpParMat3D<.., SpDCColsDev> on the same 3D grid, and back
+template <class IT, class NT>
+combblas::SpParMat3D<IT, NT, SpDCColsDev<IT, NT>> to_device(combblas::SpParMat3D<IT, NT, combblas::SpDCCols<IT, NT>>& A) {
+  return combblas::SpParMat3D<IT, NT, SpDCColsDev<IT, NT>>(new SpDCColsDev<IT, NT>(*A.seqptr()), A.getcommgrid3D(),
+                                                           A.isColSplit(), A.isSpecial());
+}
+template <class IT, class NT>
+combblas::SpParMat3D<IT, NT, combblas::SpDCCols<IT, NT>> to_host(combblas::SpParMat3D<IT, NT, SpDCColsDev<IT, NT>>& A) {
+  return combblas::SpParMat3D<IT, NT, combblas::SpDCCols<IT, NT>>(A.seqptr()->to_host(), A.getcommgrid3D(),
+                                                                  A.isColSplit(), A.isSpecial());
+}
+
+}  // namespace combblas_hip
+
+namespace combblas {
+
+template <typename IT, typename NT>
+void MCLPruneRecoverySelect(SpParMat<IT, NT, combblas_hip::SpDCColsDev<IT, NT>>& A, NT hardThreshold, IT selectNum,
+                            IT recoverNum, NT recoverPct, int kselectVersion) {
+  static_assert(std::is_same<NT, double>::value, "device MCLPruneRecoverySelect: double values");
+  (void)kselectVersion;  // Kselect1 semantics either way (radix select of the exact k-th value)
+  cbh_mat* C = combblas_hip::mcl_prune_block(A.seq().mat(), A.getcommgrid()->GetColWorld(), hardThreshold,
+                                             (int64_t)selectNum, (int64_t)recoverNum, recoverPct);
+  A.seq().reset(C);
+}
+
+// EstPerProcessNnzSUMMA (ParFriends.h:1243-1340): per stage the broadcast blocks' exact product
+// nnz (device symbolic pass), summed over the stages, max over the world
+template <typename IU, typename NU1, typename NU2>
+int64_t EstPerProcessNnzSUMMA(SpParMat<IU, NU1, combblas_hip::SpDCColsDev<IU, NU1>>& A,
+                              SpParMat<IU, NU2, combblas_hip::SpDCColsDev<IU, NU2>>& B, bool hashEstimate) {
+  (void)hashEstimate;
+  if (A.getncol() != B.getnrow()) MPI_Abort(MPI_COMM_WORLD, DIMMISMATCH);
+  int stages, dummy;
+  std::shared_ptr<CommGrid> GridC = ProductGrid(A.getcommgrid().get(), B.getcommgrid().get(), stages, dummy, dummy);
+  auto Asizes = combblas_hip::GetSetSizes(A.seq(), A.getcommgrid()->GetRowWorld());
+  auto Bsizes = combblas_hip::GetSetSizes(B.seq(), B.getcommgrid()->GetColWorld());
+  const int Aself = A.getcommgrid()->GetRankInProcRow(), Bself = B.getcommgrid()->GetRankInProcCol();
+  int64_t nnz = 0;
+  for (int i = 0; i < stages; ++i) {
+    combblas_hip::SpDCColsDev<IU, NU1> Arecv;
+    combblas_hip::SpDCColsDev<IU, NU2> Brecv;
+    auto& Ai = (i == Aself) ? A.seq() : Arecv;
+    auto& Bi = (i == Bself) ? B.seq() : Brecv;
+    combblas_hip::BCastMatrix(GridC->GetRowWorld(), Ai, Asizes[i], i);
+    combblas_hip::BCastMatrix(GridC->GetColWorld(), Bi, Bsizes[i], i);
+    int64_t flops = 0, z = 0;
+    if (Ai.getnnz() > 0 && Bi.getnnz() > 0) {
+      int rc = cbh_spgemm_symbolic(combblas_hip::context(), Ai.mat(), Bi.mat(), &flops, &z, nullptr, nullptr);
+      if (rc != CBH_OK) combblas_hip::die(combblas_hip::context(), rc, "cbh_spgemm_symbolic");
+    }
+    nnz += z;
+  }
+  int64_t mx = 0;
+  MPI_Allreduce(&nnz, &mx, 1, MPI_INT64_T, MPI_MAX, GridC->GetWorld());
+  return mx;
+}
+
+template <typename SR, typename NUO, typename UDERO, typename IU, typename NU1, typename NU2>
+SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDCColsDev<IU, NU1>>& A,
+                                            SpParMat<IU, NU2, combblas_hip::SpDCColsDev<IU, NU2>>& B, int phases,
+                                            NUO hardThreshold, IU selectNum, IU recoverNum, NUO recoverPct,
+                                            int kselectVersion, int computationKernel, int64_t perProcessMemory) {
+  static_assert(std::is_same<UDERO, combblas_hip::SpDCColsDev<IU, NUO>>::value,
+                "device-resident operands give a device-resident product");
+  (void)computationKernel;  // hash and heap contracts are both met by the device kernel
+  if (A.getncol() != B.getnrow()) {
+    SpParHelper::Print("Can not multiply, dimensions does not match\n");
+    MPI_Abort(MPI_COMM_WORLD, DIMMISMATCH);
+  }
+  if (phases < 1 || phases >= A.getncol()) phases = 1;
+  int stages, dummy;
+  std::shared_ptr<CommGrid> GridC = ProductGrid(A.getcommgrid().get(), B.getcommgrid().get(), stages, dummy, dummy);
+  if (perProcessMemory > 0) {  // the reference's memory model (ParFriends.h:480-520), exact nnz per stage
+    int p;
+    MPI_Comm_size(GridC->GetWorld(), &p);
+    const int64_t perNNZMem_in = sizeof(IU) * 2 + sizeof(NU1), perNNZMem_out = sizeof(IU) * 2 + sizeof(NUO);
+    int64_t lannz = A.getlocalnnz(), gannz = 0;
+    MPI_Allreduce(&lannz, &gannz, 1, MPI_INT64_T, MPI_MAX, GridC->GetWorld());
+    const int64_t inputMem = gannz * perNNZMem_in * 4;
+    const int64_t asquareNNZ = EstPerProcessNnzSUMMA(A, B, false);
+    const int64_t asquareMem = asquareNNZ * perNNZMem_out * 2;
+    const int64_t lcols = std::max<int64_t>(1, B.getlocalcols());
+    const int64_t d = (int64_t)std::ceil((asquareNNZ * std::sqrt((double)p)) / lcols);
+    const int64_t k = std::min(int64_t(std::max(selectNum, recoverNum)), d);
+    const int64_t kselectmem = lcols * k * 8 * 3;
+    const int64_t outputMem = (int64_t)((lcols * k) / std::sqrt((double)p)) * perNNZMem_in * 2;
+    const int64_t remainingMem = perProcessMemory * 1000000000 - inputMem - outputMem;
+    if (remainingMem > 0) phases = 1 + (int)((asquareMem + kselectmem) / remainingMem);
+  }
+  const IU C_m = A.seq().getnrow(), C_n = B.seq().getncol();
+  const auto cuts = combblas_hip::colsplit_cuts(C_n, phases);
+  std::vector<cbh_mat*> toconcatenate;
+  for (int p = 0; p < phases; ++p) {
+    combblas_hip::SpDCColsDev<IU, NU2> piece(combblas_hip::col_slice(B.seq().mat(), cuts[p], cuts[p + 1]));
+    std::shared_ptr<CommGrid> G;
+    cbh_mat* Cp = combblas_hip::summa_blocks<SR, NUO>(A.seq(), A.getcommgrid().get(), piece, B.getcommgrid().get(), G);
+    SpParMat<IU, NUO, UDERO> OnePieceOfC(new UDERO(Cp), GridC);
+    MCLPruneRecoverySelect(OnePieceOfC, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion);
+    toconcatenate.push_back(OnePieceOfC.seq().release());
+  }
+  (void)C_m;
+  return SpParMat<IU, NUO, UDERO>(new UDERO(combblas_hip::col_concat(toconcatenate)), GridC);
+}
+
+template <typename SR, typename NUO, typename UDERO, typename IU, typename NU1, typename NU2>
+SpParMat3D<IU, NUO, UDERO> Mult_AnXBn_SUMMA3D(SpParMat3D<IU, NU1, combblas_hip::SpDCColsDev<IU, NU1>>& A,
+                                              SpParMat3D<IU, NU2, combblas_hip::SpDCColsDev<IU, NU2>>& B) {
+  static_assert(std::is_same<UDERO, combblas_hip::SpDCColsDev<IU, NUO>>::value,
+                "device-resident operands give a device-resident product");
+  if (A.getncol() != B.getnrow()) {
+    SpParHelper::Print("Can not multiply, dimensions does not match\n");
+    MPI_Abort(MPI_COMM_WORLD, DIMMISMATCH);
+  }
+  std::vector<IU> div3;
+  B.CalculateColSplitDistributionOfLayer(div3);
+  std::shared_ptr<CommGrid> G;
+  cbh_mat* P = combblas_hip::summa_blocks<SR, NUO>(*A.GetLayerMat()->seqptr(), A.GetLayerMat()->getcommgrid().get(),
+                                                   *B.GetLayerMat()->seqptr(), B.GetLayerMat()->getcommgrid().get(), G);
+  std::vector<int64_t> div(div3.begin(), div3.end());
+  cbh_mat* C = combblas_hip::fiber_reduce_scatter(combblas_hip::semiring_traits<SR>::code, P, div,
+                                                  A.getcommgrid3D()->GetFiberWorld(), combblas_hip::dtype_of<NUO>::value,
+                                                  (int64_t)sizeof(NUO));
+  return SpParMat3D<IU, NUO, UDERO>(new UDERO(C), combblas_hip::product_grid3d(A), A.isColSplit(), A.isSpecial());
+}
+
+template <typename SR, typename NUO, typename UDERO, typename IU, typename NU1, typename NU2>
+SpParMat3D<IU, NUO, UDERO> MemEfficientSpGEMM3D(SpParMat3D<IU, NU1, combblas_hip::SpDCColsDev<IU, NU1>>& A,
+                                                SpParMat3D<IU, NU2, combblas_hip::SpDCColsDev<IU, NU2>>& B, int phases,
+                                                NUO hardThreshold, IU selectNum, IU recoverNum, NUO recoverPct,
+                                                int kselectVersion, int computationKernel, int64_t perProcessMemory) {
+  static_assert(std::is_same<UDERO, combblas_hip::SpDCColsDev<IU, NUO>>::value,
+                "device-resident operands give a device-resident product");
+  (void)computationKernel;
+  if (A.getncol() != B.getnrow()) {
+    SpParHelper::Print("Can not multiply, dimensions does not match\n");
+    MPI_Abort(MPI_COMM_WORLD, DIMMISMATCH);
+  }
+  if (phases < 1 || phases >= B.getncol()) phases = 1;
+  auto g3 = A.getcommgrid3D();
+  if (perProcessMemory > 0) {  // the reference's 3D memory model (ParFriends.h:3247-3290)
+    int p;
+    MPI_Comm_size(g3->GetLayerWorld(), &p);
+    const int64_t perNNZMem_in = sizeof(IU) * 2 + sizeof(NU1), perNNZMem_out = sizeof(IU) * 2 + sizeof(NUO);
+    int64_t lannz = A.GetLayerMat()->getlocalnnz(), gannz = 0;
+    MPI_Allreduce(&lannz, &gannz, 1, MPI_INT64_T, MPI_MAX, g3->GetWorld());
+    const int64_t ginputMem = gannz * perNNZMem_in * 5;
+    const int64_t asquareNNZ = EstPerProcessNnzSUMMA(*A.GetLayerMat(), *B.GetLayerMat(), true);
+    int64_t gasquareNNZ = 0;
+    MPI_Allreduce(&asquareNNZ, &gasquareNNZ, 1, MPI_INT64_T, MPI_MAX, g3->GetFiberWorld());
+    const int64_t gasquareMem = gasquareNNZ * perNNZMem_out * 2;
+    const int64_t lcols = std::max<int64_t>(1, B.GetLayerMat()->getlocalcols());
+    const int64_t d = (int64_t)std::ceil(((gasquareNNZ / g3->GetGridLayers()) * std::sqrt((double)p)) / lcols);
+    const int64_t k = std::min(int64_t(std::max(selectNum, recoverNum)), d);
+    const int64_t postMem = (int64_t)std::ceil(((lcols / g3->GetGridLayers()) * k) / std::sqrt((double)p)) *
+                            perNNZMem_out * 2;
+    const double remainingMem = perProcessMemory * 1000000000.0 - ginputMem - postMem;
+    const int64_t kselectMem = lcols * k * (int64_t)sizeof(NUO) * 3;
+    int calc = remainingMem > 0 ? (int)std::ceil((gasquareMem + kselectMem) / remainingMem) : -1, gcalc = 0;
+    MPI_Allreduce(&calc, &gcalc, 1, MPI_INT, MPI_MAX, g3->GetFiberWorld());
+    if (gcalc > phases) phases = gcalc;
+  }
+  std::vector<IU> div3;
+  B.CalculateColSplitDistributionOfLayer(div3);
+  const int L = g3->GetGridLayers(), me = g3->GetRankInFiber();
+  // B's layer block: `L` chunks of div3 columns, each cut in `phases` pieces (ColSplit)
+  std::vector<std::vector<int64_t>> piece(L);  // column offsets of chunk c's pieces in the layer block
+  int64_t c0 = 0;
+  for (int c = 0; c < L; ++c) {
+    auto cuts = combblas_hip::colsplit_cuts((int64_t)div3[c], phases);
+    for (auto& x : cuts) x += c0;
+    piece[c] = cuts;
+    c0 += div3[c];
+  }
+  cbh_mat* Bl = B.GetLayerMat()->seqptr()->mat();
+  std::vector<cbh_mat*> toconcatenate;
+  for (int p = 0; p < phases; ++p) {
+    std::vector<cbh_mat*> parts;
+    std::vector<int64_t> lb(L);
+    for (int c = 0; c < L; ++c) {
+      parts.push_back(combblas_hip::col_slice(Bl, piece[c][p], piece[c][p + 1]));
+      lb[c] = piece[c][p + 1] - piece[c][p];
+    }
+    combblas_hip::SpDCColsDev<IU, NU2> OnePieceOfB(combblas_hip::col_concat(parts));
+    SpParMat<IU, NU2, combblas_hip::SpDCColsDev<IU, NU2>> OnePieceOfBLayer(
+        new combblas_hip::SpDCColsDev<IU, NU2>(OnePieceOfB.release()), g3->GetLayerWorld());
+    std::shared_ptr<CommGrid> G;
+    cbh_mat* P = combblas_hip::summa_blocks<SR, NUO>(*A.GetLayerMat()->seqptr(), A.GetLayerMat()->getcommgrid().get(),
+                                                     OnePieceOfBLayer.seq(), OnePieceOfBLayer.getcommgrid().get(), G);
+    cbh_mat* Cp = combblas_hip::fiber_reduce_scatter(combblas_hip::semiring_traits<SR>::code, P, lb,
+                                                     g3->GetFiberWorld(), combblas_hip::dtype_of<NUO>::value,
+                                                     (int64_t)sizeof(NUO));
+    SpParMat<IU, NUO, UDERO> phaseResultantLayer(new UDERO(Cp), g3->GetLayerWorld());
+    MCLPruneRecoverySelect(phaseResultantLayer, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion);
+    toconcatenate.push_back(phaseResultantLayer.seq().release());
+  }
+  (void)me;
+  return SpParMat3D<IU, NUO, UDERO>(new UDERO(combblas_hip::col_concat(toconcatenate)),
+                                    combblas_hip::product_grid3d(A), A.isColSplit(), A.isSpecial());
+}
+
+}  // namespace combblas

@@ -257,6 +257,45 @@ inline cbh_mat* merge_all(cbh_semiring sr, std::vector<cbh_mat*> parts) {
   return parts[0];
 }
 
+// The SUMMA stage loop of Mult_AnXBn_Synch (ParFriends.h:1004-1108) over two device blocks on their
+// grids (the local blocks of A and B, or B's phase piece): sizes exchanged on the host
+// (GetSetSizes), stage blocks broadcast device to device on the product grid's row (A) and column
+// (B) communicators, multiplied on the device, the non-empty stage partials merged on the device.
+// Returns the product block (an m x n matrix even when empty); GridC = ProductGrid(GA, GB).
+template <class SR, class NUO, class IU, class NU1, class NU2>
+cbh_mat* summa_blocks(SpDCColsDev<IU, NU1>& Aloc, combblas::CommGrid* GA, SpDCColsDev<IU, NU2>& Bloc,
+                      combblas::CommGrid* GB, std::shared_ptr<combblas::CommGrid>& GridC) {
+  int stages, dummy;
+  GridC = ProductGrid(GA, GB, stages, dummy, dummy);  // found by ADL (a friend of CommGrid)
+  const IU C_m = Aloc.getnrow(), C_n = Bloc.getncol();
+  auto Asizes = GetSetSizes(Aloc, GA->GetRowWorld());
+  auto Bsizes = GetSetSizes(Bloc, GB->GetColWorld());
+  const int Aself = GA->GetRankInProcRow();
+  const int Bself = GB->GetRankInProcCol();
+  std::vector<cbh_mat*> tomerge;
+  for (int i = 0; i < stages; ++i) {
+    SpDCColsDev<IU, NU1> Arecv;
+    SpDCColsDev<IU, NU2> Brecv;
+    SpDCColsDev<IU, NU1>& Ai = (i == Aself) ? Aloc : Arecv;
+    SpDCColsDev<IU, NU2>& Bi = (i == Bself) ? Bloc : Brecv;
+    BCastMatrix(GridC->GetRowWorld(), Ai, Asizes[i], i);
+    BCastMatrix(GridC->GetColWorld(), Bi, Bsizes[i], i);
+    cbh_mat* Ci = local_multiply<SR, NUO, NU1, NU2>(Ai.mat(), Bi.mat());
+    int64_t nnz = 0;
+    cbh_mat_info(Ci, nullptr, nullptr, &nnz, nullptr, nullptr);
+    if (nnz > 0) tomerge.push_back(Ci);  // `if(!C_cont->isZero()) tomerge.push_back`
+    else cbh_mat_free(context(), Ci);
+  }  // received blocks are freed at the end of their stage (the reference's clearA/clearB = i != self)
+  if (tomerge.empty()) {
+    cbh_mat* C = nullptr;
+    int rc = cbh_mat_create(context(), C_m, C_n, 0, 0, dtype_of<NUO>::value, (int64_t)sizeof(NUO), &C);
+    if (rc != CBH_OK) die(context(), rc, "cbh_mat_create");
+    return C;
+  }
+  if (tomerge.size() == 1) return tomerge[0];  // one partial: it is the product (no copy round trip)
+  return merge_all(semiring_traits<SR>::code, tomerge);
+}
+
 // SpParMat<.., SpDCCols> <-> SpParMat<.., SpDCColsDev>: one upload / download of the local block
 template <class IT, class NT>
 combblas::SpParMat<IT, NT, SpDCColsDev<IT, NT>> to_device(combblas::SpParMat<IT, NT, combblas::SpDCCols<IT, NT>>& A) {
@@ -287,42 +326,11 @@ SpParMat<IU, NUO, UDERO> Mult_AnXBn_Synch(SpParMat<IU, NU1, combblas_hip::SpDCCo
                                           bool clearA = false, bool clearB = false) {
   static_assert(std::is_same<UDERO, combblas_hip::SpDCColsDev<IU, NUO>>::value,
                 "device-resident operands give a device-resident product");
-  typedef combblas_hip::SpDCColsDev<IU, NU1> DA;
-  typedef combblas_hip::SpDCColsDev<IU, NU2> DB;
   if (!CheckSpGEMMCompliance(A, B)) return SpParMat<IU, NUO, UDERO>();
-  int stages, dummy;
-  std::shared_ptr<CommGrid> GridC = ProductGrid(A.getcommgrid().get(), B.getcommgrid().get(), stages, dummy, dummy);
-  const IU C_m = A.seq().getnrow(), C_n = B.seq().getncol();
-  auto Asizes = combblas_hip::GetSetSizes(A.seq(), A.getcommgrid()->GetRowWorld());
-  auto Bsizes = combblas_hip::GetSetSizes(B.seq(), B.getcommgrid()->GetColWorld());
-  const int Aself = A.getcommgrid()->GetRankInProcRow();
-  const int Bself = B.getcommgrid()->GetRankInProcCol();
-  std::vector<cbh_mat*> tomerge;
-  for (int i = 0; i < stages; ++i) {
-    DA Arecv;
-    DB Brecv;
-    DA& Ai = (i == Aself) ? A.seq() : Arecv;
-    DB& Bi = (i == Bself) ? B.seq() : Brecv;
-    combblas_hip::BCastMatrix(GridC->GetRowWorld(), Ai, Asizes[i], i);
-    combblas_hip::BCastMatrix(GridC->GetColWorld(), Bi, Bsizes[i], i);
-    cbh_mat* Ci = combblas_hip::local_multiply<SR, NUO, NU1, NU2>(Ai.mat(), Bi.mat());
-    int64_t nnz = 0;
-    cbh_mat_info(Ci, nullptr, nullptr, &nnz, nullptr, nullptr);
-    if (nnz > 0) tomerge.push_back(Ci);  // `if(!C_cont->isZero()) tomerge.push_back`
-    else cbh_mat_free(combblas_hip::context(), Ci);
-  }  // received blocks are freed at the end of their stage (the reference's clearA/clearB = i != self)
-  if (clearA) A.seq() = DA();
-  if (clearB) B.seq() = DB();
-  cbh_mat* C = nullptr;
-  if (tomerge.empty()) {
-    int rc = cbh_mat_create(combblas_hip::context(), C_m, C_n, 0, 0, combblas_hip::dtype_of<NUO>::value,
-                            (int64_t)sizeof(NUO), &C);
-    if (rc != CBH_OK) combblas_hip::die(combblas_hip::context(), rc, "cbh_mat_create");
-  } else if (tomerge.size() == 1) {
-    C = tomerge[0];  // one partial: it is the product (no copy round trip)
-  } else {
-    C = combblas_hip::merge_all(combblas_hip::semiring_traits<SR>::code, tomerge);
-  }
+  std::shared_ptr<CommGrid> GridC;
+  cbh_mat* C = combblas_hip::summa_blocks<SR, NUO>(A.seq(), A.getcommgrid().get(), B.seq(), B.getcommgrid().get(), GridC);
+  if (clearA) A.seq() = combblas_hip::SpDCColsDev<IU, NU1>();
+  if (clearB) B.seq() = combblas_hip::SpDCColsDev<IU, NU2>();
   return SpParMat<IU, NUO, UDERO>(new UDERO(C), GridC);
 }
 
