@@ -17,7 +17,7 @@
 //
 //   symbolic (MODE_TSYM): distinct rows of the task -> cnt[task]        [estimateNNZ_Hash, mtSpGEMM.h:806-933]
 //            sub-tile = an LDS bitmap over 32*TA rows (exact, no hashing) or, for sparse ranges,
-//            an LDS key hash of <= T/2 products -- whichever needs fewer sub-tiles.
+//            an LDS key hash of <= TA/2 products -- whichever needs fewer sub-tiles.
 //   offsets : exclusive scan of cnt over tasks (a column's tasks are consecutive, in row order),
 //             so every task knows where its outputs go and C's column pointers fall out.
 //   numeric (MODE_TNUM): SR::add(SR::multiply(a,b)) into an order-preserving LDS hash (slot =
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
   const bool store = !NUM && a.bmp != nullptr && a.boff[task + 1] > a.boff[task];
   int64_t R = 1;
   if constexpr (!dense) {
-    constexpr int64_t cap = NUM ? (int64_t)T * kFill8 / 8 : T / 2;  // outputs (keys) per sub-tile
+    constexpr int64_t cap = NUM ? (int64_t)T * kFill8 / 8 : TA / 2;  // outputs (keys) per sub-tile
     R = (work + cap - 1) / cap;
     if constexpr (!NUM) {
       const int64_t Rb = (span + 32ll * TA - 1) / (32ll * TA);
@@ -810,7 +810,7 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
     if (!NUM && bitmap) {
       for (int s = tid; s < nwd; s += BS) words[s] = 0u;
     } else {
-      for (int s = tid; s < (NUM ? TA : T); s += BS) {
+      for (int s = tid; s < TA; s += BS) {
         keys[s] = kEmpty;
         if constexpr (NUM && !LOCKED) vals[s] = SR::identity();
       }
@@ -877,10 +877,11 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
             bad |= 1 << 8;
             return;
           }
-          constexpr int LG = __builtin_ctz(T);
-          uint32_t s = ((uint32_t)r[u] * 0x9E3779B1u) >> (32 - LG);
+          // key hash over all TA words (13312 for the large configuration: the bitmap's LDS), slot
+          // = multiplicative hash scaled to TA
+          uint32_t s = (uint32_t)(((uint64_t)((uint32_t)r[u] * 0x9E3779B1u) * (uint64_t)TA) >> 32);
           bool ok = false;
-          for (int probe = 0; probe < 2 * kPmax; ++probe, s = (s + 1) & (T - 1)) {
+          for (int probe = 0; probe < 2 * kPmax; ++probe, s = (s + 1 == (uint32_t)TA) ? 0u : s + 1) {
             const int32_t k = atomicCAS(&keys[s], kEmpty, r[u]);
             if (k == kEmpty) ++my_count;
             if (k == kEmpty || k == r[u]) {
