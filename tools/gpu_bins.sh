@@ -23,7 +23,7 @@ for PMC in "FETCH_SIZE TCC_HIT_sum" "WRITE_SIZE TCC_MISS_sum GRBM_GUI_ACTIVE" \
   timeout -s KILL 300 rocprofv3 --pmc $PMC --kernel-include-regex 'task_kernel.*true' --output-format csv -d "$OUT/bins/pmcm$i" -o run -- \
     python3 "$R/tools/merge_sample.py" "$SCALE" 0.0625 1 > "$OUT/bins/pmcm$i.log" 2>&1 || { tail -20 "$OUT/bins/pmcm$i.log"; exit 1; }
 done
-python3 "$R/tools/pmc_bins.py" "$OUT/bins" "$OUT/ks.log" "$R/profiles/r02/r02p_pmc_calib.json" "$OUT/pmc_bins.json"
+python3 "$R/tools/pmc_bins.py" "$OUT/bins" "$OUT/ks.log" "$R/profiles/pmc_calib.json" "$OUT/pmc_bins.json"
 if [ "${STAMPS:-0}" = 1 ]; then
   step stamps
   cd "$R" || exit 1
