@@ -114,6 +114,14 @@ SIGNATURES = {
     "cbh_kselect_value": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "cbh_prune_columns": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_mcl_prune_recovery_select": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double,
+                                                     ctypes.c_int64, ctypes.c_int64, ctypes.c_double,
+                                                     ctypes.c_void_p, ctypes.c_void_p,
+                                                     ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_mat_col_slice": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                         ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_mat_col_concat": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_tuples_to_dcsc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                           ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),

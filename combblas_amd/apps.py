@@ -112,6 +112,16 @@ def PruneColumn(A: SpDCCols, thresh) -> SpDCCols:
     return SpDCCols(A.ctx, h)
 
 
+def MCLPruneBlock(A: SpDCCols, hard, selectNum, recoverNum, recoverPct) -> SpDCCols:
+    """MCLPruneRecoverySelect (ParFriends.h:185-353) of a block holding its columns whole, in one
+    C-ABI call (cbh_mcl_prune_recovery_select): statistics, Kselect1 of the recovery / selection
+    columns, the recovery check after selection and PruneColumn on the device; A is kept"""
+    h = ctypes.c_void_p()
+    check(lib().cbh_mcl_prune_recovery_select(A.ctx.h, A.h, float(hard), int(selectNum), int(recoverNum),
+                                              float(recoverPct), None, None, ctypes.byref(h)), A.ctx.h)
+    return SpDCCols(A.ctx, h)
+
+
 def TCLower(ctx, scale: int, edgefactor: int = 16, seed=None) -> SpDCCols:
     """Applications/TC.cpp:98-104,139-150 on the device: the packed Graph500 R-MAT edges (bit-identical
     to DEL->GenGraph500Data), RemoveLoops, Symmetricize (A += A'), Apply(1) and

@@ -117,3 +117,7 @@ class HipBackend:
     def prune_columns(self, A: SpDCCols, thresh) -> SpDCCols:
         from .apps import PruneColumn
         return PruneColumn(A, thresh)
+
+    def mcl_prune_block(self, A: SpDCCols, hard, selectNum, recoverNum, recoverPct) -> SpDCCols:
+        from .apps import MCLPruneBlock
+        return MCLPruneBlock(A, hard, selectNum, recoverNum, recoverPct)

@@ -573,7 +573,12 @@ def _kept_stats(be, A, prune, colgroup):
 
 
 def _mcl_block(be, A, colgroup, hardThreshold, selectNum, recoverNum, recoverPct):
-    """ParFriends.h:185-353 on a local block whose columns may be split over `colgroup`"""
+    """ParFriends.h:185-353 on a local block whose columns may be split over `colgroup` (a block
+    holding its columns whole: one device call, cbh_mcl_prune_recovery_select)"""
+    if _whole_columns(colgroup) and hasattr(be, "mcl_prune_block"):
+        out = be.mcl_prune_block(A, hardThreshold, selectNum, recoverNum, recoverPct)
+        be.free(A)
+        return out
     cnt, cntp, sump = ColumnStats(be, A, hardThreshold, colgroup)  # unpruned nnz, pruned nnz, pruned sums
     prune = torch.full_like(cnt, hardThreshold)
     rec = (cntp < recoverNum) & (cnt > cntp) & (sump < recoverPct)

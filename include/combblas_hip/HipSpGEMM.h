@@ -106,7 +106,10 @@ cbh_mat* upload(const combblas::SpDCCols<IT, NT>& A) {
     cp.assign(d->cp, d->cp + d->nzc + 1);
     jc.assign(d->jc, d->jc + d->nzc);
     ir.resize(d->nz);
-    for (IT i = 0; i < d->nz; ++i) ir[i] = static_cast<int32_t>(d->ir[i]);
+    const IT nz = d->nz;
+    const IT* dir = d->ir;
+#pragma omp parallel for schedule(static)
+    for (IT i = 0; i < nz; ++i) ir[i] = static_cast<int32_t>(dir[i]);
     num.resize(sizeof(NT) * d->nz);
     std::memcpy(num.data(), d->numx, sizeof(NT) * d->nz);
   }
@@ -135,19 +138,24 @@ cbh_mat* upload(const combblas::SpTuples<IT, NT>& T, bool sort_rows = false) {
   std::vector<int64_t> cp(1, 0), jc;
   std::vector<int32_t> ir(h.nnz);
   std::unique_ptr<NT[]> num(new NT[h.nnz > 0 ? h.nnz : 1]);  // not std::vector: vector<bool> has no data()
+#pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < h.nnz; ++i) {
+    ir[i] = static_cast<int32_t>(T.rowindex(i));
+    num[i] = T.numvalue(i);
+  }
+  for (int64_t i = 0; i < h.nnz; ++i) {  // column heads (the tuples are column-sorted)
     const IT c = T.colindex(i);
     if (jc.empty() || jc.back() != c) {
       if (!jc.empty()) cp.push_back(i);
       jc.push_back(c);
     }
-    ir[i] = static_cast<int32_t>(T.rowindex(i));
-    num[i] = T.numvalue(i);
   }
   if (!jc.empty()) cp.push_back(h.nnz);
   h.nzc = (int64_t)jc.size();
+  const int64_t ncols_up = (int64_t)cp.size() - 1;
   if (sort_rows)
-    for (size_t c = 0; c + 1 < cp.size(); ++c) {
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int64_t c = 0; c < ncols_up; ++c) {
       const int64_t b = cp[c], e = cp[c + 1];
       bool sorted = true;
       for (int64_t i = b + 1; i < e && sorted; ++i) sorted = ir[i - 1] < ir[i];
@@ -184,6 +192,7 @@ combblas::SpTuples<IT, NT>* download_tuples(cbh_mat* C) {
   if (rc != CBH_OK) die(context(), rc, "cbh_mat_copy_out");
   if (nnz == 0) return new combblas::SpTuples<IT, NT>(0, (IT)m, (IT)n);
   auto* tuples = static_cast<std::tuple<IT, IT, NT>*>(::operator new(sizeof(std::tuple<IT, IT, NT>) * nnz));
+#pragma omp parallel for schedule(dynamic, 1024)
   for (int64_t c = 0; c < nzc; ++c)
     for (int64_t p = cp[c]; p < cp[c + 1]; ++p) tuples[p] = std::make_tuple((IT)ir[p], (IT)jc[c], num[p]);
   return new combblas::SpTuples<IT, NT>(nnz, (IT)m, (IT)n, tuples, true, true);
