@@ -788,10 +788,14 @@ __global__ __launch_bounds__(256) void bmp_count_kernel(const int64_t* __restric
 }
 
 // numeric tasks split between the dense (bitmap-rank) and the hash kernels: wd / wh = the task's
-// output count in the kernel it goes to, 0 in the other. Dense needs a stored bitmap (boff).
+// output count in the kernel it goes to, 0 in the other. Dense needs a stored bitmap (boff). The
+// compression ratio routes the short tasks: a task with few outputs but more than wavemax products
+// (cr above wavemax / outputs) goes to the mid workgroup kernel, whose 256 threads share its
+// products, instead of one wave (a 64-lane wave would walk them alone: a launch's tail task).
 __global__ void dense_split_kernel(const int64_t* __restrict__ tcnt, const int32_t* __restrict__ tlo,
-                                   const int32_t* __restrict__ thi, const int64_t* __restrict__ boff, int64_t n,
-                                   int64_t T, int64_t capd, int64_t nwb, int64_t dr4, int64_t smallcap, int enable,
+                                   const int32_t* __restrict__ thi, const int64_t* __restrict__ boff,
+                                   const int64_t* __restrict__ flops, int64_t n, int64_t T, int64_t capd, int64_t nwb,
+                                   int64_t dr4, int64_t smallcap, int64_t wavemax, int enable,
                                    int64_t* __restrict__ wd, int64_t* __restrict__ wh) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
@@ -799,7 +803,7 @@ __global__ void dense_split_kernel(const int64_t* __restrict__ tcnt, const int32
   const bool d = enable && boff != nullptr && boff[t + 1] > boff[t] && w > smallcap &&
                  dense_subtiles(w, (int64_t)thi[t] - tlo[t], T, capd, nwb, dr4) > 0;
   wd[t] = d ? w : 0;
-  wh[t] = d ? 0 : w;
+  wh[t] = d ? 0 : (w > 0 && w <= smallcap && flops && flops[t] > wavemax ? smallcap + 1 : w);
 }
 // CBH_DENSE=0 keeps every numeric task on the hash kernels (A/B switch)
 static bool kDenseEnabled() {
@@ -1148,7 +1152,8 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
   CBH_TRY(S.get(&wd, nt));
   CBH_TRY(S.get(&wh, nt));
   hipLaunchKernelGGL(dense_split_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.tcnt + t0, P.tlo + t0,
-                     P.thi + t0, P.bmp ? P.boff + t0 : nullptr, nt, (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, dratio4(), kSmallCap,
+                     P.thi + t0, P.bmp ? P.boff + t0 : nullptr, P.twork + t0, nt, (int64_t)TNumLarge::T, (int64_t)CD::CAPD,
+                     (int64_t)CD::NWB, dratio4(), kSmallCap, kWaveProducts,
                      kDenseEnabled() ? 1 : 0, wd, wh);
   CBH_HIP(ctx, hipGetLastError());
   BinLists bd, bl;
@@ -1172,30 +1177,33 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
   const double nb_s = eb * bl.units[0] + 16.0 * bl.small_count;
   const double nb_m = eb * bl.units[1] + 16.0 * bl.mid_count;
   if (diag_enabled()) {
-    {  // task-class totals of this numeric range (profiling aid)
-      std::vector<int64_t> hd(nt), hc(nt), hw(nt);
-      std::vector<int32_t> hlo(nt), hhi(nt), hcol(nt);
+    {  // per numeric bin: tasks, outputs, products (flop estimate), compression ratio, rows spanned
+      std::vector<int64_t> hd(nt), hh(nt), hc(nt), hw(nt);
+      std::vector<int32_t> hlo(nt), hhi(nt);
       CBH_HIP(ctx, hipMemcpyAsync(hd.data(), wd, nt * 8, hipMemcpyDeviceToHost, ctx->stream));
+      CBH_HIP(ctx, hipMemcpyAsync(hh.data(), wh, nt * 8, hipMemcpyDeviceToHost, ctx->stream));
       CBH_HIP(ctx, hipMemcpyAsync(hc.data(), P.tcnt + t0, nt * 8, hipMemcpyDeviceToHost, ctx->stream));
       CBH_HIP(ctx, hipMemcpyAsync(hw.data(), P.twork + t0, nt * 8, hipMemcpyDeviceToHost, ctx->stream));
       CBH_HIP(ctx, hipMemcpyAsync(hlo.data(), P.tlo + t0, nt * 4, hipMemcpyDeviceToHost, ctx->stream));
       CBH_HIP(ctx, hipMemcpyAsync(hhi.data(), P.thi + t0, nt * 4, hipMemcpyDeviceToHost, ctx->stream));
-      CBH_HIP(ctx, hipMemcpyAsync(hcol.data(), P.tcol + t0, nt * 4, hipMemcpyDeviceToHost, ctx->stream));
       CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
-      double s[2][5] = {{0}};  // tasks, span, outputs, flops, columns
-      int64_t lastc[2] = {-1, -1};
+      const char* names[4] = {"wave (<=256 out)", "mid (<=1024 out)", "hash large", "dense"};
+      double st[4][4] = {{0}};  // tasks, outputs, flops, span
       for (int64_t t = 0; t < nt; ++t) {
-        const int k = hd[t] > 0 ? 1 : 0;
-        if (hc[t] <= kSmallCap && !k) continue;
-        s[k][0] += 1;
-        s[k][1] += (double)(hhi[t] - hlo[t]);
-        s[k][2] += (double)hc[t];
-        s[k][3] += (double)hw[t];
-        if (hcol[t] != lastc[k]) s[k][4] += 1, lastc[k] = hcol[t];
+        int k;
+        if (hd[t] > 0) k = 3;
+        else if (hh[t] <= 0) continue;
+        else k = hh[t] <= kSmallCap ? 0 : (hh[t] <= kMidCap ? 1 : 2);
+        st[k][0] += 1;
+        st[k][1] += (double)hc[t];
+        st[k][2] += (double)hw[t];
+        st[k][3] += (double)(hhi[t] - hlo[t]);
       }
-      for (int k = 0; k < 2; ++k)
-        std::fprintf(stderr, "[cbh diag] %s tasks %.0f cols %.0f span %.4g (bitmap %.3f GB) outputs %.4g flops %.4g\n",
-                     k ? "dense" : "hash>256", s[k][0], s[k][4], s[k][1], s[k][1] / 8e9, s[k][2], s[k][3]);
+      for (int k = 0; k < 4; ++k)
+        if (st[k][0] > 0)
+          std::fprintf(stderr, "[cbh diag] bin %-17s tasks %.0f outputs %.4g flops %.4g cr %.2f out/task %.0f density %.3g%%\n",
+                       names[k], st[k][0], st[k][1], st[k][2], st[k][2] / std::max(1.0, st[k][1]),
+                       st[k][1] / st[k][0], 100.0 * st[k][1] / std::max(1.0, st[k][3]));
     }
     CBH_TRY((launch_task_diag<SR, TNumLarge, MODE_TDENSE>(ctx, a, bd, "numeric dense")));
     CBH_TRY((launch_task_diag<SR, TNumLarge, MODE_TNUM>(ctx, a, bl, "numeric hash")));
@@ -1863,8 +1871,8 @@ int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t
   CBH_TRY(p->S.get(&wd, nt));
   CBH_TRY(p->S.get(&wh, nt));
   hipLaunchKernelGGL(dense_split_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.tcnt, P.tlo, P.thi,
-                     P.bmp ? P.boff : nullptr, nt,
-                     (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, dratio4(), kSmallCap,
+                     P.bmp ? P.boff : nullptr, P.twork, nt,
+                     (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, dratio4(), kSmallCap, kWaveProducts,
                      (kDenseEnabled() && !(flags & CBH_PLAN_NO_DENSE)) ? 1 : 0, wd, wh);
   CBH_HIP(ctx, hipGetLastError());
   BinLists bd, bl;

@@ -52,6 +52,9 @@ struct TNumSmallFor {
 // twice that; four waves (four tasks) per workgroup
 struct WNumSmall { static constexpr int TW = 512, WPB = 4, U = 4; };
 constexpr int kSymWaveCap = 1024;
+// numeric tasks of <= kSmallCap outputs but more products than this (compression ratio above
+// kWaveProducts / outputs) go to the mid workgroup kernel instead (dense_split_kernel)
+constexpr int64_t kWaveProducts = 8192;
 struct WSymSmall { static constexpr int TW = 2 * kSymWaveCap, WPB = 4, U = 4; };
 // user value types: the wave table while a wave's LDS stays within ~16 KB
 template <class SR>

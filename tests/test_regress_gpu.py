@@ -124,3 +124,39 @@ def test_wave_clustered_rows(ctx, oracle, dtype):
     H.assert_dcsc_equal(got, exp, msg=f"wave clustered rows, {np.dtype(dtype).name}")
     for S in (C, dA, dB):
         S.free()
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.int64])
+def test_high_cr_short_columns_leave_the_wave_kernel(ctx, oracle, dtype):
+    """Columns with few outputs but many products (compression ratio 100: 64 output rows, 10,240
+    products) are routed by their ratio to the mid workgroup kernel (dense_split_kernel,
+    kWaveProducts); every other column of the product stays on the wave kernel. Checked against
+    the oracle."""
+    import combblas_amd as cb
+
+    rng = np.random.default_rng(3)
+    m, n = 4096, 400
+    rows, cols = [], []
+    for c in range(n):
+        r = np.sort(rng.choice(64, 64, replace=False)) * 61 if c < 160 else np.sort(rng.choice(m, 12, replace=False))
+        rows.append(r)
+        cols.append(np.full(r.size, c))
+    rows, cols = np.concatenate(rows), np.concatenate(cols)
+    cp = np.searchsorted(cols, np.arange(n + 1)).astype(np.int64)
+    av = rng.integers(1, 9, rows.size).astype(dtype) * (1 if dtype == np.int64 else 0.5)
+    A = H.Dcsc(m, n, np.arange(n, dtype=np.int64), cp, rows.astype(np.int32), av)
+    # B column 0: all 160 "cluster" columns of A (160 x 64 products onto 64 rows); the rest sparse
+    bcols = [np.arange(160)] + [np.sort(rng.choice(np.arange(160, n), 5, replace=False)) for _ in range(63)]
+    bcp = np.concatenate([[0], np.cumsum([b.size for b in bcols])]).astype(np.int64)
+    bv = rng.integers(1, 5, int(bcp[-1])).astype(dtype) * (1 if dtype == np.int64 else 0.25)
+    B = H.Dcsc(n, 64, np.arange(64, dtype=np.int64), bcp, np.concatenate(bcols).astype(np.int32), bv)
+    dA = cb.SpDCCols.from_host(ctx, cb.HostDcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num))
+    dB = cb.SpDCCols.from_host(ctx, cb.HostDcsc(B.m, B.n, B.jc, B.cp, B.ir, B.num))
+    C = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dA, dB)
+    h = C.to_host()
+    got = H.Dcsc(h.m, h.n, h.jc, h.cp, h.ir, h.num)
+    exp = oracle.spgemm(A, B, "plus_times", "hybrid")
+    assert exp.cp[1] - exp.cp[0] == 64  # 10,240 products onto 64 rows
+    H.assert_dcsc_equal(got, exp, msg=f"high-cr short column, {np.dtype(dtype).name}")
+    for S in (C, dA, dB):
+        S.free()
