@@ -641,7 +641,18 @@ static int64_t task_flops() {
 // Row blocks: C's rows are cut into blocks of RB rows (kRowBlocks blocks); interior task
 // boundaries of a split column sit on block boundaries, where the row-block table of A gives
 // every hub entry's position directly (hub_fill_kernel); short columns bisect.
-constexpr int64_t kRowBlocks = 128;
+constexpr int64_t kRowBlocks = 256;  // (128 / 192 / 384: 130.9 / 131.3 / 131.4 vs 132.2 GFLOP/s, aligned sub-tiles)
+// rows per block: a multiple of 32 from 32 rows up, so that block boundaries are stored-bitmap word boundaries
+// (CBH_ROW_BLOCKS overrides the block count, for measurements)
+static int32_t row_block(int64_t m) {
+  static int64_t nb = [] {
+    const char* e = std::getenv("CBH_ROW_BLOCKS");
+    const long long x = e ? std::atoll(e) : 0;
+    return x > 0 ? (int64_t)x : kRowBlocks;
+  }();
+  const int64_t rb = std::max<int64_t>(1, (m + nb - 1) / nb);
+  return (int32_t)(rb >= 32 ? (rb + 31) & ~int64_t(31) : rb);  // small matrices keep fine blocks
+}
 
 __global__ void task_count_kernel(const int64_t* __restrict__ flop, const int32_t* __restrict__ rmin,
                                   const int32_t* __restrict__ rmax, int64_t n, int64_t ft, int32_t RB,
@@ -679,7 +690,7 @@ __global__ __launch_bounds__(256) void task_fill_kernel(const int64_t* __restric
     const int64_t t = t0 + s;
     const int64_t c0 = nb * s / S, c1 = nb * (s + 1) / S;
     tcol[t] = (int32_t)c;
-    tlo[t] = s == 0 ? rmin[c] : (int32_t)((b0 + c0) * RB);
+    tlo[t] = s == 0 ? (rmin[c] & ~31) : (int32_t)((b0 + c0) * RB);  // word-aligned start (stored bitmaps)
     thi[t] = s == S - 1 ? rmax[c] + 1 : (int32_t)((b0 + c1) * RB);
     tfull[t] = (uint8_t)((s == 0 ? 1 : 0) | (s == S - 1 ? 2 : 0));
     twork[t] = f * c1 / nb - f * c0 / nb;
@@ -693,6 +704,14 @@ __global__ __launch_bounds__(256) void task_fill_kernel(const int64_t* __restric
 // (task_kernel.h stop_search) read it; short columns bisect instead. At scale 22: 288 K hub
 // columns (82 % of A's entries), 149 MB, instead of a table over all 4.2 M columns.
 constexpr int64_t kHubMin = 32;
+static int64_t hub_min() {  // CBH_HUB_MIN overrides, for measurements
+  static int64_t v = [] {
+    const char* e = std::getenv("CBH_HUB_MIN");
+    const long long x = e ? std::atoll(e) : 0;
+    return x > 0 ? (int64_t)x : kHubMin;
+  }();
+  return v;
+}
 __global__ void hub_flag_kernel(const int64_t* __restrict__ Acp, int64_t ncol, int64_t minlen, int64_t* __restrict__ flag) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k < ncol) flag[k] = (Acp[k + 1] - Acp[k]) >= minlen ? 1 : 0;
@@ -995,7 +1014,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
                      A->n, P.flop, P.rmin, P.rmax, ctx->d_err);
   CBH_HIP(ctx, hipGetLastError());
   CBH_TRY(sum_i64(ctx, S, P.flop, n, d_tot));
-  P.RB = (int32_t)std::max<int64_t>(1, (A->m + kRowBlocks - 1) / kRowBlocks);
+  P.RB = row_block(A->m);
   hipLaunchKernelGGL(task_count_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, P.flop, P.rmin, P.rmax, n,
                      task_flops(), P.RB, scnt);
   CBH_HIP(ctx, hipMemsetAsync(scnt + n, 0, sizeof(int64_t), ctx->stream));
@@ -1028,7 +1047,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
     CBH_TRY(S.get(&hflag, A->n + 1));
     CBH_TRY(S.get(&hpos, A->n + 1));
     CBH_TRY(S.get(&P.hidx, std::max<int64_t>(A->n, 1)));
-    hipLaunchKernelGGL(hub_flag_kernel, dim3(blocks_for(A->n, 256)), dim3(256), 0, ctx->stream, P.Adense, A->n, kHubMin,
+    hipLaunchKernelGGL(hub_flag_kernel, dim3(blocks_for(A->n, 256)), dim3(256), 0, ctx->stream, P.Adense, A->n, hub_min(),
                        hflag);
     CBH_HIP(ctx, hipMemsetAsync(hflag + A->n, 0, sizeof(int64_t), ctx->stream));
     CBH_TRY(exclusive_scan_i64(ctx, S, hflag, hpos, A->n + 1));

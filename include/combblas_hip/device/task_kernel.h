@@ -38,6 +38,11 @@ constexpr int32_t kNoRow = 0x7fffffff;
 // cursor row not loaded yet (< every row range: the entry counts as active, and its first
 // segment search starts AT the cursor, whose row the search loads with the following ones)
 constexpr int32_t kUnknownRow = -2;
+#ifdef CBH_NO_ALIGN
+constexpr bool kAlignSubtiles = false;
+#else
+constexpr bool kAlignSubtiles = true;
+#endif
 constexpr int kSymWords = 13312;  // bitmap words of the large symbolic configuration (see TaskCfg::TA)
 // numeric sub-tile: planned outputs, in eighths of the T home slots (3/8 and 5/8 measured slower:
 // 97.6 and 93.5 vs 98.6 GFLOP/s at scale 22)
@@ -153,11 +158,19 @@ __device__ __forceinline__ int64_t gallop64(const int32_t* __restrict__ rows, in
 // row-block table (blk: first position of each RB-row block, relative to the column start
 // `base`) bounds the stop to one block -- a few dozen rows of one or two cache lines -- instead
 // of a galloping search of ~2 log2(segment) dependent loads; short columns gallop. Also returns
-// the row at the stop (kNoRow past hi), the next sub-tile's cursor row.
+// the row at the stop (kNoRow past hi), the next sub-tile's cursor row. Sub-tiles and dense
+// windows end on row-block boundaries where they can (kAlignSubtiles), and there a hub's stop is
+// the table entry itself: one load instead of the preload, the table and a bisection.
 template <int W>
 __device__ __forceinline__ int64_t stop_search(const int32_t* __restrict__ rows, int64_t lo, int64_t hi, int32_t key,
                                                const int32_t* __restrict__ blk, int64_t base, int32_t RB,
                                                int32_t& row_at) {
+  if (blk != nullptr && key % RB == 0) {  // a row-block boundary (aligned sub-tiles): one table load
+    int64_t stop = base + blk[key / RB];
+    stop = stop < lo ? lo : (stop > hi ? hi : stop);
+    row_at = stop < hi ? rows[stop] : kNoRow;
+    return stop;
+  }
   int32_t v[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) v[w] = (lo + w < hi) ? rows[lo + w] : kNoRow;
@@ -176,13 +189,8 @@ __device__ __forceinline__ int64_t stop_search(const int32_t* __restrict__ rows,
   int64_t stop;
   if (blk != nullptr) {
     const int32_t b = key / RB;
-    const int64_t s0 = base + blk[b];
-    if (key % RB == 0) {
-      stop = s0 > lo ? s0 : lo;  // s0 is exactly the first row >= key (>= lo: rows[lo-1] < key)
-    } else {
-      const int64_t s1 = base + blk[b + 1];
-      stop = lb_rows64(rows, s0 > lo ? s0 : lo, s1 < hi ? s1 : hi, key);
-    }
+    const int64_t s0 = base + blk[b], s1 = base + blk[b + 1];
+    stop = lb_rows64(rows, s0 > lo ? s0 : lo, s1 < hi ? s1 : hi, key);
   } else {
     stop = gallop64(rows, lo, hi, key);
   }
@@ -474,6 +482,23 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
   }
   int64_t wnom = (span + R - 1) / R;
   if (store) wnom = (wnom + 31) & ~int64_t(31);  // <= 32*TA: R >= span / (32*TA)
+  // sub-tiles of a task cut in several end on row-block boundaries (hub stops are one table load)
+  // once they span a few blocks: the task's blocks are dealt into R runs of wblk whole blocks (R
+  // unchanged, except a bitmap sub-tile's row limit), so a sub-tile holds up to one block more than
+  // the nominal width. Stored bitmaps keep their word alignment (tlo and RB are multiples of 32).
+  const bool align = kAlignSubtiles && !dense && R >= 2 && a.RB > 0 && wnom >= 4ll * a.RB &&
+                     (!store || ((a.RB & 31) == 0 && (tlo & 31) == 0));
+  int64_t wblk = 0;  // blocks per aligned sub-tile
+  if (align) {
+    const int64_t nbt = ((int64_t)thi + a.RB - 1) / a.RB - tlo / a.RB;
+    int64_t Ra = R;
+    if (bitmap) {
+      const int64_t bmax = 32ll * TA / a.RB;  // >= 4: wnom <= 32*TA
+      Ra = (nbt + bmax - 1) / bmax;
+    }
+    wblk = (nbt + Ra - 1) / Ra;
+    wnom = wblk * a.RB;
+  }
 
   // violated bounds guards are recorded in a register and reported once at the end: a guard_fail
   // (global atomics with return values) inside a hot loop makes the compiler drain vmcnt there
@@ -692,6 +717,9 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
     constexpr int64_t TB = (int64_t)C::o_pos;
     int64_t wdes = TB * nwt / ((int64_t)sizeof(acc_t) * work + 6 * nwt);  // words whose outputs fill the rest
     wdes = wdes < 64 ? 64 : (wdes > C::NWB ? C::NWB : wdes);
+    // window ends snap to row-block boundaries when that keeps >= 3/4 of the window
+    const bool dalign = kAlignSubtiles && a.RB > 0 && (a.RB & 31) == 0 && (tlo & 31) == 0;
+    const int64_t dbw = dalign ? a.RB / 32 : 1;  // words per row block
     bool inited = !chunked;  // chunked: HBM entry state is written by the first processed window
     int64_t w0 = 0;
     while (w0 < nwt) {
@@ -727,7 +755,11 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
       }
       __syncthreads();
       CBH_STAMP(1);
-      const int cut = s_cut;
+      int cut = s_cut;
+      if (dalign && tlo + 32 * (w0 + cut) < thi) {  // snap the window end down to a row-block boundary
+        const int64_t cb = (w0 + cut) / dbw * dbw - w0;
+        if (cb > 0 && cb * 4 >= 3ll * cut) cut = (int)cb;
+      }
       const int dtotal = cut < wl ? (int)dp[cut] : wtotal;
       lo = (int32_t)(tlo + 32 * w0);
       const int64_t hcut = tlo + 32 * (w0 + cut);
@@ -802,7 +834,16 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
   }
   int64_t w = wnom;
   while (!dense && lo < thi) {
-    const int32_t hi = (int32_t)(((int64_t)lo + w < thi) ? lo + w : thi);
+    int64_t he = (int64_t)lo + w;
+    if (align) {
+      if (w == wnom) {
+        he = ((int64_t)lo / a.RB + wblk) * a.RB;
+      } else {  // a retried (halved) sub-tile: its end snaps down to a block boundary
+        const int64_t hb = he / a.RB * a.RB;
+        if (hb > lo) he = hb;
+      }
+    }
+    const int32_t hi = (int32_t)(he < thi ? he : thi);
     const bool hi_is_end = hi == thi;  // entry ends are clamped to the task (load_entries)
     const uint32_t tw = (uint32_t)(hi - lo);
     const uint64_t scale = ((uint64_t)T << 32) / (uint64_t)tw;  // numeric order-preserving slot map
