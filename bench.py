@@ -37,7 +37,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
 # the one with the most time per step
 KERNELS = {"num_large": "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 8, 1, false>",
            "num_dense": "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 8, 2, false>",
-           "sym_large": "cbh::task_kernel<cbh::PlusTimesD<long>, 8192, 512, 512, 8, 0, false>"}
+           "sym_large": "cbh::task_kernel<cbh::PlusTimesD<long>, 8192, 512, 512, 16, 0, false>"}
 # every task-kernel class of the f64 PlusTimes product (the application lines pick their dominant one)
 ALL_KERNELS = dict(KERNELS, **{
     "num_mid": "cbh::task_kernel<cbh::PlusTimesD<double>, 2048, 256, 256, 4, 1, false>",

@@ -16,7 +16,9 @@ namespace cbh {
 
 // task-kernel configurations: T slots, BS threads, EMAX entries per chunk, U products per thread
 struct TSymSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
-struct TSymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512, U = 8; };
+// 16 products per thread per window: half the owner-map windows of U = 8, for 12160 instead of
+// 13312 bitmap words so that two groups still share a CU (symbolic 201 -> 196 ms at scale 22)
+struct TSymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512, U = 16; };
 // mid-size symbolic tasks (kSmallCap < products <= kSymMidCap): one sub-tile in a 16 KB key
 // table, five workgroups per CU, so the per-task setup latency overlaps
 constexpr int kSymMid = 2048;  // (1024 / 4096 measured no better)

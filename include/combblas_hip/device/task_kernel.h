@@ -43,7 +43,7 @@ constexpr bool kAlignSubtiles = false;
 #else
 constexpr bool kAlignSubtiles = true;
 #endif
-constexpr int kSymWords = 13312;  // bitmap words of the large symbolic configuration (see TaskCfg::TA)
+constexpr int kSymWords = 12160;  // bitmap words of the large symbolic configuration (see TaskCfg::TA)
 // numeric sub-tile: planned outputs, in eighths of the T home slots (3/8 and 5/8 measured slower:
 // 97.6 and 93.5 vs 98.6 GFLOP/s at scale 22)
 constexpr int kFill8 = 4;
@@ -359,8 +359,8 @@ struct TaskCfg {
   using a_t = typename sr_a_type<SR>::type;  // A's values (NT1)
   using b_t = typename sr_b_type<SR>::type;  // B's values (NT2)
   // slots (symbolic: 32-bit words, a key hash over the first T or a bitmap over all TA). The large
-  // symbolic configuration fills two workgroups' share of LDS with bitmap words: 13312 words =
-  // 426 K rows per sub-tile instead of 262 K, so fewer sub-tiles re-scan a column's entries
+  // symbolic configuration fills two workgroups' share of LDS with bitmap words: 12160 words =
+  // 389 K rows per sub-tile instead of 262 K, so fewer sub-tiles re-scan a column's entries
   static constexpr int TA = NUM ? T + kGuard : (T >= 8192 && BS >= 512 ? kSymWords : T);
   static constexpr int NW = BS / 64;
   static constexpr int WIN = U * BS;
@@ -918,7 +918,7 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
             bad |= 1 << 8;
             return;
           }
-          // key hash over all TA words (13312 for the large configuration: the bitmap's LDS), slot
+          // key hash over all TA words (12160 for the large configuration: the bitmap's LDS), slot
           // = multiplicative hash scaled to TA
           uint32_t s = (uint32_t)(((uint64_t)((uint32_t)r[u] * 0x9E3779B1u) * (uint64_t)TA) >> 32);
           bool ok = false;
