@@ -699,10 +699,11 @@ __global__ __launch_bounds__(256) void task_fill_kernel(const int64_t* __restric
 }
 
 // Row-block table of the hub columns of A (>= kHubMin entries; wave per hub column):
-// out[h*(nblk+1) + x] = first position of A(:,k), relative to its start, whose row is >= x*RB,
-// for x = 0..nblk. Task boundaries (multiples of RB) and the stop search of long segments
-// (task_kernel.h stop_search) read it; short columns bisect instead. At scale 22: 288 K hub
-// columns (82 % of A's entries), 149 MB, instead of a table over all 4.2 M columns.
+// pair out[h*(nblk+1) + x] = (first position of A(:,k), relative to its start, whose row is
+// >= x*RB, the row there or kNoRow), for x = 0..nblk. Task and sub-tile boundaries (multiples of
+// RB) and the stop search of long segments (task_kernel.h stop_search) read it -- one 8-B load
+// gives a cursor and its row; short columns bisect instead. At scale 22: 288 K hub columns (82 %
+// of A's entries), 593 MB, instead of a table over all 4.2 M columns.
 constexpr int64_t kHubMin = 32;
 static int64_t hub_min() {  // CBH_HUB_MIN overrides, for measurements
   static int64_t v = [] {
@@ -730,14 +731,15 @@ __global__ __launch_bounds__(256) void hub_fill_kernel(const int64_t* __restrict
   const int32_t h = hidx[k];
   if (h < 0) return;
   const int64_t base = Acp[k], len = Acp[k + 1] - base;
-  int32_t* o = out + (int64_t)h * (nblk + 1);
+  int2* o = reinterpret_cast<int2*>(out) + (int64_t)h * (nblk + 1);
   for (int64_t p = lane; p < len; p += 64) {
-    const int64_t bc = Air[base + p] / RB;
+    const int32_t r = Air[base + p];
+    const int64_t bc = r / RB;
     const int64_t bp = p > 0 ? Air[base + p - 1] / RB : -1;
-    for (int64_t x = bp + 1; x <= bc; ++x) o[x] = (int32_t)p;
+    for (int64_t x = bp + 1; x <= bc; ++x) o[x] = make_int2((int32_t)p, r);
   }
   const int64_t blast = len > 0 ? Air[base + len - 1] / RB : -1;
-  for (int64_t x = blast + 1 + lane; x <= nblk; x += 64) o[x] = (int32_t)len;
+  for (int64_t x = blast + 1 + lane; x <= nblk; x += 64) o[x] = make_int2((int32_t)len, kNoRow);
 }
 
 // entries of every task that may run chunked (more than the smallest EMAX), else 0
@@ -1058,7 +1060,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
       P.nblk = (A->m + P.RB - 1) / P.RB;
       hipLaunchKernelGGL(hub_index_kernel, dim3(blocks_for(A->n, 256)), dim3(256), 0, ctx->stream, hflag, hpos, A->n,
                          P.hidx);
-      CBH_TRY(S.get(&P.htab, (size_t)nhub * (size_t)(P.nblk + 1)));
+      CBH_TRY(S.get(&P.htab, 2 * (size_t)nhub * (size_t)(P.nblk + 1)));  // (position, row) pairs
       hipLaunchKernelGGL(hub_fill_kernel, dim3(blocks_for(A->n, 4)), dim3(256), 0, ctx->stream, P.Adense, A->ir, P.hidx,
                          A->n, P.RB, P.nblk, P.htab);
       CBH_HIP(ctx, hipGetLastError());

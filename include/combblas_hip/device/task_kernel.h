@@ -84,9 +84,11 @@ struct TaskArgs {
   const void* Bnum;
   const int32_t* order;  // task ids in launch order
   int64_t norder;
-  // row-block table of the HUB columns of A (>= kHubMin entries): hidx[k] = hub id or -1,
-  // htab[h*(nblk+1) + b] = first position of A(:,k), relative to its start, whose row is
-  // >= b*RB (b = 0..nblk). Task boundaries sit on multiples of RB; RB = 0: no table.
+  // row-block table of the HUB columns of A (>= kHubMin entries): hidx[k] = hub id or -1; pair
+  // (htab[2e], htab[2e+1]), e = h*(nblk+1) + b, = first position of A(:,k), relative to its
+  // start, whose row is >= b*RB (b = 0..nblk), and the row there (kNoRow past the column): one
+  // 8-B load gives a cursor and its row. Task and sub-tile boundaries sit on multiples of RB;
+  // RB = 0: no table.
   const int32_t* hidx;
   const int32_t* htab;
   int64_t nblk;
@@ -163,12 +165,13 @@ __device__ __forceinline__ int64_t gallop64(const int32_t* __restrict__ rows, in
 // the table entry itself: one load instead of the preload, the table and a bisection.
 template <int W>
 __device__ __forceinline__ int64_t stop_search(const int32_t* __restrict__ rows, int64_t lo, int64_t hi, int32_t key,
-                                               const int32_t* __restrict__ blk, int64_t base, int32_t RB,
+                                               const int2* __restrict__ blk, int64_t base, int32_t RB,
                                                int32_t& row_at) {
   if (blk != nullptr && key % RB == 0) {  // a row-block boundary (aligned sub-tiles): one table load
-    int64_t stop = base + blk[key / RB];
-    stop = stop < lo ? lo : (stop > hi ? hi : stop);
-    row_at = stop < hi ? rows[stop] : kNoRow;
+    const int2 e = blk[key / RB];
+    const int64_t s0 = base + e.x;
+    const int64_t stop = s0 < lo ? lo : (s0 > hi ? hi : s0);
+    row_at = stop >= hi ? kNoRow : (stop == s0 ? e.y : rows[stop]);
     return stop;
   }
   int32_t v[W];
@@ -189,7 +192,7 @@ __device__ __forceinline__ int64_t stop_search(const int32_t* __restrict__ rows,
   int64_t stop;
   if (blk != nullptr) {
     const int32_t b = key / RB;
-    const int64_t s0 = base + blk[b], s1 = base + blk[b + 1];
+    const int64_t s0 = base + blk[b].x, s1 = base + blk[b + 1].x;
     stop = lb_rows64(rows, s0 > lo ? s0 : lo, s1 < hi ? s1 : hi, key);
   } else {
     stop = gallop64(rows, lo, hi, key);
@@ -503,10 +506,10 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
   // violated bounds guards are recorded in a register and reported once at the end: a guard_fail
   // (global atomics with return values) inside a hot loop makes the compiler drain vmcnt there
   int bad = 0;  // bit k: guard site k violated
-  auto hub_blk = [&](int32_t k) -> const int32_t* {
+  auto hub_blk = [&](int32_t k) -> const int2* {
     if (a.RB <= 0) return nullptr;
     const int32_t h = a.hidx[k];
-    return h >= 0 ? a.htab + (int64_t)h * (a.nblk + 1) : nullptr;
+    return h >= 0 ? reinterpret_cast<const int2*>(a.htab) + (int64_t)h * (a.nblk + 1) : nullptr;
   };
   // entry state of entries [first, first+cnt): cursor at the first row >= lo
   const int64_t go = chunked ? a.goff[task] : 0;
@@ -576,21 +579,27 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
       // the entry is clamped to the task's rows: its end is the first row >= thi. Interior task
       // boundaries sit on row-block boundaries, so a hub column finds both ends in its block
       // table (one load each); short columns bisect.
-      const int32_t* blk = base < end ? hub_blk(k) : nullptr;
+      const int2* blk = base < end ? hub_blk(k) : nullptr;
       int64_t cend = end;
       if (!(full & 2) && base < end) {
-        if (blk && thi % a.RB == 0) cend = base + blk[thi / a.RB];
+        if (blk && thi % a.RB == 0) cend = base + blk[thi / a.RB].x;
         else cend = lb_rows64(rowsA, base, end, thi);
       }
       int64_t pos = base;
+      int32_t known = kUnknownRow;  // the row at the cursor, when the block table gave it
       if (!lo_is_start && base < cend) {
-        if (blk && lo % a.RB == 0) pos = base + blk[lo / a.RB];
-        else pos = lb_rows64(rowsA, base, cend, lo);
+        if (blk && lo % a.RB == 0) {
+          const int2 e = blk[lo / a.RB];
+          pos = base + e.x;
+          known = e.y;
+        } else {
+          pos = lb_rows64(rowsA, base, cend, lo);
+        }
         if (pos > cend) pos = cend;
       }
       epos[i] = pos;
       eend[i] = cend;
-      const int32_t nx = pos < cend ? kUnknownRow : kNoRow;
+      const int32_t nx = pos < cend ? known : kNoRow;
       enext[i] = nx;
       if (chunked) {  // the first sub-tile's cursors are committed state too
         a.gend[go + first + i] = cend;
@@ -621,7 +630,7 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
           nx2 = kNoRow;
         } else {
           const int32_t k = ecol[i];
-          const int32_t* blk = MERGE ? nullptr : hub_blk(k);
+          const int2* blk = MERGE ? nullptr : hub_blk(k);
           stop = stop_search<8>(rowsA, nx == kUnknownRow ? p : p + 1, end, hi, blk, blk ? a.Acp[k] : 0, a.RB, nx2);
         }
       }
