@@ -699,8 +699,9 @@ __global__ __launch_bounds__(256) void task_fill_kernel(const int64_t* __restric
 }
 
 // Row-block table of the hub columns of A (>= kHubMin entries; wave per hub column):
-// pair out[h*(nblk+1) + x] = (first position of A(:,k), relative to its start, whose row is
-// >= x*RB, the row there or kNoRow), for x = 0..nblk. Task and sub-tile boundaries (multiples of
+// hub h owns pairs [h*(nblk+2), +nblk+2): pair 0 = the column's start (int64), pair 1 + x =
+// (first position of A(:,k), relative to its start, whose row is >= x*RB, the row there or
+// kNoRow), for x = 0..nblk. Task and sub-tile boundaries (multiples of
 // RB) and the stop search of long segments (task_kernel.h stop_search) read it -- one 8-B load
 // gives a cursor and its row; short columns bisect instead. At scale 22: 288 K hub columns (82 %
 // of A's entries), 593 MB, instead of a table over all 4.2 M columns.
@@ -731,7 +732,8 @@ __global__ __launch_bounds__(256) void hub_fill_kernel(const int64_t* __restrict
   const int32_t h = hidx[k];
   if (h < 0) return;
   const int64_t base = Acp[k], len = Acp[k + 1] - base;
-  int2* o = reinterpret_cast<int2*>(out) + (int64_t)h * (nblk + 1);
+  if (lane == 0) reinterpret_cast<int64_t*>(out)[(int64_t)h * (nblk + 2)] = base;  // pair 0: the column start
+  int2* o = reinterpret_cast<int2*>(out) + (int64_t)h * (nblk + 2) + 1;
   for (int64_t p = lane; p < len; p += 64) {
     const int32_t r = Air[base + p];
     const int64_t bc = r / RB;
@@ -957,6 +959,7 @@ struct Plan {  // device arrays describing C = A*B (B's nonzero column slots, ta
   int32_t* trk = nullptr;     // per task: row block of its middle row (launch order key)
   int32_t* gnx0 = nullptr;    // row at each committed cursor (double-buffered like gcur)
   int32_t* gnx1 = nullptr;
+  int32_t* ghub = nullptr;    // hub id of each chunked entry's A column
   int64_t* boff = nullptr;    // ntasks + 1: stored-bitmap word offsets (see bmp_count_kernel)
   uint32_t* bmp = nullptr;    // null: no stored bitmaps (dense kernel off)
   int64_t total_flops = 0, total_nnz = 0;
@@ -991,6 +994,7 @@ static TaskArgs task_args(const cbh_mat* A, const cbh_mat* B, const Plan& P, cbh
   a.gend = P.gend;
   a.gnx0 = P.gnx0;
   a.gnx1 = P.gnx1;
+  a.ghub = P.ghub;
   a.boff = P.bmp ? P.boff : nullptr;
   a.bmp = P.bmp;
   return a;
@@ -1060,7 +1064,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
       P.nblk = (A->m + P.RB - 1) / P.RB;
       hipLaunchKernelGGL(hub_index_kernel, dim3(blocks_for(A->n, 256)), dim3(256), 0, ctx->stream, hflag, hpos, A->n,
                          P.hidx);
-      CBH_TRY(S.get(&P.htab, 2 * (size_t)nhub * (size_t)(P.nblk + 1)));  // (position, row) pairs
+      CBH_TRY(S.get(&P.htab, 2 * (size_t)nhub * (size_t)(P.nblk + 2)));  // start + (position, row) pairs
       hipLaunchKernelGGL(hub_fill_kernel, dim3(blocks_for(A->n, 4)), dim3(256), 0, ctx->stream, P.Adense, A->ir, P.hidx,
                          A->n, P.RB, P.nblk, P.htab);
       CBH_HIP(ctx, hipGetLastError());
@@ -1084,6 +1088,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
       CBH_TRY(S.get(&P.gend, (size_t)gtot));
       CBH_TRY(S.get(&P.gnx0, (size_t)gtot));
       CBH_TRY(S.get(&P.gnx1, (size_t)gtot));
+      CBH_TRY(S.get(&P.ghub, (size_t)gtot));
     } else {
       P.goff = nullptr;
     }
@@ -1924,6 +1929,7 @@ int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t
   out->gend = P.gend;
   out->gnx0 = P.gnx0;
   out->gnx1 = P.gnx1;
+  out->ghub = P.ghub;
   out->boff = P.bmp ? P.boff : nullptr;
   out->bmp = P.bmp;
   out->err = ctx->d_err;

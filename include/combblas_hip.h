@@ -206,7 +206,7 @@ typedef struct cbh_plan cbh_plan;
 typedef struct cbh_numeric_plan {
   const int64_t* Acp; const int32_t* Air; const void* Anum;  /* A: dense column pointers, rows, values */
   const int64_t* Bcp; const int32_t* Bir; const void* Bnum;  /* B: DCSC pointers, rows, values         */
-  const int32_t* hidx; const int32_t* htab; int64_t nblk; int32_t RB; /* hub row-block table: (position, row) pairs */
+  const int32_t* hidx; const int32_t* htab; int64_t nblk; int32_t RB; /* hub row-block table: start + (position, row) pairs */
   const int32_t* tcol; const int32_t* tlo; const int32_t* thi; const uint8_t* tfull; /* tasks    */
   const int64_t* tcnt; const int64_t* toff;                  /* outputs per task, output offsets  */
   const int64_t* goff; int64_t* gcur0; int64_t* gcur1; int64_t* gend; /* chunked-task cursors    */
@@ -218,6 +218,7 @@ typedef struct cbh_numeric_plan {
   void* stream;                                              /* hipStream_t of the context        */
   int64_t mid_first, mid_count;                              /* mid-size hash tasks (<= 1024 out) */
   const int64_t* boff; uint32_t* bmp;                        /* stored row bitmaps of dense tasks */
+  int32_t* ghub;                                             /* hub id of each chunked-task entry */
 } cbh_numeric_plan;
 /* bin every task for the hash kernels: the dense (bitmap-rank) kernel needs a lock-free SR::add
  * and 8-byte accumulators, the layout the plan's dense split is computed for (numeric.h

@@ -135,6 +135,7 @@ inline TaskArgs numeric_args(const cbh_numeric_plan& p, int64_t cbase, int32_t* 
   a.gend = p.gend;
   a.gnx0 = p.gnx0;
   a.gnx1 = p.gnx1;
+  a.ghub = p.ghub;
   a.boff = p.boff;
   a.bmp = p.bmp;
   return a;

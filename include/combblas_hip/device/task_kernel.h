@@ -84,11 +84,11 @@ struct TaskArgs {
   const void* Bnum;
   const int32_t* order;  // task ids in launch order
   int64_t norder;
-  // row-block table of the HUB columns of A (>= kHubMin entries): hidx[k] = hub id or -1; pair
-  // (htab[2e], htab[2e+1]), e = h*(nblk+1) + b, = first position of A(:,k), relative to its
-  // start, whose row is >= b*RB (b = 0..nblk), and the row there (kNoRow past the column): one
-  // 8-B load gives a cursor and its row. Task and sub-tile boundaries sit on multiples of RB;
-  // RB = 0: no table.
+  // row-block table of the HUB columns of A (>= kHubMin entries): hidx[k] = hub id or -1. Hub h
+  // owns nblk + 2 int32 pairs from pair h*(nblk+2): pair 0 is the column's start (int64), pair
+  // 1 + b = (first position of A(:,k), relative to its start, whose row is >= b*RB, the row there
+  // or kNoRow), b = 0..nblk: one 8-B load gives a cursor and its row, and the start loads beside
+  // it. Task and sub-tile boundaries sit on multiples of RB; RB = 0: no table.
   const int32_t* hidx;
   const int32_t* htab;
   int64_t nblk;
@@ -118,6 +118,7 @@ struct TaskArgs {
   // only when it is active
   int32_t* gnx0;
   int32_t* gnx1;
+  int32_t* ghub;  // hub id of each chunked entry's A column (-1: none), written at its first visit
   // stored row bitmaps of the dense candidates (bmp_count_kernel): task t owns words
   // [boff[t], boff[t+1]) of bmp, bit x of word w = row tlo[t] + 32 w + x. The large symbolic kernel
   // writes them while it counts; the dense numeric kernel reads them instead of a marking pass.
@@ -425,7 +426,7 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
   b_t* escale = reinterpret_cast<b_t*>(smem + C::o_scale);        // B value
   int32_t* enext = reinterpret_cast<int32_t*>(smem + C::o_next);  // row at the cursor (kNoRow: done)
   int32_t* enext2 = reinterpret_cast<int32_t*>(smem + C::o_next2);  // row at the sub-tile's stop
-  int32_t* ecol = reinterpret_cast<int32_t*>(smem + C::o_col);    // A column id
+  int32_t* ecol = reinterpret_cast<int32_t*>(smem + C::o_col);    // hub id of the A column (-1: none)
   int32_t* eoff = reinterpret_cast<int32_t*>(smem + C::o_off);
   typename C::own_t* own = reinterpret_cast<typename C::own_t*>(smem + C::o_own);
   int32_t* red = reinterpret_cast<int32_t*>(smem + C::o_red);
@@ -506,10 +507,13 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
   // violated bounds guards are recorded in a register and reported once at the end: a guard_fail
   // (global atomics with return values) inside a hot loop makes the compiler drain vmcnt there
   int bad = 0;  // bit k: guard site k violated
-  auto hub_blk = [&](int32_t k) -> const int2* {
-    if (a.RB <= 0) return nullptr;
-    const int32_t h = a.hidx[k];
-    return h >= 0 ? reinterpret_cast<const int2*>(a.htab) + (int64_t)h * (a.nblk + 1) : nullptr;
+  // hub h's block pairs and its column start (TaskArgs::htab); entries keep h in ecol, so a
+  // sub-tile's stop search loads the pair and the start side by side
+  auto hub_tab = [&](int32_t h) -> const int2* {
+    return reinterpret_cast<const int2*>(a.htab) + (int64_t)h * (a.nblk + 2) + 1;
+  };
+  auto hub_base = [&](int32_t h) -> int64_t {
+    return reinterpret_cast<const int64_t*>(a.htab)[(int64_t)h * (a.nblk + 2)];
   };
   // entry state of entries [first, first+cnt): cursor at the first row >= lo
   const int64_t go = chunked ? a.goff[task] : 0;
@@ -519,7 +523,7 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
       for (int i = tid; i < cnt; i += BS) {
         const int64_t rdelta = (int64_t)(a.lir[i] - a.lir[0]);
         s_vdelta[i] = (int64_t)(reinterpret_cast<const val_t*>(a.lnum[i]) - valsA) - rdelta;
-        ecol[i] = i;
+        ecol[i] = -1;
         const int64_t base = a.mstart[(int64_t)c * a.nl + i] + rdelta;
         const int64_t end = base + a.mlen[(int64_t)c * a.nl + i];
         int64_t cend = end;
@@ -535,23 +539,14 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
     for (int i = tid; i < cnt; i += BS) {
       const int64_t p = e0 + first + i;
       if (from_state) {  // later sub-tile of a chunked task: committed cursor and its row from HBM
+        // (the column was validated at the entry's first visit: an invalid one is idle for good)
         const int64_t g = go + first + i;
         const int32_t nx = (par ? a.gnx1 : a.gnx0)[g];
+        const int32_t h = a.ghub[g];
         epos[i] = (par ? a.gcur1 : a.gcur0)[g];
         enext[i] = nx;
-        if (nx >= hi) {  // idle in this sub-tile: segments() reads only the cursor and its row
-          ecol[i] = 0;
-          continue;
-        }
-        const int32_t k = a.Bir[p];
-        if (k < 0 || k >= a.ncolA) {
-          bad |= 1 << 1;
-          ecol[i] = 0;
-          eend[i] = epos[i];
-          enext[i] = kNoRow;
-          continue;
-        }
-        ecol[i] = k;
+        ecol[i] = h;
+        if (nx >= hi) continue;  // idle in this sub-tile: segments() reads only the cursor and its row
         eend[i] = a.gend[g];
         if constexpr (NUM) escale[i] = reinterpret_cast<const b_t*>(a.Bnum)[p];
         continue;
@@ -560,17 +555,17 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
       if constexpr (NUM) escale[i] = reinterpret_cast<const b_t*>(a.Bnum)[p];
       if (k < 0 || k >= a.ncolA) {
         bad |= 1 << 1;
-        ecol[i] = 0;
+        ecol[i] = -1;
         epos[i] = eend[i] = 0;
         enext[i] = kNoRow;
         if (chunked) {
           a.gend[go + first + i] = 0;
           (par ? a.gcur1 : a.gcur0)[go + first + i] = 0;
           (par ? a.gnx1 : a.gnx0)[go + first + i] = kNoRow;
+          a.ghub[go + first + i] = -1;
         }
         continue;
       }
-      ecol[i] = k;
       int64_t base = a.Acp[k], end = a.Acp[k + 1];
       if (base < 0 || end < base || end > a.nnzA) {
         bad |= 1 << 2;
@@ -579,7 +574,9 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
       // the entry is clamped to the task's rows: its end is the first row >= thi. Interior task
       // boundaries sit on row-block boundaries, so a hub column finds both ends in its block
       // table (one load each); short columns bisect.
-      const int2* blk = base < end ? hub_blk(k) : nullptr;
+      const int32_t h = (base < end && a.RB > 0) ? a.hidx[k] : -1;
+      ecol[i] = h;
+      const int2* blk = h >= 0 ? hub_tab(h) : nullptr;
       int64_t cend = end;
       if (!(full & 2) && base < end) {
         if (blk && thi % a.RB == 0) cend = base + blk[thi / a.RB].x;
@@ -605,6 +602,7 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
         a.gend[go + first + i] = cend;
         (par ? a.gcur1 : a.gcur0)[go + first + i] = pos;
         (par ? a.gnx1 : a.gnx0)[go + first + i] = nx;
+        a.ghub[go + first + i] = h;
       }
     }
   };
@@ -629,9 +627,9 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
           stop = end;
           nx2 = kNoRow;
         } else {
-          const int32_t k = ecol[i];
-          const int2* blk = MERGE ? nullptr : hub_blk(k);
-          stop = stop_search<8>(rowsA, nx == kUnknownRow ? p : p + 1, end, hi, blk, blk ? a.Acp[k] : 0, a.RB, nx2);
+          const int32_t h = MERGE ? -1 : ecol[i];
+          const int2* blk = h >= 0 ? hub_tab(h) : nullptr;
+          stop = stop_search<8>(rowsA, nx == kUnknownRow ? p : p + 1, end, hi, blk, h >= 0 ? hub_base(h) : 0, a.RB, nx2);
         }
       }
       eoff[i] = (int32_t)(stop - p);
