@@ -728,6 +728,9 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
     const bool dalign = kAlignSubtiles && a.RB > 0 && (a.RB & 31) == 0 && (tlo & 31) == 0;
     const int64_t dbw = dalign ? a.RB / 32 : 1;  // words per row block
     bool inited = !chunked;  // chunked: HBM entry state is written by the first processed window
+    constexpr int KW = (C::NWB + BS - 1) / BS;  // window words per thread
+    uint32_t pre[KW];
+    int64_t pre_w0 = -1;
     int64_t w0 = 0;
     while (w0 < nwt) {
       const int wl = (int)((nwt - w0) < wdes ? (nwt - w0) : wdes);
@@ -736,7 +739,13 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
       int16_t* dp = reinterpret_cast<int16_t*>(smem + dbase + 4 * wl);
       const int capv = dbase / (int)sizeof(acc_t);
       const int kw = (wl + BS - 1) / BS;
-      for (int x = tid; x < wl; x += BS) dw[x] = tb[w0 + x];
+      if (pre_w0 == w0) {  // words gathered while the previous window was cut (same thread mapping)
+#pragma unroll
+        for (int j = 0; j < KW; ++j)
+          if (tid + j * BS < wl) dw[tid + j * BS] = pre[j];
+      } else {
+        for (int x = tid; x < wl; x += BS) dw[x] = tb[w0 + x];
+      }
       if (tid == 0) {
         s_cut = wl;
         __hip_atomic_store(&s_ovf, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // sweep() reads it
@@ -768,6 +777,15 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
         if (cb > 0 && cb * 4 >= 3ll * cut) cut = (int)cb;
       }
       const int dtotal = cut < wl ? (int)dp[cut] : wtotal;
+      {  // the next window's words: their loads overlap this window's entry loads
+        const int64_t w0n = w0 + cut;
+        if (w0n < nwt) {
+          const int wln = (int)((nwt - w0n) < wdes ? (nwt - w0n) : wdes);
+#pragma unroll
+          for (int j = 0; j < KW; ++j) pre[j] = (tid + j * BS < wln) ? tb[w0n + tid + j * BS] : 0u;
+          pre_w0 = w0n;
+        }
+      }
       lo = (int32_t)(tlo + 32 * w0);
       const int64_t hcut = tlo + 32 * (w0 + cut);
       const int32_t hi = (int32_t)(hcut < thi ? hcut : thi);
@@ -803,7 +821,7 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
               gn[go + (int64_t)ch * EMAX + i] = epos[i] + eoff[i + 1];
               gx[go + (int64_t)ch * EMAX + i] = enext2[i];
             }
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the stores land before the next barrier
+            // no store wait: the thread that wrote an entry's cursor is the one that reloads it
           }
           sweep(nec, P, true, place);  // ends with a barrier: the entry state may be reloaded
         }
@@ -951,7 +969,7 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
           gn[go + (int64_t)ch * EMAX + i] = epos[i] + eoff[i + 1];
           gx[go + (int64_t)ch * EMAX + i] = enext2[i];
         }
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the stores land before the barrier
+        // (no store wait: the thread that wrote an entry's cursor is the one that reloads it)
         __syncthreads();  // entry state is reloaded by the next chunk
       }
     }
