@@ -788,7 +788,7 @@ __device__ __forceinline__ int bmp_class(int64_t w, int64_t span) {
 __global__ __launch_bounds__(256) void bmp_count_kernel(const int64_t* __restrict__ twork, const int32_t* __restrict__ tlo,
                                                         const int32_t* __restrict__ thi, int64_t n, int64_t T,
                                                         int64_t capd, int64_t nwb, int64_t minwork, int64_t dr4,
-                                                        int min_class, int64_t* __restrict__ words,
+                                                        int64_t cr4, int min_class, int64_t* __restrict__ words,
                                                         unsigned long long* __restrict__ class_words) {
   __shared__ unsigned long long h[kBmpClasses];
   for (int i = threadIdx.x; i < kBmpClasses; i += blockDim.x) h[i] = 0;
@@ -796,7 +796,8 @@ __global__ __launch_bounds__(256) void bmp_count_kernel(const int64_t* __restric
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < n) {
     const int64_t w = twork[t], span = (int64_t)thi[t] - tlo[t];
-    int64_t nw = (w > minwork && span > 0 && dense_subtiles(w, span, T, capd, nwb, dr4) > 0) ? (span + 31) / 32 : 0;
+    const int64_t we = w * 4 / cr4;  // outputs expected of the flops at compression ratio cr4 / 4
+    int64_t nw = (w > minwork && span > 0 && dense_subtiles(we, span, T, capd, nwb, dr4) > 0) ? (span + 31) / 32 : 0;
     if (nw > 0) {
       const int b = bmp_class(w, span);
       if (b < min_class) nw = 0;
@@ -849,6 +850,16 @@ static int64_t dratio4() {
   static int64_t v = [] {
     const char* e = std::getenv("CBH_DRATIO4");
     return e ? (int64_t)std::atoi(e) : (int64_t)kDRatio4;
+  }();
+  return v;
+}
+// compression ratio (quarters) a candidate's flops are divided by before the dense test
+// (CBH_BMP_CR4, for measurements)
+static int64_t bmp_cr4() {
+  static int64_t v = [] {
+    const char* e = std::getenv("CBH_BMP_CR4");
+    const int x = e ? std::atoi(e) : 0;
+    return x > 0 ? (int64_t)x : (int64_t)4;
   }();
   return v;
 }
@@ -1102,8 +1113,8 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
     CBH_TRY(S.get(&P.boff, nt + 1));
     CBH_HIP(ctx, hipMemsetAsync(cw, 0, sizeof(unsigned long long) * kBmpClasses, ctx->stream));
     hipLaunchKernelGGL(bmp_count_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.twork, P.tlo, P.thi,
-                       P.ntasks, (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSymMidCap, dratio4(), 0,
-                       bw, cw);
+                       P.ntasks, (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSymMidCap, dratio4(),
+                       bmp_cr4(), 0, bw, cw);
     CBH_HIP(ctx, hipGetLastError());
     unsigned long long hc[kBmpClasses];
     CBH_HIP(ctx, hipMemcpyAsync(hc, cw, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream));
@@ -1119,7 +1130,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
     if (min_class > 0 && words > 0)  // drop the classes that did not fit
       hipLaunchKernelGGL(bmp_count_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.twork, P.tlo, P.thi,
                          P.ntasks, (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSymMidCap, dratio4(),
-                         min_class, bw, nullptr);
+                         bmp_cr4(), min_class, bw, nullptr);
     CBH_HIP(ctx, hipMemsetAsync(bw + P.ntasks, 0, sizeof(int64_t), ctx->stream));
     CBH_TRY(exclusive_scan_i64(ctx, S, bw, P.boff, P.ntasks + 1));
     if (words > 0 && kDenseEnabled()) CBH_TRY(S.get(&P.bmp, (size_t)words));
