@@ -181,8 +181,11 @@ def _stage_product_operands(be, A, B, grid, stages, Ab, Bb, vdtype):
     ONE local product over the inner dimension of all stages: the kernels accumulate every k, so
     no partial is materialised and no MultiwayMerge pass runs; C is the same matrix (integer and
     boolean semirings bit for bit; floating-point sums in another order). The received stage
-    blocks are released once copied."""
+    blocks are released once copied. One stage: the operands ARE A's and B's local blocks
+    (_release_operands leaves those alone)."""
     m, n = be.dims(A.seq)[0], be.dims(B.seq)[1]
+    if stages == 1:  # the rank's own blocks, used in place (no copy, no column sort of B)
+        return Ab[0], Bb[0]
     Acat = _hcat(be, Ab, m, vdtype)
     Bcat = _vcat(be, Bb, n, vdtype)
     Aself, Bself = grid.GetRankInProcRow(), grid.GetRankInProcCol()
@@ -192,6 +195,13 @@ def _stage_product_operands(be, A, B, grid, stages, Ab, Bb, vdtype):
         if i != Bself and Bb[i] is not Bcat:
             be.free(Bb[i])
     return Acat, Bcat
+
+
+def _release_operands(be, A, B, Acat, Bcat):
+    if Acat is not A.seq:
+        be.free(Acat)
+    if Bcat is not B.seq and Bcat is not Acat:
+        be.free(Bcat)
 
 
 def _check_dims(A, B):
@@ -391,8 +401,7 @@ def MemEfficientSpGEMM(SR, A: SpParMat, B: SpParMat, phases=0, hardThreshold=Non
             out.append(C)
     for p in plans:
         p.close()
-    be.free(Acat)
-    be.free(Bcat)
+    _release_operands(be, A, B, Acat, Bcat)
     if on_phase is not None:
         return len(cuts)
     return SpParMat(_concat_cols(be, out, m, n, vdtype), grid, be, A.m, B.n, A.row_off, B.col_off)
@@ -471,8 +480,7 @@ def Mult_AnXBn_SUMMA3D(SR, A: SpParMat3D, B: SpParMat3D, phases=1, perProcessMem
             out.append(C)
     for p in plans:
         p.close()
-    be.free(Acat)
-    be.free(Bcat)
+    _release_operands(be, A, B, Acat, Bcat)
     if on_phase is not None:
         return len(cuts)
     w = div[g3.rankInFiber]

@@ -22,14 +22,17 @@ struct TSymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512, U = 16; 
 // mid-size symbolic tasks (kSmallCap < products <= kSymMidCap): one sub-tile in a 16 KB key
 // table, five workgroups per CU, so the per-task setup latency overlaps
 constexpr int kSymMid = 2048;  // (1024 / 4096 measured no better)
-struct TSymMid { static constexpr int T = 2 * kSymMid, BS = 256, EMAX = 256, U = 4; };
+#ifndef CBH_MID_U
+#define CBH_MID_U 4
+#endif
+struct TSymMid { static constexpr int T = 2 * kSymMid, BS = 256, EMAX = 256, U = CBH_MID_U; };
 struct TNumSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 // (T = 8192 with 1024-thread groups, one per CU: 89.1 vs 98.2 GFLOP/s at scale 22)
 struct TNumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512, U = 8; };
 // mid-size hash tasks (kSmallCap < outputs <= kMidCap) of the library's A^2 path: a quarter of the
 // large kernel's LDS, so four workgroups share a CU and the per-task setup latency overlaps
 constexpr int kMidOut = 1024;  // (512 / 2048 measured no better)
-struct TNumMid { static constexpr int T = 2 * kMidOut, BS = 256, EMAX = 256, U = 4; };
+struct TNumMid { static constexpr int T = 2 * kMidOut, BS = 256, EMAX = 256, U = CBH_MID_U; };
 // wider accumulators (user value types) keep the large table within ~50 KB of LDS
 template <class SR>
 struct TNumLargeFor {
@@ -41,7 +44,7 @@ template <class SR>
 struct TNumMidFor {
   static constexpr int bytes = (int)(sizeof(int32_t) + sizeof(typename SR::acc_t));
   static constexpr int T = bytes <= 12 ? 2 * kMidOut : (bytes <= 24 ? kMidOut : 512);
-  static constexpr int BS = 256, EMAX = 256, U = 4;
+  static constexpr int BS = 256, EMAX = 256, U = CBH_MID_U;
 };
 template <class SR>
 struct TNumSmallFor {
