@@ -11,6 +11,16 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$R" || exit 1
 step() { echo "== $(date +%T) $*"; }
+# PART=2 runs only the application lines (C5, C3, C4), so the two halves fit one call each
+if [ "${PART:-1}" = 2 ]; then
+  for app in mcl galerkin tc; do
+    step "bench_$app"
+    timeout -k 10 700 python -u bench_$app.py > "$OUT/bench_$app.json" 2> "$OUT/bench_$app.err" || { tail -20 "$OUT/bench_$app.err"; exit 1; }
+    cat "$OUT/bench_$app.json"
+  done
+  step done
+  exit 0
+fi
 step "pytest -m gpu"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 \
   || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
@@ -34,6 +44,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
   || { tail -20 "$OUT/prof.err"; exit 1; }
 head -6 "$OUT/prof/run_kernel_stats.csv" | cut -c1-160
 cd "$R" || exit 1
+[ -n "$NOAPPS" ] && { step done; exit 0; }
 step "C5 line"
 timeout -k 10 600 python -u bench_mcl.py > "$OUT/bench_mcl.json" 2> "$OUT/bench_mcl.err" || { tail -20 "$OUT/bench_mcl.err"; exit 1; }
 cat "$OUT/bench_mcl.json"
