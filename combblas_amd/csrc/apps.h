@@ -679,7 +679,7 @@ constexpr int kSelStage = 4096;
 __global__ __launch_bounds__(256) void kselect_cols_kernel(const int64_t* __restrict__ jc, const int64_t* __restrict__ cp,
                                                            const double* __restrict__ num, int64_t nzc,
                                                            const int32_t* __restrict__ aidx, int64_t k,
-                                                           int64_t nmin, double* __restrict__ out) {
+                                                           double* __restrict__ out) {
   __shared__ uint64_t keys[kSelStage];
   __shared__ uint32_t h[256];
   __shared__ uint64_t s_pre;
@@ -688,7 +688,7 @@ __global__ __launch_bounds__(256) void kselect_cols_kernel(const int64_t* __rest
   for (int64_t s = blockIdx.x; s < nzc; s += gridDim.x) {
     const int32_t ai = aidx[jc[s]];
     const int64_t p0 = cp[s], n = cp[s + 1] - p0;
-    if (ai < 0 || n <= nmin) continue;  // uniform over the workgroup (n <= nmin: the wave kernel's)
+    if (ai < 0 || n <= 0) continue;  // uniform over the workgroup
     const bool staged = n <= kSelStage;
     if (staged)
       for (int64_t i = tid; i < n; i += 256) keys[i] = fkey(num[p0 + i]);
@@ -739,71 +739,6 @@ __global__ __launch_bounds__(256) void kselect_cols_kernel(const int64_t* __rest
     }
     if (tid == 0) out[ai] = fval(pre);
     __syncthreads();
-  }
-}
-
-// Kselect1 of the active columns of at most kWaveSel entries, one column per wavefront: the 8
-// radix passes re-read the column (cache-resident after the first), histogram by LDS atomics in
-// the wave's own 256 bins, and the same wave finds the digit (shuffle prefix + ballot) -- no
-// workgroup barriers (wave_lds_sync, wave_kernel.h), four columns per workgroup at a time. Longer
-// columns: kselect_cols_kernel.
-constexpr int64_t kWaveSel = 8192;
-__global__ __launch_bounds__(256) void kselect_cols_wave_kernel(const int64_t* __restrict__ jc,
-                                                                const int64_t* __restrict__ cp,
-                                                                const double* __restrict__ num, int64_t nzc,
-                                                                const int32_t* __restrict__ aidx, int64_t k,
-                                                                double* __restrict__ out) {
-  __shared__ uint32_t hs[4][256];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t* h = hs[wid];
-  for (int64_t s = (int64_t)blockIdx.x * 4 + wid; s < nzc; s += (int64_t)gridDim.x * 4) {
-    const int32_t ai = aidx[jc[s]];
-    const int64_t p0 = cp[s], n = cp[s + 1] - p0;
-    if (ai < 0 || n <= 0 || n > kWaveSel) continue;  // uniform over the wave
-    const double* __restrict__ col = num + p0;
-    int64_t r = (n >= k ? k : n) - 1;
-    uint64_t pre = 0;
-    for (int shift = 56; shift >= 0; shift -= 8) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) h[lane + 64 * j] = 0u;
-      wave_lds_sync();
-      const uint64_t himask = shift >= 56 ? 0ull : (~0ull << (shift + 8));
-      for (int64_t i = lane; i < n; i += 64) {
-        const uint64_t key = fkey(col[i]);
-        if ((key & himask) == pre) atomicAdd(&h[(key >> shift) & 255u], 1u);
-      }
-      wave_lds_sync();
-      uint32_t c[4], sum = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        c[j] = h[255 - 4 * lane - j];
-        sum += c[j];
-      }
-      uint32_t incl = sum;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o);
-        if (lane >= o) incl += t;
-      }
-      const uint64_t m = __ballot((int64_t)incl > r);
-      const int L = m ? __ffsll((long long)m) - 1 : 63;
-      int64_t rr = r - (int64_t)(incl - sum);
-      int d = 255 - 4 * lane;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (rr < (int64_t)c[j]) {
-          d = 255 - 4 * lane - j;
-          break;
-        }
-        rr -= c[j];
-      }
-      d = __shfl(d, L);
-      const int32_t rlo = __shfl((int32_t)(rr & 0xffffffff), L), rhi = __shfl((int32_t)(rr >> 32), L);
-      r = (int64_t)(((uint64_t)(uint32_t)rhi << 32) | (uint32_t)rlo);
-      pre |= (uint64_t)d << shift;
-      wave_lds_sync();  // every lane has read the bins before the next pass clears them
-    }
-    if (lane == 0) out[ai] = fval(pre);
   }
 }
 

@@ -2585,17 +2585,8 @@ int cbh_kselect_cols(cbh_ctx* ctx, const cbh_mat* A, const int32_t* active_index
   if (!active_index || !out) return fail(ctx, CBH_E_ARG, "null argument");
   if (A->nzc > 0) {
     const int64_t grid = A->nzc < 8192 ? A->nzc : 8192;  // workgroups stride over the slots
-#ifndef CBH_WAVESEL  // (the wave-per-column kernel is opt-in until measured on the device)
-    const int64_t nmin = 0;
-#else
-    const int64_t nmin = kWaveSel;  // columns up to kWaveSel entries: one per wavefront
-    const int64_t wgrid = std::min<int64_t>((A->nzc + 3) / 4, 16384);
-    hipLaunchKernelGGL(kselect_cols_wave_kernel, dim3((unsigned)wgrid), dim3(256), 0, ctx->stream, A->jc, A->cp,
-                       reinterpret_cast<const double*>(A->num), A->nzc, active_index, k, out);
-    CBH_HIP(ctx, hipGetLastError());
-#endif
     hipLaunchKernelGGL(kselect_cols_kernel, dim3((unsigned)grid), dim3(256), 0, ctx->stream, A->jc, A->cp,
-                       reinterpret_cast<const double*>(A->num), A->nzc, active_index, k, nmin, out);
+                       reinterpret_cast<const double*>(A->num), A->nzc, active_index, k, out);
     CBH_HIP(ctx, hipGetLastError());
   }
   return CBH_OK;
