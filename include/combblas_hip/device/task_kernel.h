@@ -46,7 +46,14 @@ constexpr bool kAlignSubtiles = true;
 constexpr int kSymWords = 12160;  // bitmap words of the large symbolic configuration (see TaskCfg::TA)
 // numeric sub-tile: planned outputs, in eighths of the T home slots (3/8 and 5/8 measured slower:
 // 97.6 and 93.5 vs 98.6 GFLOP/s at scale 22)
-constexpr int kFill8 = 4;
+#ifndef CBH_FILL8
+#define CBH_FILL8 4
+#endif
+#ifndef CBH_SYMFILL8
+#define CBH_SYMFILL8 4
+#endif
+constexpr int kFill8 = CBH_FILL8;
+constexpr int kSymFill8 = CBH_SYMFILL8;  // symbolic key-hash sub-tiles: keys, in eighths of TA
 // dense numeric sub-tile capacity in quarters of T: 3 = 3072 values for T = 4096 (2 and 4
 // measured slower: 98.7 / 104.5 vs 105.3 GFLOP/s at scale 22)
 constexpr int kCapD4 = 3;
@@ -472,7 +479,7 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
   const bool store = !NUM && a.bmp != nullptr && a.boff[task + 1] > a.boff[task];
   int64_t R = 1;
   if constexpr (!dense) {
-    constexpr int64_t cap = NUM ? (int64_t)T * kFill8 / 8 : TA / 2;  // outputs (keys) per sub-tile
+    constexpr int64_t cap = NUM ? (int64_t)T * kFill8 / 8 : (int64_t)TA * kSymFill8 / 8;  // outputs (keys) per sub-tile
     R = (work + cap - 1) / cap;
     if constexpr (!NUM) {
       const int64_t Rb = (span + 32ll * TA - 1) / (32ll * TA);
