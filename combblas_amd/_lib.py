@@ -44,6 +44,10 @@ K_NAMES = ["sym_large", "sym_small", "num_large", "num_small", "merge_sym", "mer
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
 FREE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p)
 # per-phase consumer of cbh_spgemm_phased: (user, phase, slot0, slot1, const cbh_mat* view) -> status
+FILL_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                           ctypes.c_void_p)
+TAKE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                           ctypes.c_void_p)
 PHASE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                             ctypes.c_void_p)
 
@@ -56,6 +60,7 @@ SIGNATURES = {
     "cbh_ctx_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
     "cbh_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "cbh_ctx_trim": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbh_ctx_take_retries": (ctypes.c_int, [ctypes.c_void_p, c_int64_p]),
     "cbh_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "cbh_ctx_set_allocator": (ctypes.c_int, [ctypes.c_void_p, ALLOC_FN, FREE_FN, ctypes.c_void_p]),
     "cbh_ctx_set_phase_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
@@ -80,6 +85,12 @@ SIGNATURES = {
     "cbh_mat_wrap_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cbh_dcsc), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_mat_info": (ctypes.c_int, [ctypes.c_void_p, c_int64_p, c_int64_p, c_int64_p, c_int64_p, ctypes.POINTER(ctypes.c_int)]),
     "cbh_mat_device_arrays": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_void_p)] * 4),
+    "cbh_mat_upload_chunks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                             ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                             ctypes.c_int64, ctypes.c_int64, FILL_FN, ctypes.c_void_p,
+                                             ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_mat_download_chunks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_int64, TAKE_FN, ctypes.c_void_p]),
     "cbh_mat_copy_out": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "cbh_mat_free": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
@@ -166,6 +177,8 @@ def lib():
                               "(there is no CPU fallback)")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("CBH_LIB") and not hasattr(L, name):
+                continue  # a diagnostic variant built from an older tree: entry points it lacks stay unbound
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

@@ -40,7 +40,7 @@ struct cbh_ctx {
   bool timing = false;
   cbh_kernel_times times{-1, -1, -1, 0};
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  int* d_err = nullptr;  // 4 ints of device-side error flags
+  int* d_err = nullptr;  // 32 ints: [0..15] device-side error flags (check_err), [16] sub-tile retries
   void* ws = nullptr;  // persistent phase workspace (hipMalloc'd once, grow-only): a ~150 GB
   int64_t ws_bytes = 0;  // buffer must not be re-mapped on every product
   cbh_alloc_fn alloc = nullptr;
@@ -57,9 +57,11 @@ struct cbh_ctx {
   std::multimap<size_t, void*> cache;
   std::unordered_map<void*, size_t> live;
   size_t cached_bytes = 0;
-  // CBH_CACHE_CAP_GB; above it the cache is released. Default: the device's memory -- a product
-  // near HBM capacity (scale-22 A^2: 108 GB of stored bitmaps + the phase workspace) otherwise
-  // re-maps its scratch every call (4-5 s per call measured); OOM still releases the cache
+  // CBH_CACHE_CAP_GB; above it the cache is released. Default: half the device's memory -- a
+  // product near HBM capacity (scale-22 A^2: 108 GB of stored bitmaps) otherwise re-maps its
+  // scratch every call (4-5 s per call measured with a 64 GB cap), while the other half stays
+  // for allocators outside the context (RCCL communicators, the caller); OOM and cbh_ctx_trim
+  // still release the cache
   size_t cache_cap = size_t(128) << 30;
   bool poison = false;  // CBH_ALLOC_POISON=1: freed blocks are filled with 0xFF and never reused
   std::vector<void*> quarantine;
@@ -71,6 +73,11 @@ struct cbh_ctx {
   double k_bytes[CBH_K_NKINDS] = {0};
   cbh_phase_fn phase_fn = nullptr;  // per-phase consumer of cbh_spgemm_phased
   void* phase_user = nullptr;
+  // pinned staging of the chunked host transfers (cbh_mat_upload_chunks / _download_chunks):
+  // two halves of pin_bytes / 2, grow-only, with one event per half
+  void* pin = nullptr;
+  size_t pin_bytes = 0;
+  hipEvent_t pin_ev[2] = {nullptr, nullptr};
 };
 
 struct cbh_mat {
@@ -200,6 +207,15 @@ struct Scratch {
     int rc = dalloc(ctx, p, count);
     if (rc == CBH_OK) ptrs.push_back(*p);
     return rc;
+  }
+  // frees one allocation of this holder before the call ends (no-op for foreign pointers)
+  void drop(void* p) {
+    for (auto it = ptrs.begin(); it != ptrs.end(); ++it)
+      if (*it == p) {
+        dfree(ctx, p);
+        ptrs.erase(it);
+        return;
+      }
   }
   ~Scratch() {
     for (void* p : ptrs) dfree(ctx, p);
@@ -1011,7 +1027,9 @@ static TaskArgs task_args(const cbh_mat* A, const cbh_mat* B, const Plan& P, cbh
   return a;
 }
 
-static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat* B, Plan& P) {
+// count_only: the caller needs the counts alone (cbh_spgemm_symbolic, EstPerProcessNnzSUMMA), so no
+// dense-candidate bitmaps are sized, stored or kept
+static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat* B, Plan& P, bool count_only = false) {
   P.nzcB = B->nzc;
   const int64_t n = P.nzcB;
   CBH_TRY(S.get(&P.Adense, A->n + 1));
@@ -1104,7 +1122,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
       P.goff = nullptr;
     }
   }
-  {  // stored row bitmaps of the dense candidates, within CBH_BMP_FRAC (default 0.4) of the HBM
+  if (!count_only) {  // stored row bitmaps of the dense candidates, within CBH_BMP_FRAC (default 0.4) of the HBM
     using CD = TaskCfg<PlusTimesD<double>, TNumLarge::T, TNumLarge::BS, TNumLarge::EMAX, TNumLarge::U, MODE_TDENSE>;
     int64_t* bw;
     unsigned long long* cw;
@@ -1243,10 +1261,10 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
                        st[k][1] / st[k][0], 100.0 * st[k][1] / std::max(1.0, st[k][3]));
     }
     CBH_TRY((launch_task_diag<SR, TNumLarge, MODE_TDENSE>(ctx, a, bd, "numeric dense")));
-    CBH_TRY((launch_task_diag<SR, TNumLarge, MODE_TNUM>(ctx, a, bl, "numeric hash")));
+    CBH_TRY((launch_task_diag<SR, TNumHash, MODE_TNUM>(ctx, a, bl, "numeric hash")));
   } else {
     CBH_TRY((launch_task<SR, TNumLarge, MODE_TDENSE>(ctx, a, bd.large_first, bd.large_count, CBH_K_NUM_DENSE, nb_d)));
-    CBH_TRY((launch_task<SR, TNumLarge, MODE_TNUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
+    CBH_TRY((launch_task<SR, TNumHash, MODE_TNUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
   }
   CBH_TRY((launch_task<SR, TNumMid, MODE_TNUM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_NUM_MID, nb_m)));
   if (bl.small_count > 0)  // one task per wave (wave_kernel.h)
@@ -1308,6 +1326,25 @@ static int new_mat(cbh_ctx* ctx, int64_t m, int64_t n, int64_t nnz, int64_t nzc,
   return CBH_OK;
 }
 
+// C's allocation once the symbolic pass knows nnz(C). The dense candidates' stored bitmaps were
+// sized before nnz(C) was known (up to CBH_BMP_FRAC of the device): when C does not fit beside
+// them, they are dropped -- every task then runs on the hash kernels -- and C is allocated again.
+static int new_result(cbh_ctx* ctx, Scratch& S, Plan& P, int64_t m, int64_t n, int64_t nnz, int64_t nzc, int dtype,
+                      cbh_mat** out, int64_t vbytes = 0) {
+  int rc = new_mat(ctx, m, n, nnz, nzc, dtype, out, vbytes);
+  if (rc == CBH_OK && P.bmp != nullptr && std::getenv("CBH_TEST_RESULT_OOM")) {  // test hook: the fallback below
+    cbh_mat_free(ctx, *out);
+    *out = nullptr;
+    rc = fail(ctx, CBH_E_OOM, "CBH_TEST_RESULT_OOM");
+  }
+  if (rc != CBH_E_OOM || P.bmp == nullptr) return rc;
+  S.drop(P.bmp);
+  P.bmp = nullptr;
+  release_cache(ctx);
+  if (diag_enabled()) std::fprintf(stderr, "[cbh diag] C does not fit beside the stored bitmaps: dense windows off\n");
+  return new_mat(ctx, m, n, nnz, nzc, dtype, out, vbytes);
+}
+
 static int empty_result(cbh_ctx* ctx, int64_t m, int64_t n, int dtype, cbh_mat** C) {
   CBH_TRY(new_mat(ctx, m, n, 0, 0, dtype, C));
   CBH_HIP(ctx, hipMemsetAsync((*C)->cp, 0, sizeof(int64_t), ctx->stream));
@@ -1352,7 +1389,7 @@ int cbh_ctx_create(int device, cbh_ctx** out) {
   if (const char* v = std::getenv("CBH_ALLOC_POISON")) c->poison = std::atoi(v) != 0;
   {
     size_t freeb = 0, totb = 0;
-    if (hipMemGetInfo(&freeb, &totb) == hipSuccess && totb > 0) c->cache_cap = totb;
+    if (hipMemGetInfo(&freeb, &totb) == hipSuccess && totb > 0) c->cache_cap = totb / 2;
   }
   if (const char* v = std::getenv("CBH_CACHE_CAP_GB")) c->cache_cap = size_t(std::atof(v) * double(size_t(1) << 30));
   for (auto& e : c->ev)
@@ -1360,7 +1397,7 @@ int cbh_ctx_create(int device, cbh_ctx** out) {
       delete c;
       return CBH_E_HIP;
     }
-  if (hipMalloc(&c->d_err, 16 * sizeof(int)) != hipSuccess || hipMemset(c->d_err, 0, 16 * sizeof(int)) != hipSuccess) {
+  if (hipMalloc(&c->d_err, 32 * sizeof(int)) != hipSuccess || hipMemset(c->d_err, 0, 32 * sizeof(int)) != hipSuccess) {
     delete c;
     return CBH_E_HIP;
   }
@@ -1376,6 +1413,9 @@ int cbh_ctx_destroy(cbh_ctx* ctx) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->evpool) (void)hipEventDestroy(e);
   if (ctx->ws) (void)hipFree(ctx->ws);
+  if (ctx->pin) (void)hipHostFree(ctx->pin);
+  for (auto& e : ctx->pin_ev)
+    if (e) (void)hipEventDestroy(e);
   release_cache(ctx);
   for (auto& kv : ctx->live) (void)hipFree(kv.first);  // matrices not freed by the caller
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
@@ -1420,6 +1460,16 @@ int cbh_ctx_trim(cbh_ctx* ctx) {
 }
 
 const char* cbh_last_error(cbh_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int cbh_ctx_take_retries(cbh_ctx* ctx, int64_t* subtile_retries) {
+  if (!ctx || !subtile_retries) return CBH_E_ARG;
+  int h = 0;
+  CBH_HIP(ctx, hipMemcpyAsync(&h, ctx->d_err + 16, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipMemsetAsync(ctx->d_err + 16, 0, sizeof(int), ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  *subtile_retries = h;
+  return CBH_OK;
+}
 
 int cbh_ctx_set_allocator(cbh_ctx* ctx, cbh_alloc_fn alloc, cbh_free_fn release, void* user) {
   if (!ctx || (alloc == nullptr) != (release == nullptr)) return CBH_E_ARG;
@@ -1531,6 +1581,114 @@ int cbh_mat_device_arrays(const cbh_mat* M, const int64_t** cp, const int64_t** 
   return CBH_OK;
 }
 
+}  // extern "C"
+
+// the two pinned staging halves for chunks of `chunk` entries of (int32 row, vb-byte value)
+static int pinned_halves(cbh_ctx* ctx, int64_t chunk, int64_t vb, char* half[2]) {
+  const size_t hb = (size_t)chunk * (size_t)(4 + vb) + 256;
+  if (ctx->pin_bytes < 2 * hb) {
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->pin) (void)hipHostFree(ctx->pin);
+    ctx->pin = nullptr;
+    ctx->pin_bytes = 0;
+    CBH_HIP(ctx, hipHostMalloc(&ctx->pin, 2 * hb, hipHostMallocDefault));
+    ctx->pin_bytes = 2 * hb;
+  }
+  for (auto& e : ctx->pin_ev)
+    if (!e) CBH_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  half[0] = reinterpret_cast<char*>(ctx->pin);
+  half[1] = half[0] + ctx->pin_bytes / 2;
+  return CBH_OK;
+}
+static int64_t chunk_entries(int64_t chunk) { return chunk > 0 ? chunk : (int64_t)4 << 20; }
+
+extern "C" {
+
+int cbh_mat_upload_chunks(cbh_ctx* ctx, int64_t m, int64_t n, int64_t nnz, int64_t nzc, const int64_t* cp,
+                          const int64_t* jc, cbh_dtype dtype, int64_t value_bytes, int64_t chunk, cbh_fill_fn fill,
+                          void* user, cbh_mat** out) {
+  if (!ctx || !out || !fill || nnz < 0 || nzc < 0 || m < 0 || n < 0 || (nzc > 0 && (!cp || !jc)))
+    return fail(ctx, CBH_E_ARG, "bad chunked upload arguments");
+  const int64_t vb = dtype == CBH_OPAQUE ? value_bytes : (int64_t)dtype_size(dtype);
+  if (vb <= 0) return fail(ctx, CBH_E_ARG, "bad value size");
+  if (m > INT32_MAX) return fail(ctx, CBH_E_DIMMISMATCH, "local rows exceed int32");
+  *out = nullptr;
+  cbh_mat* M;
+  CBH_TRY(new_mat(ctx, m, n, nnz, nzc, dtype, &M, vb));
+  int rc = CBH_OK;
+  auto body = [&]() -> int {
+    if (nzc > 0) {
+      CBH_HIP(ctx, hipMemcpyAsync(M->cp, cp, sizeof(int64_t) * (nzc + 1), hipMemcpyHostToDevice, ctx->stream));
+      CBH_HIP(ctx, hipMemcpyAsync(M->jc, jc, sizeof(int64_t) * nzc, hipMemcpyHostToDevice, ctx->stream));
+    } else {
+      CBH_HIP(ctx, hipMemsetAsync(M->cp, 0, sizeof(int64_t), ctx->stream));
+    }
+    const int64_t ch = chunk_entries(chunk);
+    char* half[2];
+    CBH_TRY(pinned_halves(ctx, ch, vb, half));
+    bool used[2] = {false, false};
+    for (int64_t f = 0, k = 0; f < nnz; f += ch, ++k) {
+      const int h = (int)(k & 1);
+      const int64_t cnt = std::min(ch, nnz - f);
+      if (used[h]) CBH_HIP(ctx, hipEventSynchronize(ctx->pin_ev[h]));  // the copy out of this half is done
+      int32_t* sir = reinterpret_cast<int32_t*>(half[h]);
+      char* snum = half[h] + (((size_t)ch * 4 + 255) & ~size_t(255));
+      const int r = fill(user, f, cnt, sir, snum);
+      if (r != 0) return fail(ctx, r, "upload fill callback returned " + std::to_string(r));
+      CBH_HIP(ctx, hipMemcpyAsync(M->ir + f, sir, sizeof(int32_t) * cnt, hipMemcpyHostToDevice, ctx->stream));
+      CBH_HIP(ctx, hipMemcpyAsync(reinterpret_cast<char*>(M->num) + f * vb, snum, (size_t)(vb * cnt),
+                                  hipMemcpyHostToDevice, ctx->stream));
+      CBH_HIP(ctx, hipEventRecord(ctx->pin_ev[h], ctx->stream));
+      used[h] = true;
+    }
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // cp / jc may be released on return
+    return CBH_OK;
+  };
+  rc = body();
+  if (rc != CBH_OK) {
+    (void)hipStreamSynchronize(ctx->stream);
+    cbh_mat_free(ctx, M);
+    return rc;
+  }
+  *out = M;
+  return CBH_OK;
+}
+
+int cbh_mat_download_chunks(cbh_ctx* ctx, const cbh_mat* M, int64_t* cp, int64_t* jc, int64_t chunk, cbh_take_fn take,
+                            void* user) {
+  if (!ctx || !M || !take) return fail(ctx, CBH_E_ARG, "bad chunked download arguments");
+  if (cp) CBH_HIP(ctx, hipMemcpyAsync(cp, M->cp, sizeof(int64_t) * (M->nzc + 1), hipMemcpyDeviceToHost, ctx->stream));
+  if (jc && M->nzc) CBH_HIP(ctx, hipMemcpyAsync(jc, M->jc, sizeof(int64_t) * M->nzc, hipMemcpyDeviceToHost, ctx->stream));
+  const int64_t nnz = M->nnz, vb = M->vbytes;
+  const int64_t ch = chunk_entries(chunk);
+  char* half[2];
+  CBH_TRY(pinned_halves(ctx, ch, vb, half));
+  auto issue = [&](int64_t f, int h) -> int {
+    const int64_t cnt = std::min(ch, nnz - f);
+    char* snum = half[h] + (((size_t)ch * 4 + 255) & ~size_t(255));
+    CBH_HIP(ctx, hipMemcpyAsync(half[h], M->ir + f, sizeof(int32_t) * cnt, hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(snum, reinterpret_cast<const char*>(M->num) + f * vb, (size_t)(vb * cnt),
+                                hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipEventRecord(ctx->pin_ev[h], ctx->stream));
+    return CBH_OK;
+  };
+  if (nnz > 0) CBH_TRY(issue(0, 0));
+  for (int64_t f = 0, k = 0; f < nnz; f += ch, ++k) {
+    const int h = (int)(k & 1);
+    if (f + ch < nnz) CBH_TRY(issue(f + ch, h ^ 1));  // the next chunk moves while this one is taken
+    CBH_HIP(ctx, hipEventSynchronize(ctx->pin_ev[h]));
+    const int64_t cnt = std::min(ch, nnz - f);
+    const int r = take(user, f, cnt, reinterpret_cast<const int32_t*>(half[h]),
+                       half[h] + (((size_t)ch * 4 + 255) & ~size_t(255)));
+    if (r != 0) {
+      (void)hipStreamSynchronize(ctx->stream);
+      return fail(ctx, r, "download take callback returned " + std::to_string(r));
+    }
+  }
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return CBH_OK;
+}
+
 int cbh_mat_copy_out(cbh_ctx* ctx, const cbh_mat* M, int64_t* cp, int64_t* jc, int32_t* ir, void* num,
                      int dst_on_device) {
   if (!ctx || !M) return CBH_E_ARG;
@@ -1613,7 +1771,7 @@ int cbh_spgemm_symbolic(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, int64_
   }
   Scratch S(ctx);
   Plan P;
-  CBH_TRY(run_symbolic(ctx, S, A, B, P));
+  CBH_TRY(run_symbolic(ctx, S, A, B, P, true));
   if (flops) *flops = P.total_flops;
   if (nnzC) *nnzC = P.total_nnz;
   if (col_flops_dev)
@@ -1651,7 +1809,7 @@ int cbh_spgemm(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh_mat* B
       CBH_HIP(ctx, hipMemcpyAsync(&nzcC, pos + P.nzcB, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
       CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
     }
-    CBH_TRY(new_mat(ctx, A->m, B->n, P.total_nnz, nzcC, A->dtype, &out));
+    CBH_TRY(new_result(ctx, S, P, A->m, B->n, P.total_nnz, nzcC, A->dtype, &out));
     int64_t launches = 0;
     int rc = run_numeric<SR>(ctx, S, A, B, P, 0, P.ntasks, 0, out->ir, out->num, &launches, P.total_nnz);
     if (rc == CBH_OK) {
@@ -1754,6 +1912,10 @@ int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh
       ctx->ws_bytes = 0;
       if (hipMalloc(&ctx->ws, (size_t)need) != hipSuccess) {
         (void)hipGetLastError();
+        if (P.bmp) {  // the workspace does not fit beside the stored bitmaps: dense windows off
+          S.drop(P.bmp);
+          P.bmp = nullptr;
+        }
         release_cache(ctx);
         CBH_HIP(ctx, hipMalloc(&ctx->ws, (size_t)need));
       }
@@ -1785,6 +1947,7 @@ int cbh_spgemm_phased(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh
       const double tp = hnow();
       CBH_TRY(run_numeric<SR>(ctx, S, A, B, P, hts[c0], hts[c1], hcp[c0], ir, num, &launches, maxphase));
       if (ctx->phase_fn) {
+        CBH_TRY(check_err(ctx));  // the consumer sees only a phase whose guards all passed
         hipLaunchKernelGGL(keep_cols_kernel, dim3(blocks_for(c1 - c0 + 1, 256)), dim3(256), 0, ctx->stream, B->jc + c0,
                            P.Ccp + c0, c1 - c0, hcp[c0], vjc, vcp);
         CBH_HIP(ctx, hipGetLastError());
@@ -1900,7 +2063,7 @@ int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t
   CBH_TRY(exclusive_scan_i64(ctx, p->S, flag, p->pos, P.nzcB + 1));
   CBH_HIP(ctx, hipMemcpyAsync(&p->nzcC, p->pos + P.nzcB, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  CBH_TRY(new_mat(ctx, p->A->m, p->B->n, P.total_nnz, P.nzcB, dtype, C, value_bytes));
+  CBH_TRY(new_result(ctx, p->S, P, p->A->m, p->B->n, P.total_nnz, P.nzcB, dtype, C, value_bytes));
   // bins: dense (built-in, lock-free semirings only), then hash large / small
   using CD = TaskCfg<PlusTimesD<double>, TNumLarge::T, TNumLarge::BS, TNumLarge::EMAX, TNumLarge::U, MODE_TDENSE>;
   const int64_t nt = P.ntasks;
@@ -2025,7 +2188,7 @@ int cbh_plan_spgemm_slots(cbh_plan* p, cbh_semiring sr, int64_t s0, int64_t s1, 
     CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
     const int64_t nnz = h[3] - h[2];
     cbh_mat* out;
-    CBH_TRY(new_mat(ctx, A->m, B->n, nnz, nzcC, A->dtype, &out));
+    CBH_TRY(new_result(ctx, p->S, P, A->m, B->n, nnz, nzcC, A->dtype, &out));
     int rc = run_numeric<SR>(ctx, S, A, B, P, h[0], h[1], h[2], out->ir, out->num, nullptr, nnz);
     if (rc == CBH_OK) {
       if (keep)

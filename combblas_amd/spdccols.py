@@ -117,6 +117,12 @@ class Context:
         """return the built-in allocator's cached blocks and the phase workspace to HIP"""
         check(lib().cbh_ctx_trim(self.h), self.h)
 
+    def take_retries(self):
+        """sub-tiles the task kernels retried with half the row range since the last call (resets)"""
+        n = ctypes.c_int64()
+        check(lib().cbh_ctx_take_retries(self.h, ctypes.byref(n)), self.h)
+        return n.value
+
     def enable_timing(self, on=True):
         check(lib().cbh_ctx_enable_timing(self.h, int(on)), self.h)
 

@@ -94,6 +94,9 @@ int cbh_ctx_synchronize(cbh_ctx* ctx);
  * default allocator keeps freed blocks for reuse in stream order).                            */
 int cbh_ctx_trim(cbh_ctx* ctx);
 const char* cbh_last_error(cbh_ctx* ctx);
+/* Sub-tiles the task kernels retried with half the row range (table overflow, commit queue) since
+ * the last call; resets the counter (diagnostics and tests). */
+int cbh_ctx_take_retries(cbh_ctx* ctx, int64_t* subtile_retries);
 /* Route every device allocation of this context through caller callbacks (e.g. the torch
  * caching allocator), stream-ordered on `stream`. NULL alloc restores the built-in block cache.        */
 typedef void* (*cbh_alloc_fn)(void* user, int64_t bytes, void* stream);
@@ -121,6 +124,21 @@ int cbh_mat_info(const cbh_mat* mat, int64_t* m, int64_t* n, int64_t* nnz, int64
 /* Device pointers of the matrix arrays (valid until cbh_mat_free). */
 int cbh_mat_device_arrays(const cbh_mat* mat, const int64_t** cp, const int64_t** jc,
                           const int32_t** ir, const void** num);
+/* Chunked host transfers through the context's pinned staging buffers (the drop-in adaptors'
+ * SpDCCols <-> device path, HipSpGEMM.h). Entries move in chunks of `chunk` (<= 0: 4 M); while
+ * the copy engine moves chunk k+1, the callback converts chunk k on the host (the adaptor's
+ * OpenMP threads: int64 row ids <-> the device's int32, AoS tuples, ...).
+ *   upload: cbh_fill_fn writes entries [first, first+count) into the staging arrays ir / num
+ *           (num: value_bytes per entry); cp / jc are copied as given (nzc + 1 and nzc int64s).
+ *   download: cbh_take_fn reads entries [first, first+count) of the matrix from staging.
+ * A callback returning nonzero aborts the transfer with that code.                           */
+typedef int (*cbh_fill_fn)(void* user, int64_t first, int64_t count, int32_t* ir, void* num);
+typedef int (*cbh_take_fn)(void* user, int64_t first, int64_t count, const int32_t* ir, const void* num);
+int cbh_mat_upload_chunks(cbh_ctx* ctx, int64_t m, int64_t n, int64_t nnz, int64_t nzc, const int64_t* cp,
+                          const int64_t* jc, cbh_dtype dtype, int64_t value_bytes, int64_t chunk,
+                          cbh_fill_fn fill, void* user, cbh_mat** out);
+int cbh_mat_download_chunks(cbh_ctx* ctx, const cbh_mat* mat, int64_t* cp, int64_t* jc, int64_t chunk,
+                            cbh_take_fn take, void* user);
 /* Copy the matrix arrays to caller buffers; dst_on_device selects hipMemcpy direction. */
 int cbh_mat_copy_out(cbh_ctx* ctx, const cbh_mat* mat, int64_t* cp, int64_t* jc, int32_t* ir,
                      void* num, int dst_on_device);

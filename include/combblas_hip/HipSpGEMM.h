@@ -5,12 +5,14 @@
 //   combblas_hip::LocalSpGEMMHash<SR,NTO>(A, B, clearA, clearB, sort)    (mtSpGEMM.h:463-467)
 //   combblas_hip::LocalSpGEMM<SR,NTO>(A, B, clearA, clearB)              (mtSpGEMM.h:74-78)
 //   combblas_hip::MultiwayMerge<SR>(ArrSpTups, mdim, ndim, delarrs)      (MultiwayMerge.h:411-412)
+//   combblas_hip::mult_synch_host<SR>(A, B, clearA, clearB)              (Mult_AnXBn_Synch, ParFriends.h:1004-1108)
 // with the reference signatures and ownership rules (heap SpTuples* the caller deletes, tuples
 // allocated with ::operator new and flagged isOperatorNew, clearA/clearB delete the inputs,
 // delarrs deletes the merged lists), and the macro
 //   COMBBLAS_HIP_INSTANTIATE(SR, IT, NT)
 // that declares explicit specializations of combblas::LocalHybridSpGEMM / LocalSpGEMMHash /
-// LocalSpGEMM / MultiwayMerge for that semiring and types, so that the UNCHANGED reference
+// LocalSpGEMM / MultiwayMerge / MultiwayMergeHash and, for SpParMats over SpDCCols<IT,NT>,
+// Mult_AnXBn_Synch (PSpGEMM's driver) for that semiring and types, so that the UNCHANGED reference
 // drivers (PSpGEMM -> Mult_AnXBn_Synch, ParFriends.h:1004-1108; MemEfficientSpGEMM; the 3D
 // drivers) instantiate the HIP versions. Use it at namespace scope, after this header and before
 // the first call that instantiates a driver. Built-in semirings map to device functors through
@@ -24,7 +26,9 @@
 #include <mpi.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <limits>
@@ -90,38 +94,69 @@ struct MatGuard {
   }
 };
 
+// Host <-> device transfers of the adaptors go through the context's pinned staging in chunks
+// (cbh_mat_upload_chunks / cbh_mat_download_chunks): the copy engine moves one chunk while the
+// OpenMP threads below convert the next (int64 row ids <-> int32, SpTuples' AoS layout).
+// Per-process totals of the adaptor's stages (seconds), printed per driver call with
+// COMBBLAS_HIP_TIMING=1 and read by the drop-in bench harness.
+struct AdaptorTimes {
+  double upload = 0, kernel = 0, merge = 0, download = 0, build = 0;
+  int64_t calls = 0;
+};
+inline AdaptorTimes& adaptor_times() {
+  static AdaptorTimes t;
+  return t;
+}
+inline double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+inline bool timing_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("COMBBLAS_HIP_TIMING");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+
 // SpDCCols<IT,NT> (Dcsc arrays) -> device matrix. Row ids narrowed to the local int32 layout.
 template <class IT, class NT>
 cbh_mat* upload(const combblas::SpDCCols<IT, NT>& A) {
-  cbh_dcsc h{};
-  h.m = A.getnrow();
-  h.n = A.getncol();
-  h.nnz = A.getnnz();
-  h.nzc = A.getnzc();
-  std::vector<int64_t> cp(1, 0), jc;
-  std::vector<int32_t> ir;
-  std::vector<unsigned char> num;
-  if (h.nnz > 0) {
-    combblas::Dcsc<IT, NT>* d = A.GetDCSC();
-    cp.assign(d->cp, d->cp + d->nzc + 1);
-    jc.assign(d->jc, d->jc + d->nzc);
-    ir.resize(d->nz);
-    const IT nz = d->nz;
-    const IT* dir = d->ir;
-#pragma omp parallel for schedule(static)
-    for (IT i = 0; i < nz; ++i) ir[i] = static_cast<int32_t>(dir[i]);
-    num.resize(sizeof(NT) * d->nz);
-    std::memcpy(num.data(), d->numx, sizeof(NT) * d->nz);
-  }
-  h.cp = cp.data();
-  h.jc = jc.data();
-  h.ir = ir.data();
-  h.num = num.data();
-  if (h.m > std::numeric_limits<int32_t>::max()) die(context(), CBH_E_DIMMISMATCH, "local rows exceed int32");
   static_assert(std::is_trivially_copyable<NT>::value, "device values must be trivially copyable");
+  const int64_t m = A.getnrow(), n = A.getncol();
+  if (m > std::numeric_limits<int32_t>::max()) die(context(), CBH_E_DIMMISMATCH, "local rows exceed int32");
+  combblas::Dcsc<IT, NT>* d = A.getnnz() > 0 ? A.GetDCSC() : nullptr;
+  const int64_t nnz = d ? (int64_t)d->nz : 0, nzc = d ? (int64_t)d->nzc : 0;
+  std::vector<int64_t> cpv, jcv;
+  const int64_t *cp = nullptr, *jc = nullptr;
+  if (d) {
+    if (std::is_same<IT, int64_t>::value) {
+      cp = reinterpret_cast<const int64_t*>(d->cp);
+      jc = reinterpret_cast<const int64_t*>(d->jc);
+    } else {
+      cpv.assign(d->cp, d->cp + nzc + 1);
+      jcv.assign(d->jc, d->jc + nzc);
+      cp = cpv.data();
+      jc = jcv.data();
+    }
+  }
+  struct Src {
+    const IT* ir;
+    const NT* num;
+  } src{d ? d->ir : nullptr, d ? d->numx : nullptr};
+  cbh_fill_fn fill = [](void* u, int64_t f, int64_t cnt, int32_t* ir, void* num) -> int {
+    const Src* s = static_cast<const Src*>(u);
+    NT* out = static_cast<NT*>(num);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < cnt; ++i) {
+      ir[i] = static_cast<int32_t>(s->ir[f + i]);
+      out[i] = s->num[f + i];
+    }
+    return 0;
+  };
   cbh_mat* out = nullptr;
-  int rc = upload_dcsc(h, dtype_of<NT>::value, (int64_t)sizeof(NT), &out);
-  if (rc != CBH_OK) die(context(), rc, "cbh_mat_upload");
+  int rc = cbh_mat_upload_chunks(context(), m, n, nnz, nzc, cp, jc, dtype_of<NT>::value, (int64_t)sizeof(NT), 0, fill,
+                                 &src, &out);
+  if (rc != CBH_OK) die(context(), rc, "cbh_mat_upload_chunks");
   return out;
 }
 
@@ -180,22 +215,107 @@ cbh_mat* upload(const combblas::SpTuples<IT, NT>& T, bool sort_rows = false) {
   return out;
 }
 
-// device DCSC -> SpTuples<IT,NT>* (column-sorted; ::operator new tuples, mtSpGEMM.h:272,453)
+// device DCSC -> SpTuples<IT,NT>* (column-sorted; ::operator new tuples, mtSpGEMM.h:272,453). The
+// tuples are packed from the pinned chunks by the OpenMP threads, blocks of 4096 entries each
+// finding their first column by one bisection of cp.
 template <class IT, class NT>
 combblas::SpTuples<IT, NT>* download_tuples(cbh_mat* C) {
   int64_t m, n, nnz, nzc;
   cbh_mat_info(C, &m, &n, &nnz, &nzc, nullptr);
-  std::vector<int64_t> cp(nzc + 1), jc(nzc);
-  std::vector<int32_t> ir(nnz);
-  std::unique_ptr<NT[]> num(new NT[nnz > 0 ? nnz : 1]);
-  int rc = cbh_mat_copy_out(context(), C, cp.data(), jc.data(), ir.data(), reinterpret_cast<void*>(num.get()), 0);
-  if (rc != CBH_OK) die(context(), rc, "cbh_mat_copy_out");
   if (nnz == 0) return new combblas::SpTuples<IT, NT>(0, (IT)m, (IT)n);
+  std::vector<int64_t> cp(nzc + 1), jc(nzc);
   auto* tuples = static_cast<std::tuple<IT, IT, NT>*>(::operator new(sizeof(std::tuple<IT, IT, NT>) * nnz));
-#pragma omp parallel for schedule(dynamic, 1024)
-  for (int64_t c = 0; c < nzc; ++c)
-    for (int64_t p = cp[c]; p < cp[c + 1]; ++p) tuples[p] = std::make_tuple((IT)ir[p], (IT)jc[c], num[p]);
+  struct Dst {
+    std::tuple<IT, IT, NT>* t;
+    const int64_t* cp;
+    const int64_t* jc;
+    int64_t nzc;
+  } dst{tuples, cp.data(), jc.data(), nzc};
+  cbh_take_fn take = [](void* u, int64_t f, int64_t cnt, const int32_t* ir, const void* num) -> int {
+    const Dst* d = static_cast<const Dst*>(u);
+    const NT* v = static_cast<const NT*>(num);
+    const int64_t nb = (cnt + 4095) / 4096;
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < nb; ++b) {
+      const int64_t p0 = f + b * 4096, p1 = std::min(f + cnt, p0 + 4096);
+      int64_t c = (int64_t)(std::upper_bound(d->cp, d->cp + d->nzc + 1, p0) - d->cp) - 1;
+      for (int64_t p = p0; p < p1; ++p) {
+        while (d->cp[c + 1] <= p) ++c;
+        d->t[p] = std::make_tuple((IT)ir[p - f], (IT)d->jc[c], v[p - f]);
+      }
+    }
+    return 0;
+  };
+  int rc = cbh_mat_download_chunks(context(), C, cp.data(), jc.data(), 0, take, &dst);
+  if (rc != CBH_OK) die(context(), rc, "cbh_mat_download_chunks");
   return new combblas::SpTuples<IT, NT>(nnz, (IT)m, (IT)n, tuples, true, true);
+}
+
+// device DCSC -> a host SpDCCols<IT,NT> built directly (no SpTuples round trip): the Dcsc arrays
+// are allocated by SpDCCols(nnz, m, n, nzc) (SpDCCols.cpp:55-62) and filled from the chunks.
+template <class IT, class NT>
+combblas::SpDCCols<IT, NT>* download_dcsc(const cbh_mat* C) {
+  int64_t m, n, nnz, nzc;
+  cbh_mat_info(C, &m, &n, &nnz, &nzc, nullptr);
+  if (nnz == 0) return new combblas::SpDCCols<IT, NT>((IT)0, (IT)m, (IT)n, (IT)0);
+  auto* S = new combblas::SpDCCols<IT, NT>((IT)nnz, (IT)m, (IT)n, (IT)nzc);
+  combblas::Dcsc<IT, NT>* d = S->GetDCSC();
+  std::vector<int64_t> cpv, jcv;
+  int64_t *cp, *jc;
+  if (std::is_same<IT, int64_t>::value) {
+    cp = reinterpret_cast<int64_t*>(d->cp);
+    jc = reinterpret_cast<int64_t*>(d->jc);
+  } else {
+    cpv.resize(nzc + 1);
+    jcv.resize(nzc);
+    cp = cpv.data();
+    jc = jcv.data();
+  }
+  struct Dst {
+    IT* ir;
+    NT* num;
+  } dst{d->ir, d->numx};
+  cbh_take_fn take = [](void* u, int64_t f, int64_t cnt, const int32_t* ir, const void* num) -> int {
+    const Dst* t = static_cast<const Dst*>(u);
+    const NT* v = static_cast<const NT*>(num);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < cnt; ++i) {
+      t->ir[f + i] = (IT)ir[i];
+      t->num[f + i] = v[i];
+    }
+    return 0;
+  };
+  int rc = cbh_mat_download_chunks(context(), C, cp, jc, 0, take, &dst);
+  if (rc != CBH_OK) die(context(), rc, "cbh_mat_download_chunks");
+  if (!std::is_same<IT, int64_t>::value) {
+    std::copy(cpv.begin(), cpv.end(), d->cp);
+    std::copy(jcv.begin(), jcv.end(), d->jc);
+  }
+  return S;
+}
+
+// MultiwayMerge of any number of device partials (MultiwayMerge.h:411-526 takes any count): one
+// cbh_merge per group of at most kMaxLists (16) lists, the group results merged again until one
+// is left; every input and intermediate is freed. Takes ownership of `parts` (non-empty).
+inline cbh_mat* merge_all(cbh_semiring sr, std::vector<cbh_mat*> parts) {
+  constexpr size_t kGroup = 16;  // cbh_merge's list limit (kMaxLists)
+  while (parts.size() > 1) {
+    std::vector<cbh_mat*> next;
+    for (size_t g = 0; g < parts.size(); g += kGroup) {
+      const size_t k = std::min(kGroup, parts.size() - g);
+      if (k == 1) {
+        next.push_back(parts[g]);
+        continue;
+      }
+      cbh_mat* C = nullptr;
+      int rc = cbh_merge(context(), sr, (int)k, parts.data() + g, &C);
+      if (rc != CBH_OK) die(context(), rc, "cbh_merge");
+      for (size_t i = g; i < g + k; ++i) cbh_mat_free(context(), parts[i]);
+      next.push_back(C);
+    }
+    parts.swap(next);
+  }
+  return parts[0];
 }
 
 template <class SR, class NTO, class IT, class NT1, class NT2>
@@ -243,11 +363,14 @@ combblas::SpTuples<IT, NT>* MultiwayMerge(std::vector<combblas::SpTuples<IT, NT>
   if (nlists == 0) return new combblas::SpTuples<IT, NT>(0, mdim, ndim);
   if (nlists == 1) {
     if (delarrs) return lists[0];  // MultiwayMerge.h:422-425 steals the input
-    // MultiwayMerge.h:426-438: a copy of the one list, no dimension check (pure data movement)
+    // MultiwayMerge.h:426-438: a copy of the one list, no dimension check (pure data movement;
+    // ::operator new storage, filled in parallel, no value-initialisation pass)
     const int64_t nnz = lists[0]->getnnz();
-    auto* t = new std::tuple<IT, IT, NT>[nnz];
-    for (int64_t i = 0; i < nnz; ++i) t[i] = lists[0]->tuples[i];
-    return new combblas::SpTuples<IT, NT>(nnz, mdim, ndim, t, false);
+    auto* t = static_cast<std::tuple<IT, IT, NT>*>(::operator new(sizeof(std::tuple<IT, IT, NT>) * (nnz > 0 ? nnz : 1)));
+    const std::tuple<IT, IT, NT>* src = lists[0]->tuples;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < nnz; ++i) t[i] = src[i];
+    return new combblas::SpTuples<IT, NT>(nnz, mdim, ndim, t, false, true);
   }
   for (int i = 0; i < nlists; ++i)
     if (mdim != lists[i]->getnrow() || ndim != lists[i]->getncol()) {
@@ -302,6 +425,90 @@ combblas::SpTuples<IT, NT>* MultiwayMergeHash(std::vector<combblas::SpTuples<IT,
   return combblas_hip::MultiwayMerge<SR, IT, NT>(lists, mdim, ndim, delarrs, true);
 }
 
+// Mult_AnXBn_Synch (ParFriends.h:1004-1108) for SpParMats over the stock SpDCCols with a built-in
+// semiring: the reference's SUMMA stage loop and host MPI broadcasts of the stage blocks
+// (SpParHelper::GetSetSizes / BCastMatrix, unchanged), every stage block uploaded through the
+// pinned chunks and multiplied on the device, the stage partials merged on the device
+// (MultiwayMerge), and C downloaded straight into the result's Dcsc arrays -- no SpTuples, no
+// host merge copy and no serial SpDCCols(SpTuples) conversion (SpDCCols.cpp:109-183).
+// clearA / clearB leave A / B with an empty block (the reference deletes it and sets NULL).
+template <class SR, class IU, class NU>
+combblas::SpParMat<IU, NU, combblas::SpDCCols<IU, NU>> mult_synch_host(
+    combblas::SpParMat<IU, NU, combblas::SpDCCols<IU, NU>>& A, combblas::SpParMat<IU, NU, combblas::SpDCCols<IU, NU>>& B,
+    bool clearA, bool clearB) {
+  typedef combblas::SpDCCols<IU, NU> DER;
+  if (!combblas::CheckSpGEMMCompliance(A, B)) return combblas::SpParMat<IU, NU, DER>();
+  AdaptorTimes& T = adaptor_times();
+  const AdaptorTimes before = T;
+  int stages, dummy;
+  std::shared_ptr<combblas::CommGrid> GridC =
+      ProductGrid(A.getcommgrid().get(), B.getcommgrid().get(), stages, dummy, dummy);
+  const IU C_m = A.seq().getnrow(), C_n = B.seq().getncol();
+  IU** ARecvSizes = combblas::SpHelper::allocate2D<IU>(DER::esscount, stages);
+  IU** BRecvSizes = combblas::SpHelper::allocate2D<IU>(DER::esscount, stages);
+  combblas::SpParHelper::GetSetSizes(A.seq(), ARecvSizes, A.getcommgrid()->GetRowWorld());
+  combblas::SpParHelper::GetSetSizes(B.seq(), BRecvSizes, B.getcommgrid()->GetColWorld());
+  const int Aself = A.getcommgrid()->GetRankInProcRow();
+  const int Bself = B.getcommgrid()->GetRankInProcCol();
+  std::vector<cbh_mat*> parts;
+  for (int i = 0; i < stages; ++i) {
+    std::vector<IU> ess;
+    DER* ARecv = &A.seq();
+    if (i != Aself) {
+      for (int j = 0; j < DER::esscount; ++j) ess.push_back(ARecvSizes[j][i]);
+      ARecv = new DER();
+    }
+    combblas::SpParHelper::BCastMatrix(GridC->GetRowWorld(), *ARecv, ess, i);
+    ess.clear();
+    DER* BRecv = &B.seq();
+    if (i != Bself) {
+      for (int j = 0; j < DER::esscount; ++j) ess.push_back(BRecvSizes[j][i]);
+      BRecv = new DER();
+    }
+    combblas::SpParHelper::BCastMatrix(GridC->GetColWorld(), *BRecv, ess, i);
+    if (!ARecv->isZero() && !BRecv->isZero()) {
+      const double t0 = now_s();
+      MatGuard a, b;
+      a.m = upload(*ARecv);
+      b.m = upload(*BRecv);
+      const double t1 = now_s();
+      cbh_mat* Ci = nullptr;
+      int rc = cbh_spgemm(context(), semiring_traits<SR>::code, a.m, b.m, CBH_SORTED_ROWS, &Ci);
+      if (rc != CBH_OK) die(context(), rc, "cbh_spgemm");
+      T.upload += t1 - t0;
+      T.kernel += now_s() - t1;
+      int64_t nnz = 0;
+      cbh_mat_info(Ci, nullptr, nullptr, &nnz, nullptr, nullptr);
+      if (nnz > 0) parts.push_back(Ci);  // `if(!C_cont->isZero()) tomerge.push_back`
+      else cbh_mat_free(context(), Ci);
+    }
+    if (i != Aself) delete ARecv;  // the reference's clearA / clearB = i != self
+    if (i != Bself) delete BRecv;
+  }
+  combblas::SpHelper::deallocate2D(ARecvSizes, DER::esscount);
+  combblas::SpHelper::deallocate2D(BRecvSizes, DER::esscount);
+  if (clearA) A.seq() = DER();
+  if (clearB) B.seq() = DER();
+  const double t2 = now_s();
+  DER* C;
+  if (parts.empty()) {
+    C = new DER((IU)0, C_m, C_n, (IU)0);
+  } else {
+    cbh_mat* Cd = parts.size() == 1 ? parts[0] : merge_all(semiring_traits<SR>::code, parts);
+    const double t3 = now_s();
+    T.merge += t3 - t2;
+    C = download_dcsc<IU, NU>(Cd);
+    cbh_mat_free(context(), Cd);
+    T.download += now_s() - t3;
+  }
+  T.calls += 1;
+  if (timing_enabled())
+    std::fprintf(stderr, "[combblas_hip] Mult_AnXBn_Synch: upload %.1f ms, kernel %.1f ms, merge %.1f ms, download %.1f ms\n",
+                 1e3 * (T.upload - before.upload), 1e3 * (T.kernel - before.kernel), 1e3 * (T.merge - before.merge),
+                 1e3 * (T.download - before.download));
+  return combblas::SpParMat<IU, NU, DER>(C, GridC);
+}
+
 }  // namespace combblas_hip
 
 // Route the reference's own drivers to the device path for (SR, IT, NT): explicit
@@ -334,5 +541,11 @@ combblas::SpTuples<IT, NT>* MultiwayMergeHash(std::vector<combblas::SpTuples<IT,
   inline SpTuples<IT, NT>* MultiwayMergeHash<SR, IT, NT>(std::vector<SpTuples<IT, NT>*> & L, IT mdim, IT ndim, \
                                                          bool delarrs, bool sorted) {                         \
     return combblas_hip::MultiwayMergeHash<SR, IT, NT>(L, mdim, ndim, delarrs, sorted);                      \
+  }                                                                                                           \
+  template <>                                                                                                 \
+  inline SpParMat<IT, NT, SpDCCols<IT, NT>>                                                                   \
+  Mult_AnXBn_Synch<SR, NT, SpDCCols<IT, NT>, IT, NT, NT, SpDCCols<IT, NT>, SpDCCols<IT, NT>>(                 \
+      SpParMat<IT, NT, SpDCCols<IT, NT>> & A, SpParMat<IT, NT, SpDCCols<IT, NT>> & B, bool clearA, bool clearB) { \
+    return combblas_hip::mult_synch_host<SR, IT, NT>(A, B, clearA, clearB);                                  \
   }                                                                                                           \
   }

@@ -233,30 +233,6 @@ cbh_mat* local_multiply(const cbh_mat* A, const cbh_mat* B) {
   return C;
 }
 
-// MultiwayMerge of any number of device partials (MultiwayMerge.h:411-526 takes any count): one
-// cbh_merge per group of at most kMaxLists (16) lists, the group results merged again until one
-// is left; every input and intermediate is freed. Takes ownership of `parts` (non-empty).
-inline cbh_mat* merge_all(cbh_semiring sr, std::vector<cbh_mat*> parts) {
-  constexpr size_t kGroup = 16;  // cbh_merge's list limit (kMaxLists)
-  while (parts.size() > 1) {
-    std::vector<cbh_mat*> next;
-    for (size_t g = 0; g < parts.size(); g += kGroup) {
-      const size_t k = std::min(kGroup, parts.size() - g);
-      if (k == 1) {
-        next.push_back(parts[g]);
-        continue;
-      }
-      cbh_mat* C = nullptr;
-      int rc = cbh_merge(context(), sr, (int)k, parts.data() + g, &C);
-      if (rc != CBH_OK) die(context(), rc, "cbh_merge");
-      for (size_t i = g; i < g + k; ++i) cbh_mat_free(context(), parts[i]);
-      next.push_back(C);
-    }
-    parts.swap(next);
-  }
-  return parts[0];
-}
-
 // The SUMMA stage loop of Mult_AnXBn_Synch (ParFriends.h:1004-1108) over two device blocks on their
 // grids (the local blocks of A and B, or B's phase piece): sizes exchanged on the host
 // (GetSetSizes), stage blocks broadcast device to device on the product grid's row (A) and column

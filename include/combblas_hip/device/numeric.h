@@ -18,7 +18,13 @@ namespace cbh {
 struct TSymSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 // 16 products per thread per window: half the owner-map windows of U = 8, for 12160 instead of
 // 13312 bitmap words so that two groups still share a CU (symbolic 201 -> 196 ms at scale 22)
-struct TSymLarge { static constexpr int T = 8192, BS = 512, EMAX = 512, U = 16; };
+#ifndef CBH_SYM_BS
+#define CBH_SYM_BS 512
+#endif
+#ifndef CBH_SYM_U
+#define CBH_SYM_U 16
+#endif
+struct TSymLarge { static constexpr int T = 8192, BS = CBH_SYM_BS, EMAX = 512, U = CBH_SYM_U; };
 // mid-size symbolic tasks (kSmallCap < products <= kSymMidCap): one sub-tile in a 16 KB key
 // table, five workgroups per CU, so the per-task setup latency overlaps
 constexpr int kSymMid = 2048;  // (1024 / 4096 measured no better)
@@ -29,6 +35,17 @@ struct TSymMid { static constexpr int T = 2 * kSymMid, BS = 256, EMAX = 256, U =
 struct TNumSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 // (T = 8192 with 1024-thread groups, one per CU: 89.1 vs 98.2 GFLOP/s at scale 22)
 struct TNumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512, U = 8; };
+// the library's large hash bin (MODE_TNUM; the dense windows keep TNumLarge)
+#ifndef CBH_HASH_T
+#define CBH_HASH_T 4096
+#endif
+#ifndef CBH_HASH_BS
+#define CBH_HASH_BS 512
+#endif
+#ifndef CBH_HASH_U
+#define CBH_HASH_U 8
+#endif
+struct TNumHash { static constexpr int T = CBH_HASH_T, BS = CBH_HASH_BS, EMAX = 512, U = CBH_HASH_U; };
 // mid-size hash tasks (kSmallCap < outputs <= kMidCap) of the library's A^2 path: a quarter of the
 // large kernel's LDS, so four workgroups share a CU and the per-task setup latency overlaps
 constexpr int kMidOut = 1024;  // (512 / 2048 measured no better)

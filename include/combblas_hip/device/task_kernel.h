@@ -407,10 +407,18 @@ struct TaskCfg {
 // MultiwayMerge.h:411-526); rows and values are addressed through list 0's arrays plus a
 // per-list element offset (all device allocations share one address space, 256-byte aligned),
 // so the sub-tile machinery above runs unchanged and the "product" is the list value itself.
+// Waves per SIMD the launch bounds ask for: groups of >= 512 threads get as many waves as the LDS
+// lets share a CU (160 KB: two 80 KB groups of 512 threads -> 4 waves per SIMD -> <= 128 VGPRs);
+// smaller groups keep 4.
+template <int BS, size_t BYTES>
+constexpr int task_waves_per_eu() {
+  if (BS < 512) return 4;
+  const int groups = (int)(163840 / (BYTES > 0 ? BYTES : 1));
+  const int w = (groups < 1 ? 1 : groups) * (BS / 64) / 4;
+  return w < 1 ? 1 : (w > 8 ? 8 : w);
+}
 template <class SR, int T, int BS, int EMAX, int U, int MODE, bool MERGE = false>
-// 512-thread groups: two per CU (LDS-bound), so 4 waves per SIMD -> <= 128 VGPRs; a 1024-thread
-// group is alone on its CU, same 4 waves per SIMD
-__global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) void task_kernel(TaskArgs a) {
+__global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX, U, MODE>::bytes>())) void task_kernel(TaskArgs a) {
   using C = TaskCfg<SR, T, BS, EMAX, U, MODE>;
   using val_t = typename C::val_t;
   using acc_t = typename C::acc_t;
@@ -1015,6 +1023,7 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 1 : (BS >= 512 ? 2048 / BS : 4)) v
         for (int i = tid; i < (int)ne; i += BS) epos[i] += eoff[i];
       __syncthreads();
       my_count = count_before;
+      if (tid == 0) atomicAdd(&a.err[16], 1);  // retry counter (cbh_ctx_take_retries)
       if (tw == 1) {
         if (tid == 0) atomicOr(&a.err[1], 1);
         return;

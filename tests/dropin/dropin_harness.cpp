@@ -17,9 +17,12 @@
 //   dropin_harness <scale>      -> prints "DROPIN <case> OK nnz=..." lines, exit 0 on success
 #include <mpi.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
+#include <string>
+#include <vector>
 
 #include "CombBLAS/CombBLAS.h"
 #include "combblas_hip/HipSpGEMMDevice.h"
@@ -108,8 +111,72 @@ static int run_case(const char* name, SpParMat<int64_t, NA, SpDCCols<int64_t, NA
   return ok ? 0 : 1;
 }
 
+// C1 line (bench_c1.py): PSpGEMM<PlusTimesSRing<double,double>> -- the reference's MultTest.cpp:161-181
+// plumbing, Mult_AnXBn_Synch on SpParMat<int64_t, double, SpDCCols> -- on the device path
+// (COMBBLAS_HIP_INSTANTIATE) and on the stock OpenMP path, first call and the median of `reps`
+// warm calls each, the device calls split into the adaptor's stages. Prints one BENCHC1 JSON line.
+static double median(std::vector<double> v) {
+  std::sort(v.begin(), v.end());
+  return v.empty() ? 0.0 : (v.size() % 2 ? v[v.size() / 2] : 0.5 * (v[v.size() / 2 - 1] + v[v.size() / 2]));
+}
+static int bench_c1(int scale, int reps) {
+  double init[4] = {.57, .19, .19, .05};
+  DistEdgeList<int64_t>* DEL = new DistEdgeList<int64_t>();
+  DEL->GenGraph500Data(init, scale, 16, true, true);
+  SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>> G(*DEL, false);
+  delete DEL;
+  typedef SpDCCols<int64_t, double> DER;
+  SpParMat<int64_t, double, DER> A(G), B(G);
+  combblas_hip::AdaptorTimes& T = combblas_hip::adaptor_times();
+  double t0 = MPI_Wtime();
+  SpParMat<int64_t, double, DER> C = Mult_AnXBn_Synch<PTDD, double, DER>(A, B);
+  const double first = MPI_Wtime() - t0;
+  std::vector<double> dev, up, ker, mer, down, cpu;
+  for (int r = 0; r < reps; ++r) {
+    const combblas_hip::AdaptorTimes b = T;
+    t0 = MPI_Wtime();
+    C = Mult_AnXBn_Synch<PTDD, double, DER>(A, B);
+    dev.push_back(MPI_Wtime() - t0);
+    up.push_back(T.upload - b.upload);
+    ker.push_back(T.kernel - b.kernel);
+    mer.push_back(T.merge - b.merge);
+    down.push_back(T.download - b.download);
+  }
+  t0 = MPI_Wtime();
+  SpParMat<int64_t, double, DER> Cc = Mult_AnXBn_Synch<CpuPlusTimes<double>, double, DER>(A, B);
+  const double cpu_first = MPI_Wtime() - t0;
+  for (int r = 0; r < reps; ++r) {
+    t0 = MPI_Wtime();
+    Cc = Mult_AnXBn_Synch<CpuPlusTimes<double>, double, DER>(A, B);
+    cpu.push_back(MPI_Wtime() - t0);
+  }
+  const bool ok = same(C.seq(), Cc.seq());
+  // flops = sum_k nnz(A(:,k)) * nnz(B(k,:)) on the one rank (EstimateFLOP)
+  std::vector<int64_t> rowcnt(A.seq().getnrow(), 0);
+  Dcsc<int64_t, double>* da = A.seq().GetDCSC();
+  for (int64_t i = 0; i < da->nz; ++i) rowcnt[da->ir[i]]++;
+  int64_t flops = 0;
+  for (int64_t c = 0; c < da->nzc; ++c) flops += (da->cp[c + 1] - da->cp[c]) * rowcnt[da->jc[c]];
+  const char* omp = std::getenv("OMP_NUM_THREADS");
+  std::printf("BENCHC1 {\"scale\": %d, \"nnzA\": %lld, \"nnzC\": %lld, \"flops\": %lld, \"match\": %s, \"reps\": %d, "
+              "\"first_s\": %.6f, \"warm_s\": %.6f, \"upload_s\": %.6f, \"kernel_s\": %.6f, \"merge_s\": %.6f, "
+              "\"download_s\": %.6f, \"cpu_first_s\": %.6f, \"cpu_s\": %.6f, \"cpu_threads\": %s}\n",
+              scale, (long long)A.getnnz(), (long long)C.getnnz(), (long long)flops, ok ? "true" : "false", reps, first,
+              median(dev), median(up), median(ker), median(mer), median(down), cpu_first, median(cpu), omp ? omp : "0");
+  std::fflush(stdout);
+  return ok ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
   MPI_Init(&argc, &argv);
+  if (argc > 1 && std::string(argv[1]) == "bench") {
+    int rc = 0;
+    {
+      rc = bench_c1(argc > 2 ? std::atoi(argv[2]) : 16, argc > 3 ? std::atoi(argv[3]) : 5);
+    }
+    MPI_Finalize();
+    return rc;
+  }
   int scale = argc > 1 ? std::atoi(argv[1]) : 12;
   int bad = 0;
   {  // every CombBLAS object must be destroyed before MPI_Finalize

@@ -1,0 +1,128 @@
+"""GPU tests of the driver-level fallbacks and hooks around the kernels:
+
+* the stored dense-candidate bitmaps are sized before nnz(C) is known; when C does not fit beside
+  them they are dropped and every task runs on the hash kernels (spgemm.hip new_result). The
+  test-only CBH_TEST_RESULT_OOM makes the first allocation of C report an OOM while bitmaps are
+  held; the product must still equal the oracle's, without any dense launch;
+* count-only symbolic callers (estimateFLOPandNNZ = cbh_spgemm_symbolic, EstPerProcessNnzSUMMA)
+  allocate no bitmaps: their counts equal the plan's;
+* the per-phase consumer of cbh_spgemm_phased (MemEfficientSpGEMM's prune hook) sees every phase of
+  a many-phase product, the concatenation of its cloned views equals the single-call product, and
+  an exception raised inside it comes back out of PhasedSpGEMM.
+"""
+import numpy as np
+import pytest
+
+import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rmat14(oracle):
+    import combblas_amd as cb
+
+    A = cb.rmat(14)
+    d = H.Dcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num)
+    return d, oracle.spgemm(d, d, "plus_times", threads=8)
+
+
+def _dense_launches(ctx, A, monkeypatch=None):
+    import combblas_amd as cb
+
+    h = cb.HostDcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num)
+    dA, dB = cb.SpDCCols.from_host(ctx, h), cb.SpDCCols.from_host(ctx, h)
+    ctx.synchronize()
+    ctx.reset_kernel_stats()
+    ctx.enable_timing(True)
+    C = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dA, dB)
+    ctx.synchronize()
+    ctx.enable_timing(False)
+    ks = ctx.kernel_stats()
+    c = C.to_host()
+    for S in (C, dA, dB):
+        S.free()
+    return ks["num_dense"]["launches"], H.Dcsc(c.m, c.n, c.jc, c.cp, c.ir, c.num)
+
+
+def test_result_oom_drops_stored_bitmaps(ctx, rmat14, monkeypatch):
+    A, exp = rmat14
+    nd, got = _dense_launches(ctx, A)
+    assert nd > 0, "scale-14 A^2 has no dense-window tasks: the fallback would not be exercised"
+    H.assert_dcsc_equal(got, exp, msg="scale-14 A^2")
+    monkeypatch.setenv("CBH_TEST_RESULT_OOM", "1")
+    nd2, got2 = _dense_launches(ctx, A)
+    assert nd2 == 0, "C's allocation failed beside the bitmaps, yet the dense kernel still ran"
+    H.assert_dcsc_equal(got2, exp, msg="scale-14 A^2 after dropping the stored bitmaps")
+
+
+def test_count_only_symbolic_matches_plan(ctx, rmat14):
+    import combblas_amd as cb
+
+    A, exp = rmat14
+    h = cb.HostDcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num)
+    dA, dB = cb.SpDCCols.from_host(ctx, h), cb.SpDCCols.from_host(ctx, h)
+    f, z, cf, cz = cb.estimateFLOPandNNZ(dA, dB, per_column=True)
+    plan = cb.SpGEMMPlan(dA, dB)
+    assert plan.info() == (f, z) and z == exp.nnz
+    assert bool((plan.col_nnz() == cz).all().item())
+    cz = cz.cpu().numpy()  # per nonzero column of B; C drops the empty product columns
+    assert np.array_equal(cz[cz > 0], np.diff(exp.cp))
+    plan.close()
+    dA.free()
+    dB.free()
+
+
+def test_phase_consumer_sees_every_phase(ctx, rmat14):
+    import torch
+    import combblas_amd as cb
+
+    A, exp = rmat14
+    h = cb.HostDcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num)
+    dA, dB = cb.SpDCCols.from_host(ctx, h), cb.SpDCCols.from_host(ctx, h)
+    parts = []
+
+    def keep(phase, s0, s1, C):
+        parts.append((phase, s0, s1, C.clone()))
+
+    budget = 12 * exp.nnz // 7  # ~7 phases of 12-byte entries
+    try:
+        _consumer_checks(ctx, cb, A, exp, dA, dB, parts, keep, budget)
+    finally:
+        ctx.set_phase_budget(0)  # the session context's default (half of free HBM)
+    torch.cuda.synchronize()
+    dA.free()
+    dB.free()
+
+
+def _consumer_checks(ctx, cb, A, exp, dA, dB, parts, keep, budget):
+    st = cb.PhasedSpGEMM(cb.PlusTimesSRing, dA, dB, checksum=True, budget_bytes=budget, on_phase=keep)
+    assert st["phases"] == len(parts) >= 5, (st["phases"], len(parts))
+    assert [p[0] for p in parts] == list(range(len(parts)))
+    assert parts[0][1] == 0 and parts[-1][2] == dB.nzc
+    assert all(parts[i][2] == parts[i + 1][1] for i in range(len(parts) - 1))
+    # concatenated views = the single-call product (empty columns of a view are dropped here)
+    rows, vals, cols = [], [], []
+    for _, _, _, C in parts:
+        cp, jc, ir, num = (t.cpu().numpy() for t in C.tensors())
+        counts = np.diff(cp)
+        cols.append(np.repeat(jc, counts))
+        rows.append(ir[:cp[-1]])
+        vals.append(num[:cp[-1]])
+        C.free()
+    got = H.Dcsc.from_coo(A.m, A.n, np.concatenate(rows), np.concatenate(cols), np.concatenate(vals))
+    H.assert_dcsc_equal(got, exp, msg="concatenated phase views")
+    assert (st["value_sum"], st["digest"]) == H.digest(exp)
+
+    class Boom(RuntimeError):
+        pass
+
+    def explode(phase, s0, s1, C):
+        if phase == 2:
+            raise Boom("consumer failure in phase 2")
+
+    with pytest.raises(Boom):
+        cb.PhasedSpGEMM(cb.PlusTimesSRing, dA, dB, budget_bytes=budget, on_phase=explode)
+    # the context is usable afterwards
+    st2 = cb.PhasedSpGEMM(cb.PlusTimesSRing, dA, dB, checksum=True, budget_bytes=budget)
+    assert (st2["value_sum"], st2["digest"]) == H.digest(exp)

@@ -55,12 +55,17 @@ def test_hash_commit_queue_only_overflow(ctx, oracle, nentries, dtype):
     A, B = _queue_overflow_operands(nentries, dtype, 7 + nentries)
     dA = cb.SpDCCols.from_host(ctx, cb.HostDcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num))
     dB = cb.SpDCCols.from_host(ctx, cb.HostDcsc(B.m, B.n, B.jc, B.cp, B.ir, B.num))
+    ctx.take_retries()  # reset the device retry counter
     C = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dA, dB)
+    retries = ctx.take_retries()
     h = C.to_host()
     got = H.Dcsc(h.m, h.n, h.jc, h.cp, h.ir, h.num)
     exp = oracle.spgemm(A, B, "plus_times", "hybrid")
     assert exp.nnz == 4101
     H.assert_dcsc_equal(got, exp, msg=f"queue-only overflow, {nentries} B entries, {np.dtype(dtype).name}")
+    # the retry path fired: the first sub-tile (4100 occupied slots > the 4096-entry queue) was
+    # redone with half its rows
+    assert retries >= 1, "the commit-queue overflow did not trigger a sub-tile retry"
     for S in (C, dA, dB):
         S.free()
 
