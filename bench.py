@@ -35,14 +35,13 @@ METRIC = "semiring GFLOP/s for R-MAT A² SpGEMM at 1/2/4/8 GPUs; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
 # the task kernels of one product (bench kernel kinds -> rocprof names); the roofline line reports
 # the one with the most time per step
-KERNELS = {"num_large": "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 8, 1, false>",
+KERNELS = {"num_large": "cbh::task_kernel<cbh::PlusTimesD<double>, 2048, 512, 512, 4, 1, false>",
            "num_dense": "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 8, 2, false>",
            "sym_large": "cbh::task_kernel<cbh::PlusTimesD<long>, 8192, 512, 512, 16, 0, false>"}
 # every task-kernel class of the f64 PlusTimes product (the application lines pick their dominant one)
 ALL_KERNELS = dict(KERNELS, **{
     "num_mid": "cbh::task_kernel<cbh::PlusTimesD<double>, 2048, 256, 256, 4, 1, false>",
-    # one task per wave (wave_kernel.h); numeric tasks a wave table rejects rerun on
-    # task_kernel<PlusTimesD<double>, 512, 128, 256, 4, 1> inside the same timed launch
+    # one task per wave (wave_kernel.h): per-wave key hash tables sized so that they never fill
     "num_small": "cbh::wave_kernel<cbh::PlusTimesD<double>, 512, 4, 4, 1>",
     "sym_mid": "cbh::task_kernel<cbh::PlusTimesD<long>, 4096, 256, 256, 4, 0, false>",
     "sym_small": "cbh::wave_kernel<cbh::PlusTimesD<long>, 2048, 4, 4, 0>"})

@@ -76,8 +76,67 @@ def reference_baseline(A, flops, stride):
                       f"{d['nnz_after_prune']} kept): median of {d['reps']} after 1 warm-up = {d['median_s']:.3f} s"}
 
 
+def cpp_line(args):
+    """config C5 through the C++ driver HipMCL calls: oracle/_ref/mclbench_harness runs the
+    reference-API MemEfficientSpGEMM on SpParMat<SpDCColsDev> (include/combblas_hip/ParFriendsDev.h,
+    the overload Applications/MCL.cpp:574-577 resolves to), checks sampled columns against the
+    reference's stock driver and times the stock driver on a column sample (the CPU baseline)"""
+    import subprocess
+
+    from combblas_amd import _lib
+    from bench import kernel_roofline
+
+    harness = os.path.join(HERE, "oracle", "_ref", "mclbench_harness")
+    if not os.path.exists(harness):
+        sys.exit("oracle/_ref/mclbench_harness is missing: run __graft_entry__.build() where the reference exists")
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    env = dict(os.environ, OMP_NUM_THREADS=str(cores), LD_LIBRARY_PATH="/usr/lib/x86_64-linux-gnu:/opt/conda/lib")
+    cmd = [harness, str(args.log2n), str(args.deg), str(args.steps), str(args.phases), str(args.check_cols),
+           str(args.cpu_stride)]
+    r = subprocess.run(cmd, env=env, cwd="/tmp", capture_output=True, text=True, timeout=1100)
+    line = [l for l in r.stdout.splitlines() if l.startswith("BENCHC5CPP ")]
+    if not line:
+        sys.exit(f"harness failed (rc {r.returncode}):\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}")
+    d = json.loads(line[-1][len("BENCHC5CPP "):])
+    ks = {name: {"ms": v[0], "launches": v[1], "alg_bytes": v[2]} for name, v in zip(_lib.K_NAMES, d["kernel_stats"])}
+    out = {"metric": "HipMCL expansion A^2 + MCLPruneRecoverySelect (C5): semiring GFLOP/s of the expansion",
+           "value": round(2.0 * d["flops"] / d["step_s"] / 1e9, 3), "unit": "GFLOP/s", "n_gpus": 1,
+           "steps": d["steps"], "warmup": 1, "ms_per_step": round(d["step_s"] * 1e3, 3), "higher_is_better": True,
+           "dtype": "f64",
+           "data": f"synthetic: planted-partition generated on the GPU (cbh_gen_planted_partition), column-stochastic, "
+                   f"n = 2^{args.log2n}, {args.deg} draws/col",
+           "config": {"workload": f"mcl_pp{args.log2n}_deg{args.deg}_A2_prune", "n": d["n"], "nnzA": d["nnzA"],
+                      "flops": d["flops"], "nnzC_unpruned": d["nnzC_unpruned"],
+                      "nnz_after_prune": d["nnz_after_prune"], "phases": d["phases"],
+                      "prune": {"hard": HARD, "select": SELECT, "recover": RECOVER, "pct": PCT},
+                      "driver": "C++: combblas::MemEfficientSpGEMM on SpParMat<int64_t, double, SpDCColsDev> "
+                                "(ParFriendsDev.h; StagePlans: one symbolic pass, numeric per phase)",
+                      "parallelism": "1 GPU (config C5 names 2x2x2)", "kernel_ms": {k: round(v["ms"] / d["steps"], 3)
+                                                                                   for k, v in ks.items() if v["ms"]}},
+           "roofline": kernel_roofline(ks),
+           "cpu_baseline": {"value": round(2.0 * d["cpu_flops"] / d["cpu_s"] / 1e9, 6), "unit": "GFLOP/s",
+                            "cores": int(d["cpu_threads"]) or cores, "kind": "reference",
+                            "sample": f"the reference's stock MemEfficientSpGEMM + MCLPruneRecoverySelect (OpenMP "
+                                      f"kernels, same harness, 1 rank) on B = A's {d['cpu_cols']} columns c % "
+                                      f"{d['cpu_stride']} == 0 ({d['cpu_flops']} multiplies, {d['cpu_kept']} kept): "
+                                      f"median of 3 after 1 warm-up = {d['cpu_s']:.3f} s"},
+           "check": {"sample_columns": d["check_cols"], "reference": "stock MemEfficientSpGEMM + prune on the sampled "
+                                                                       "columns (rows exact, values 1e-12 relative)",
+                     "row_mismatches": d["row_mismatches"], "value_mismatches": d["value_mismatches"],
+                     "max_rel": d["max_rel"], "ok": d["ok"]}}
+    print(json.dumps(out), flush=True)
+    if not d["ok"] or r.returncode != 0:
+        sys.exit(1)
+
+
 def main():
     p = argparse.ArgumentParser()
+    p.add_argument("--driver", choices=["python", "cpp"], default="python",
+                   help="python: the parfriends mirror; cpp: the C++ overload (oracle/_ref/mclbench_harness)")
+    p.add_argument("--gen", choices=["lib", "torch"], default="lib",
+                   help="lib: cbh_gen_planted_partition (the C++ harness's input); torch: mclgen.planted_partition_device")
+    p.add_argument("--phases", type=int, default=0, help="cpp driver: MemEfficientSpGEMM's phases (0: C's phase "
+                                                          "blocks within 0.4 of free HBM, as the Python mirror)")
     p.add_argument("--log2n", type=int, default=24)
     p.add_argument("--deg", type=int, default=100)
     p.add_argument("--steps", type=int, default=2)
@@ -87,13 +146,15 @@ def main():
     p.add_argument("--cpu-stride", type=int, default=0, help="0: about 3e8 multiplies in the CPU sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     args = p.parse_args()
+    if args.driver == "cpp":
+        return cpp_line(args)
     import torch
 
     import combblas_amd as cb
     from combblas_amd import parfriends as pf
     from combblas_amd.backend import HipBackend
     from combblas_amd.commgrid import CommGrid
-    from combblas_amd.mclgen import planted_partition, planted_partition_device
+    from combblas_amd.mclgen import planted_partition, planted_partition_device, planted_partition_lib
     from combblas_amd.spparmat import SpParMat
 
     torch.cuda.set_device(0)
@@ -106,7 +167,7 @@ def main():
         A = planted_partition(n, args.deg, 7)
         dA, dB = SpParMat.distribute(A, grid, be), SpParMat.distribute(A, grid, be)
     else:
-        gA = planted_partition_device(ctx, n, args.deg, 7)
+        gA = (planted_partition_lib if args.gen == "lib" else planted_partition_device)(ctx, n, args.deg, 7)
         dA, dB = SpParMat(gA, grid, be, n, n), SpParMat(gA.clone(), grid, be, n, n)
         A = gA.to_host()
     log(f"input: n {n}, nnz {A.nnz} ({time.perf_counter() - t0:.1f} s)")
@@ -194,7 +255,7 @@ def main():
     out = {"metric": "HipMCL expansion A^2 + MCLPruneRecoverySelect (C5): semiring GFLOP/s of the expansion",
            "value": round(2.0 * flops / dt / 1e9, 3), "unit": "GFLOP/s", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "dtype": "f64",
-           "data": f"synthetic: planted-partition ({'host numpy' if args.host_gen else 'generated on the GPU'}), "
+           "data": f"synthetic: planted-partition ({'host numpy' if args.host_gen else 'generated on the GPU: ' + args.gen}), "
                    f"column-stochastic, n = 2^{args.log2n}, {args.deg} draws/col",
            "config": {"workload": f"mcl_pp{args.log2n}_deg{args.deg}_A2_prune", "n": n, "nnzA": int(A.nnz),
                       "flops": flops, "phases": phases, "nnz_after_prune": int(kept["nnz"]),

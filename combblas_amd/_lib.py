@@ -61,6 +61,7 @@ SIGNATURES = {
     "cbh_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "cbh_ctx_trim": (ctypes.c_int, [ctypes.c_void_p]),
     "cbh_ctx_take_retries": (ctypes.c_int, [ctypes.c_void_p, c_int64_p]),
+    "cbh_hash_config": (ctypes.c_int, [c_int64_p, c_int64_p, c_int64_p]),
     "cbh_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "cbh_ctx_set_allocator": (ctypes.c_int, [ctypes.c_void_p, ALLOC_FN, FREE_FN, ctypes.c_void_p]),
     "cbh_ctx_set_phase_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
@@ -91,6 +92,11 @@ SIGNATURES = {
                                              ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_mat_download_chunks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_int64, TAKE_FN, ctypes.c_void_p]),
+    "cbh_gen_planted_partition": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64,
+                                                 ctypes.c_double, ctypes.c_double, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_mat_row_slice": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                         ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_mat_rebase_cols": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64]),
     "cbh_mat_copy_out": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "cbh_mat_free": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcombblas_hip.so")
 SOURCES = ["spgemm.hip", "rmat.cpp"]
-HEADERS = ["apps.h", "convert.h", "host_util.h"] + [os.path.join("..", "..", "include", h) for h in (
+HEADERS = ["apps.h", "blocks.h", "convert.h", "host_util.h", "mclgen.h"] + [os.path.join("..", "..", "include", h) for h in (
     "combblas_hip.h", "combblas_hip/device/semiring.h", "combblas_hip/device/block_ops.h",
     "combblas_hip/device/task_kernel.h", "combblas_hip/device/wave_kernel.h",
     "combblas_hip/device/numeric.h")]

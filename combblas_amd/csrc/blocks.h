@@ -2,6 +2,8 @@
 //
 //   column slice     SpDCCols::ColSplit piece [c0, c1) (SpDCCols.cpp:936-1012, Dcsc::ColSplit):
 //                    the slot range by two lower bounds on jc, then cp / jc rebased, ir / num copied
+//   row slice        rows [r0, r1) of every column, ids rebased (Mult_AnXBn_DoubleBuff's row halves of
+//                    B: Transpose + Split + Transpose, ParFriends.h:823-828)
 //   column concat    SpDCCols::ColConcatenate (SpDCCols.cpp:1014-1090): column ids and pointers
 //                    offset by the earlier blocks' columns / entries
 //   MCL masks        MCLPruneRecoverySelect's per-column decisions (ParFriends.h:196-330): which
@@ -34,6 +36,39 @@ __global__ void col_range_kernel(const int64_t* __restrict__ jc, const int64_t* 
   out[1] = s[1];
   out[2] = cp[s[0]];
   out[3] = cp[s[1]];
+}
+
+// row slice [r0, r1) of every column (rows sorted): first and count of its entries in the range
+__global__ void row_range_kernel(const int64_t* __restrict__ cp, const int32_t* __restrict__ ir, int64_t nzc, int32_t r0,
+                                 int32_t r1, int64_t* __restrict__ first, int64_t* __restrict__ cnt) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nzc) return;
+  int64_t b[2];
+  const int32_t key[2] = {r0, r1};
+  for (int t = 0; t < 2; ++t) {
+    int64_t lo = cp[c], hi = cp[c + 1];
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (ir[mid] < key[t]) lo = mid + 1;
+      else hi = mid;
+    }
+    b[t] = lo;
+  }
+  first[c] = b[0];
+  cnt[c] = b[1] - b[0];
+}
+// the kept columns' entries (wave per column): rows rebased by -r0, values copied (vb bytes each)
+__global__ __launch_bounds__(256) void row_slice_copy_kernel(const int64_t* __restrict__ first,
+                                                             const int64_t* __restrict__ cnt,
+                                                             const int64_t* __restrict__ off, const int32_t* __restrict__ ir,
+                                                             const char* __restrict__ num, int64_t nzc, int32_t r0,
+                                                             int64_t vb, int32_t* __restrict__ oir, char* __restrict__ onum) {
+  const int lane = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= nzc) return;
+  const int64_t f = first[c], k = cnt[c], o = off[c];
+  for (int64_t i = lane; i < k; i += 64) oir[o + i] = ir[f + i] - r0;
+  for (int64_t i = lane; i < k * vb; i += 64) onum[o * vb + i] = num[f * vb + i];
 }
 
 __global__ void fill_f64_kernel(double* __restrict__ p, int64_t n, double v) {

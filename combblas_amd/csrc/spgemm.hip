@@ -27,6 +27,7 @@
 #include "apps.h"
 #include "convert.h"
 #include "blocks.h"
+#include "mclgen.h"
 
 using namespace cbh;
 
@@ -511,14 +512,7 @@ struct BinLists {
 // indexed like `work`.
 // Inside each bin, tasks launch in row-block order (rowkey), so the tasks in flight at a time
 // read one slice of A (98.3 -> 99.0 GFLOP/s at scale 22: the dense kernel's over-fetch hits L2
-// more often). CBH_ROWORDER=0 restores the unsorted bin order.
-static bool row_order_enabled() {
-  static int v = [] {
-    const char* e = std::getenv("CBH_ROWORDER");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v != 0;
-}
+// more often).
 static int make_bins(cbh_ctx* ctx, Scratch& S, const int64_t* work, int64_t n, int64_t col0, int32_t* ids,
                      BinLists* out, BinCaps caps, const int64_t* units = nullptr, const int32_t* rowkey = nullptr) {
   constexpr int NS = kGroups;
@@ -540,7 +534,7 @@ static int make_bins(cbh_ctx* ctx, Scratch& S, const int64_t* work, int64_t n, i
     off[b] = run;
     run += h[b];
   }
-  if (rowkey && row_order_enabled() && n > 0) {
+  if (rowkey && n > 0) {
     uint32_t *kin, *kout;
     int32_t* vin;
     CBH_TRY(S.get(&kin, n));
@@ -644,29 +638,15 @@ static int check_err(cbh_ctx* ctx) {
 // with about kTaskFlops products each (S_j = 1 for light columns). Tasks of a column are
 // consecutive and in row order, so the exclusive scan of the per-task counts gives every task
 // its output offset and C's column pointers are the offsets of each column's first task.
-constexpr int64_t kTaskFlopsDefault = 131072;  // (65536 / 262144: 121.8 / 124.9 vs 124.8 GFLOP/s at scale 22)
-static int64_t task_flops() {
-  static int64_t v = [] {
-    const char* e = std::getenv("CBH_TASK_FLOPS");
-    const long long x = e ? std::atoll(e) : 0;
-    return x > 0 ? (int64_t)x : kTaskFlopsDefault;
-  }();
-  return v;
-}
+constexpr int64_t kTaskFlops = 131072;  // (65536 / 262144: 121.8 / 124.9 vs 124.8 GFLOP/s at scale 22)
 
 // Row blocks: C's rows are cut into blocks of RB rows (kRowBlocks blocks); interior task
 // boundaries of a split column sit on block boundaries, where the row-block table of A gives
 // every hub entry's position directly (hub_fill_kernel); short columns bisect.
 constexpr int64_t kRowBlocks = 256;  // (128 / 192 / 384: 130.9 / 131.3 / 131.4 vs 132.2 GFLOP/s, aligned sub-tiles)
 // rows per block: a multiple of 32 from 32 rows up, so that block boundaries are stored-bitmap word boundaries
-// (CBH_ROW_BLOCKS overrides the block count, for measurements)
 static int32_t row_block(int64_t m) {
-  static int64_t nb = [] {
-    const char* e = std::getenv("CBH_ROW_BLOCKS");
-    const long long x = e ? std::atoll(e) : 0;
-    return x > 0 ? (int64_t)x : kRowBlocks;
-  }();
-  const int64_t rb = std::max<int64_t>(1, (m + nb - 1) / nb);
+  const int64_t rb = std::max<int64_t>(1, (m + kRowBlocks - 1) / kRowBlocks);
   return (int32_t)(rb >= 32 ? (rb + 31) & ~int64_t(31) : rb);  // small matrices keep fine blocks
 }
 
@@ -721,15 +701,7 @@ __global__ __launch_bounds__(256) void task_fill_kernel(const int64_t* __restric
 // RB) and the stop search of long segments (task_kernel.h stop_search) read it -- one 8-B load
 // gives a cursor and its row; short columns bisect instead. At scale 22: 288 K hub columns (82 %
 // of A's entries), 593 MB, instead of a table over all 4.2 M columns.
-constexpr int64_t kHubMin = 32;
-static int64_t hub_min() {  // CBH_HUB_MIN overrides, for measurements
-  static int64_t v = [] {
-    const char* e = std::getenv("CBH_HUB_MIN");
-    const long long x = e ? std::atoll(e) : 0;
-    return x > 0 ? (int64_t)x : kHubMin;
-  }();
-  return v;
-}
+constexpr int64_t kHubMin = 32;  // (8 / 16 / 64: 132.5 / 131.5 / 130.6 vs 132.2 GFLOP/s at scale 22)
 __global__ void hub_flag_kernel(const int64_t* __restrict__ Acp, int64_t ncol, int64_t minlen, int64_t* __restrict__ flag) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k < ncol) flag[k] = (Acp[k + 1] - Acp[k]) >= minlen ? 1 : 0;
@@ -845,14 +817,6 @@ __global__ void dense_split_kernel(const int64_t* __restrict__ tcnt, const int32
   wd[t] = d ? w : 0;
   wh[t] = d ? 0 : (w > 0 && w <= smallcap && flops && flops[t] > wavemax ? smallcap + 1 : w);
 }
-// CBH_DENSE=0 keeps every numeric task on the hash kernels (A/B switch)
-static bool kDenseEnabled() {
-  static int v = [] {
-    const char* e = std::getenv("CBH_DENSE");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v != 0;
-}
 // share of the free HBM the phase workspace of cbh_spgemm_phased takes (CBH_PHASE_FRAC)
 static double phase_frac() {
   static double v = [] {
@@ -861,24 +825,9 @@ static double phase_frac() {
   }();
   return v;
 }
-// dense split rule (dense_subtiles): dense sub-tiles at most CBH_DRATIO4/4 of the hash ones (A/B switch)
-static int64_t dratio4() {
-  static int64_t v = [] {
-    const char* e = std::getenv("CBH_DRATIO4");
-    return e ? (int64_t)std::atoi(e) : (int64_t)kDRatio4;
-  }();
-  return v;
-}
-// compression ratio (quarters) a candidate's flops are divided by before the dense test
-// (CBH_BMP_CR4, for measurements)
-static int64_t bmp_cr4() {
-  static int64_t v = [] {
-    const char* e = std::getenv("CBH_BMP_CR4");
-    const int x = e ? std::atoi(e) : 0;
-    return x > 0 ? (int64_t)x : (int64_t)4;
-  }();
-  return v;
-}
+// compression ratio (quarters) a dense candidate's flops are divided by before the dense test
+// (5/4, 6/4, 8/4 and 12/4 measured flat or slower than 4/4)
+constexpr int64_t kBmpCr4 = 4;
 static double bmp_frac() {
   static double v = [] {
     const char* e = std::getenv("CBH_BMP_FRAC");
@@ -1051,7 +1000,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   CBH_TRY(sum_i64(ctx, S, P.flop, n, d_tot));
   P.RB = row_block(A->m);
   hipLaunchKernelGGL(task_count_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, P.flop, P.rmin, P.rmax, n,
-                     task_flops(), P.RB, scnt);
+                     kTaskFlops, P.RB, scnt);
   CBH_HIP(ctx, hipMemsetAsync(scnt + n, 0, sizeof(int64_t), ctx->stream));
   CBH_TRY(exclusive_scan_i64(ctx, S, scnt, P.tstart, n + 1));
   int64_t h[2];
@@ -1082,7 +1031,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
     CBH_TRY(S.get(&hflag, A->n + 1));
     CBH_TRY(S.get(&hpos, A->n + 1));
     CBH_TRY(S.get(&P.hidx, std::max<int64_t>(A->n, 1)));
-    hipLaunchKernelGGL(hub_flag_kernel, dim3(blocks_for(A->n, 256)), dim3(256), 0, ctx->stream, P.Adense, A->n, hub_min(),
+    hipLaunchKernelGGL(hub_flag_kernel, dim3(blocks_for(A->n, 256)), dim3(256), 0, ctx->stream, P.Adense, A->n, kHubMin,
                        hflag);
     CBH_HIP(ctx, hipMemsetAsync(hflag + A->n, 0, sizeof(int64_t), ctx->stream));
     CBH_TRY(exclusive_scan_i64(ctx, S, hflag, hpos, A->n + 1));
@@ -1131,8 +1080,8 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
     CBH_TRY(S.get(&P.boff, nt + 1));
     CBH_HIP(ctx, hipMemsetAsync(cw, 0, sizeof(unsigned long long) * kBmpClasses, ctx->stream));
     hipLaunchKernelGGL(bmp_count_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.twork, P.tlo, P.thi,
-                       P.ntasks, (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSymMidCap, dratio4(),
-                       bmp_cr4(), 0, bw, cw);
+                       P.ntasks, kSplitHashT, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSymMidCap, (int64_t)kDRatio4,
+                       kBmpCr4, 0, bw, cw);
     CBH_HIP(ctx, hipGetLastError());
     unsigned long long hc[kBmpClasses];
     CBH_HIP(ctx, hipMemcpyAsync(hc, cw, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream));
@@ -1147,11 +1096,11 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
     while (min_class > 0 && words + (double)hc[min_class - 1] <= cap_words) words += (double)hc[--min_class];
     if (min_class > 0 && words > 0)  // drop the classes that did not fit
       hipLaunchKernelGGL(bmp_count_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.twork, P.tlo, P.thi,
-                         P.ntasks, (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSymMidCap, dratio4(),
-                         bmp_cr4(), min_class, bw, nullptr);
+                         P.ntasks, kSplitHashT, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSymMidCap, (int64_t)kDRatio4,
+                         kBmpCr4, min_class, bw, nullptr);
     CBH_HIP(ctx, hipMemsetAsync(bw + P.ntasks, 0, sizeof(int64_t), ctx->stream));
     CBH_TRY(exclusive_scan_i64(ctx, S, bw, P.boff, P.ntasks + 1));
-    if (words > 0 && kDenseEnabled()) CBH_TRY(S.get(&P.bmp, (size_t)words));
+    if (words > 0) CBH_TRY(S.get(&P.bmp, (size_t)words));
     if (diag_enabled()) {
       double all = 0;
       for (int i = 0; i < kBmpClasses; ++i) all += (double)hc[i];
@@ -1207,9 +1156,9 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
   CBH_TRY(S.get(&wd, nt));
   CBH_TRY(S.get(&wh, nt));
   hipLaunchKernelGGL(dense_split_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.tcnt + t0, P.tlo + t0,
-                     P.thi + t0, P.bmp ? P.boff + t0 : nullptr, P.twork + t0, nt, (int64_t)TNumLarge::T, (int64_t)CD::CAPD,
-                     (int64_t)CD::NWB, dratio4(), kSmallCap, kWaveProducts,
-                     kDenseEnabled() ? 1 : 0, wd, wh);
+                     P.thi + t0, P.bmp ? P.boff + t0 : nullptr, P.twork + t0, nt, kSplitHashT, (int64_t)CD::CAPD,
+                     (int64_t)CD::NWB, (int64_t)kDRatio4, kSmallCap, kWaveProducts,
+                     1, wd, wh);
   CBH_HIP(ctx, hipGetLastError());
   BinLists bd, bl;
   CBH_TRY(make_bins(ctx, S, wd, nt, t0, P.order, &bd, BinCaps{kSmallCap, kSmallCap}, P.tunits + t0, P.trk + t0));
@@ -1460,6 +1409,13 @@ int cbh_ctx_trim(cbh_ctx* ctx) {
 }
 
 const char* cbh_last_error(cbh_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int cbh_hash_config(int64_t* table_slots, int64_t* threads, int64_t* per_thread) {
+  if (table_slots) *table_slots = TNumHash::T;
+  if (threads) *threads = TNumHash::BS;
+  if (per_thread) *per_thread = TNumHash::U;
+  return CBH_OK;
+}
 
 int cbh_ctx_take_retries(cbh_ctx* ctx, int64_t* subtile_retries) {
   if (!ctx || !subtile_retries) return CBH_E_ARG;
@@ -2072,8 +2028,8 @@ int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t
   CBH_TRY(p->S.get(&wh, nt));
   hipLaunchKernelGGL(dense_split_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.tcnt, P.tlo, P.thi,
                      P.bmp ? P.boff : nullptr, P.twork, nt,
-                     (int64_t)TNumLarge::T, (int64_t)CD::CAPD, (int64_t)CD::NWB, dratio4(), kSmallCap, kWaveProducts,
-                     (kDenseEnabled() && !(flags & CBH_PLAN_NO_DENSE)) ? 1 : 0, wd, wh);
+                     kSplitHashT, (int64_t)CD::CAPD, (int64_t)CD::NWB, (int64_t)kDRatio4, kSmallCap, kWaveProducts,
+                     !(flags & CBH_PLAN_NO_DENSE) ? 1 : 0, wd, wh);
   CBH_HIP(ctx, hipGetLastError());
   BinLists bd, bl;
   CBH_TRY(make_bins(ctx, p->S, wd, nt, 0, P.order, &bd, BinCaps{kSmallCap, kSmallCap}, nullptr, P.trk));
@@ -2291,7 +2247,7 @@ int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* p
     hipLaunchKernelGGL(iota_scaled_kernel, dim3(blocks_for(ncols + 1, 256)), dim3(256), 0, ctx->stream, bcp, ncols + 1,
                        (int64_t)nlists);
     hipLaunchKernelGGL(task_count_kernel, dim3(blocks_for(ncols, 256)), dim3(256), 0, ctx->stream, work, rmin, rmax,
-                       ncols, task_flops(), RB, scnt);
+                       ncols, kTaskFlops, RB, scnt);
     CBH_HIP(ctx, hipMemsetAsync(scnt + ncols, 0, sizeof(int64_t), ctx->stream));
     CBH_TRY(exclusive_scan_i64(ctx, S, scnt, tstart, ncols + 1));
     int64_t ntasks = 0;
@@ -2830,6 +2786,65 @@ int cbh_mat_col_slice(cbh_ctx* ctx, const cbh_mat* M, int64_t c0, int64_t c1, cb
   return CBH_OK;
 }
 
+int cbh_mat_row_slice(cbh_ctx* ctx, const cbh_mat* M, int64_t r0, int64_t r1, cbh_mat** out) {
+  if (!ctx || !M || !out) return fail(ctx, CBH_E_ARG, "null argument");
+  if (r0 < 0 || r1 < r0 || r1 > M->m) return fail(ctx, CBH_E_ARG, "row range outside the block");
+  *out = nullptr;
+  if (M->nzc == 0) {
+    CBH_TRY(new_mat(ctx, r1 - r0, M->n, 0, 0, M->dtype, out, M->vbytes));
+    CBH_HIP(ctx, hipMemsetAsync((*out)->cp, 0, sizeof(int64_t), ctx->stream));
+    return CBH_OK;
+  }
+  Scratch S(ctx);
+  const int64_t nz = M->nzc;
+  int64_t *first, *cnt, *off, *flag, *pos;
+  CBH_TRY(S.get(&first, nz + 1));
+  CBH_TRY(S.get(&cnt, nz + 1));
+  CBH_TRY(S.get(&off, nz + 1));
+  CBH_TRY(S.get(&flag, nz + 1));
+  CBH_TRY(S.get(&pos, nz + 1));
+  hipLaunchKernelGGL(row_range_kernel, dim3(blocks_for(nz, 256)), dim3(256), 0, ctx->stream, M->cp, M->ir, nz,
+                     (int32_t)r0, (int32_t)r1, first, cnt);
+  CBH_HIP(ctx, hipMemsetAsync(cnt + nz, 0, sizeof(int64_t), ctx->stream));
+  CBH_TRY(exclusive_scan_i64(ctx, S, cnt, off, nz + 1));
+  hipLaunchKernelGGL(nz_flag_kernel, dim3(blocks_for(nz + 1, 256)), dim3(256), 0, ctx->stream, cnt, nz + 1, flag);
+  CBH_TRY(exclusive_scan_i64(ctx, S, flag, pos, nz + 1));
+  int64_t h[2];
+  CBH_HIP(ctx, hipMemcpyAsync(&h[0], off + nz, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipMemcpyAsync(&h[1], pos + nz, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  cbh_mat* C;
+  CBH_TRY(new_mat(ctx, r1 - r0, M->n, h[0], h[1], M->dtype, &C, M->vbytes));
+  hipLaunchKernelGGL(row_slice_copy_kernel, dim3(blocks_for(nz, 4)), dim3(256), 0, ctx->stream, first, cnt, off, M->ir,
+                     static_cast<const char*>(M->num), nz, (int32_t)r0, M->vbytes, C->ir, static_cast<char*>(C->num));
+  hipLaunchKernelGGL(compact_cols_kernel, dim3(blocks_for(nz, 256)), dim3(256), 0, ctx->stream, cnt, pos, M->jc, off, nz,
+                     C->jc, C->cp);
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess && h[1] == 0) (void)hipMemsetAsync(C->cp, 0, sizeof(int64_t), ctx->stream);
+  if (e != hipSuccess) {
+    cbh_mat_free(ctx, C);
+    return fail(ctx, CBH_E_HIP, std::string("row slice: ") + hipGetErrorString(e));
+  }
+  *out = C;
+  return CBH_OK;
+}
+
+int cbh_mat_rebase_cols(cbh_ctx* ctx, cbh_mat* M, int64_t c0, int64_t n) {
+  if (!ctx || !M || c0 < 0 || n < 0) return fail(ctx, CBH_E_ARG, "bad rebase arguments");
+  if (M->nzc > 0) {
+    int64_t h[2];
+    CBH_HIP(ctx, hipMemcpyAsync(&h[0], M->jc, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(&h[1], M->jc + M->nzc - 1, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (h[0] < c0 || h[1] >= c0 + n) return fail(ctx, CBH_E_ARG, "columns outside [c0, c0 + n)");
+    hipLaunchKernelGGL(add_const_i64_kernel, dim3(blocks_for(M->nzc, 256)), dim3(256), 0, ctx->stream, M->jc, M->nzc, -c0,
+                       M->jc);
+    CBH_HIP(ctx, hipGetLastError());
+  }
+  M->n = n;
+  return CBH_OK;
+}
+
 int cbh_mat_col_concat(cbh_ctx* ctx, int k, const cbh_mat* const* parts, cbh_mat** out) {
   if (!ctx || !out || k < 1 || !parts) return fail(ctx, CBH_E_ARG, "bad concat arguments");
   *out = nullptr;
@@ -3050,6 +3065,88 @@ extern "C" int cbh_tuples_to_dcsc(cbh_ctx* ctx, int64_t m, int64_t n, int64_t nn
     cbh_mat_free(ctx, M);
     return rc;
   }
+  *out = M;
+  return CBH_OK;
+}
+
+// config C5's input (mclgen.h): planted partition, symmetric, unit loops, column-stochastic, f64
+extern "C" int cbh_gen_planted_partition(cbh_ctx* ctx, int64_t n, int64_t avg_deg, uint64_t seed, double p_in,
+                                         double alpha, cbh_mat** out) {
+  if (!ctx || !out || n < 2 || n > INT32_MAX || avg_deg < 2 || !(alpha > 0) || !(p_in >= 0 && p_in <= 1))
+    return fail(ctx, CBH_E_ARG, "bad planted-partition arguments");
+  *out = nullptr;
+  const int64_t half = avg_deg / 2, draws = n * half;
+  if (draws > INT32_MAX) return fail(ctx, CBH_E_ARG, "n * avg_deg / 2 must stay below 2^31 draws");
+  std::vector<int64_t> start{0};  // power-law cluster sizes 2 + floor(6 * Lomax(alpha)), summing to n
+  for (uint64_t i = 0; start.back() < n; ++i) {
+    const double lomax = std::pow(1.0 - gen_u01(seed, 0, i), -1.0 / alpha) - 1.0;
+    const double sz = std::min((double)n, 2.0 + std::floor(6.0 * lomax));
+    start.push_back(std::min<int64_t>(n, start.back() + (int64_t)sz));
+  }
+  const int64_t ncl = (int64_t)start.size() - 1;
+  Scratch S(ctx);
+  int64_t *dstart, *head, *pos;
+  int32_t *cl, *perm, *pval;
+  uint64_t *pkey, *pkey2, *key, *key2;
+  CBH_TRY(S.get(&dstart, ncl + 1));
+  CBH_TRY(S.get(&cl, n));
+  CBH_TRY(S.get(&perm, n));
+  CBH_TRY(S.get(&pval, n));
+  CBH_TRY(S.get(&pkey, n));
+  CBH_TRY(S.get(&pkey2, n));
+  CBH_HIP(ctx, hipMemcpyAsync(dstart, start.data(), sizeof(int64_t) * (ncl + 1), hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(gen_cluster_of_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, dstart, ncl, n, cl);
+  hipLaunchKernelGGL(gen_perm_keys_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, seed, n, pkey, pval);
+  CBH_HIP(ctx, hipGetLastError());
+  size_t tmp = 0;
+  CBH_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, pkey, pkey2, pval, perm, (int)n, 0, 64, ctx->stream));
+  char* t;
+  CBH_TRY(S.get(&t, tmp));
+  CBH_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(t, tmp, pkey, pkey2, pval, perm, (int)n, 0, 64, ctx->stream));
+  CBH_TRY(S.get(&key, draws));
+  CBH_TRY(S.get(&key2, draws));
+  hipLaunchKernelGGL(gen_edge_keys_kernel, dim3(blocks_for(draws, 256)), dim3(256), 0, ctx->stream, seed, (int64_t)0,
+                     draws, half, n, p_in, cl, dstart, perm, key);
+  CBH_HIP(ctx, hipGetLastError());
+  tmp = 0;
+  CBH_HIP(ctx, hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, key, key2, (int)draws, 0, 64, ctx->stream));
+  char* t2;
+  CBH_TRY(S.get(&t2, tmp));
+  CBH_HIP(ctx, hipcub::DeviceRadixSort::SortKeys(t2, tmp, key, key2, (int)draws, 0, 64, ctx->stream));
+  S.drop(t2);
+  S.drop(key);
+  CBH_TRY(S.get(&head, draws + 1));
+  CBH_TRY(S.get(&pos, draws + 1));
+  hipLaunchKernelGGL(gen_head_kernel, dim3(blocks_for(draws, 256)), dim3(256), 0, ctx->stream, key2, draws, head);
+  CBH_HIP(ctx, hipMemsetAsync(head + draws, 0, sizeof(int64_t), ctx->stream));
+  CBH_TRY(exclusive_scan_i64(ctx, S, head, pos, draws + 1));
+  int64_t npairs = 0;
+  CBH_HIP(ctx, hipMemcpyAsync(&npairs, pos + draws, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  const int64_t total = 2 * npairs + n;
+  if (total > INT32_MAX) return fail(ctx, CBH_E_ARG, "planted partition above 2^31 entries");
+  int32_t* rows;
+  int64_t* cols;
+  double* vals;
+  CBH_TRY(S.get(&rows, total));
+  CBH_TRY(S.get(&cols, total));
+  CBH_TRY(S.get(&vals, total));
+  hipLaunchKernelGGL(gen_tuples_kernel, dim3(blocks_for(std::max(draws, n), 256)), dim3(256), 0, ctx->stream, seed, key2,
+                     head, pos, draws, npairs, n, rows, cols, vals);
+  CBH_HIP(ctx, hipGetLastError());
+  S.drop(key2);
+  S.drop(head);
+  S.drop(pos);
+  cbh_mat* M = nullptr;
+  CBH_TRY(cbh_tuples_to_dcsc(ctx, n, n, total, rows, cols, vals, CBH_F64, 0, &M));
+  hipLaunchKernelGGL(gen_col_stochastic_kernel, dim3(blocks_for(M->nzc, 4)), dim3(256), 0, ctx->stream, M->cp, M->nzc,
+                     reinterpret_cast<double*>(M->num));
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    cbh_mat_free(ctx, M);
+    return fail(ctx, CBH_E_HIP, std::string("gen_col_stochastic: ") + hipGetErrorString(e));
+  }
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   *out = M;
   return CBH_OK;
 }

@@ -128,3 +128,18 @@ def planted_partition_device(ctx, n: int, avg_deg: int = 100, seed: int = 7, p_i
     del rows, cols, vals
     torch.cuda.synchronize(ctx.device)
     return M
+
+
+def planted_partition_lib(ctx, n: int, avg_deg: int = 100, seed: int = 7, p_in: float = 0.9, alpha: float = 1.6):
+    """the same recipe generated by the library (cbh_gen_planted_partition, csrc/mclgen.h): counter-based
+    draws, so the matrix depends on the arguments only -- the input the C++ C5 harness
+    (tests/dropin/mclbench_harness.cpp) builds too. Returns a device SpDCCols (f64)."""
+    import ctypes
+
+    from ._lib import check, lib
+    from .spdccols import SpDCCols
+
+    h = ctypes.c_void_p()
+    check(lib().cbh_gen_planted_partition(ctx.h, int(n), int(avg_deg), int(seed), float(p_in), float(alpha),
+                                          ctypes.byref(h)), ctx.h)
+    return SpDCCols(ctx, h)

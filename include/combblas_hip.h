@@ -97,6 +97,9 @@ const char* cbh_last_error(cbh_ctx* ctx);
 /* Sub-tiles the task kernels retried with half the row range (table overflow, commit queue) since
  * the last call; resets the counter (diagnostics and tests). */
 int cbh_ctx_take_retries(cbh_ctx* ctx, int64_t* subtile_retries);
+/* The large numeric hash kernel's configuration: table slots T (plus 64 guard slots), threads per
+ * workgroup and products per thread per window (the commit queue holds threads * per_thread). */
+int cbh_hash_config(int64_t* table_slots, int64_t* threads, int64_t* per_thread);
 /* Route every device allocation of this context through caller callbacks (e.g. the torch
  * caching allocator), stream-ordered on `stream`. NULL alloc restores the built-in block cache.        */
 typedef void* (*cbh_alloc_fn)(void* user, int64_t bytes, void* stream);
@@ -330,6 +333,12 @@ int cbh_mcl_prune_recovery_select(cbh_ctx* ctx, const cbh_mat* A, double hardThr
  *                       rows = the largest m, columns offset by the earlier blocks' n            */
 int cbh_mat_col_slice(cbh_ctx* ctx, const cbh_mat* M, int64_t c0, int64_t c1, cbh_mat** out);
 int cbh_mat_col_concat(cbh_ctx* ctx, int k, const cbh_mat* const* parts, cbh_mat** out);
+/* Rows [r0, r1) of the block as an (r1 - r0) x n block, row ids rebased, empty columns dropped
+ * (Mult_AnXBn_DoubleBuff's row halves of B). */
+int cbh_mat_row_slice(cbh_ctx* ctx, const cbh_mat* M, int64_t r0, int64_t r1, cbh_mat** out);
+/* In place: the block's columns [c0, c0 + n) become columns [0, n) of an m x n block (a phase
+ * piece of a plan's slot product, which keeps B's column ids, rebased like a ColSplit piece). */
+int cbh_mat_rebase_cols(cbh_ctx* ctx, cbh_mat* M, int64_t c0, int64_t n);
 
 /* ---------------------------------------------------------------- format conversions (device)
  *   cbh_tuples_to_dcsc  device COO (rows, cols, vals; any order, duplicates allowed) -> a DCSC block:
@@ -343,6 +352,14 @@ int cbh_mat_col_concat(cbh_ctx* ctx, int k, const cbh_mat* const* parts, cbh_mat
 int cbh_tuples_to_dcsc(cbh_ctx* ctx, int64_t m, int64_t n, int64_t nnz, const int32_t* rows, const int64_t* cols,
                        const void* vals, cbh_dtype dtype, uint32_t flags, cbh_mat** out);
 int cbh_dcsc_to_tuples(cbh_ctx* ctx, const cbh_mat* M, int32_t* rows, int64_t* cols, void* vals);
+
+/* Config C5's input on the device (combblas_amd/csrc/mclgen.h): a planted-partition graph of n
+ * vertices, power-law cluster sizes (2 + floor(6 * Lomax(alpha))), avg_deg / 2 draws per vertex
+ * (a fraction p_in inside the vertex's cluster), symmetric, uniform (0, 1] weights, unit loops,
+ * column-stochastic (MakeColStochastic, MCL.cpp:390-396); f64. Counter-based draws: the matrix
+ * depends on the arguments only. n * avg_deg / 2 < 2^31.                                       */
+int cbh_gen_planted_partition(cbh_ctx* ctx, int64_t n, int64_t avg_deg, uint64_t seed, double p_in, double alpha,
+                              cbh_mat** out);
 
 /* ---------------------------------------------------------------- inputs (host side) */
 int cbh_rmat_edges(int scale, uint64_t userseed, int64_t start_edge, int64_t end_edge, int64_t* src,

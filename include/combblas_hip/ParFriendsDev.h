@@ -7,17 +7,20 @@
 //                                                   statistics and Kselect histograms summed over
 //                                                   the processor column with ncclAllReduce
 //   EstPerProcessNnzSUMMA    ParFriends.h:1243-1340 stage broadcasts + device symbolic pass
-//   MemEfficientSpGEMM       ParFriends.h:449-730   B's block cut in `phases` column pieces
-//                                                   (ColSplit), per phase the device SUMMA
-//                                                   (summa_blocks) and MCLPruneRecoverySelect, the
-//                                                   pruned pieces concatenated (ColConcatenate)
+//   MemEfficientSpGEMM       ParFriends.h:449-730   the stage blocks broadcast once and every stage
+//                                                   pair planned once (StagePlans: one symbolic
+//                                                   pass, which also feeds the memory model); per
+//                                                   phase the numeric pass of B's ColSplit columns,
+//                                                   the stage partials merged, MCLPruneRecoverySelect,
+//                                                   the pruned pieces concatenated (ColConcatenate)
 //   Mult_AnXBn_SUMMA3D       ParFriends.h:2918-3208 layer SUMMA, then the fiber reduce-scatter
 //                                                   (:3097-3183) as device column pieces exchanged
 //                                                   with grouped ncclSend / ncclRecv and merged
 //   MemEfficientSpGEMM3D     ParFriends.h:3214-3705 B's layer block cut in `layers` chunks, each in
-//                                                   `phases` pieces; phase p = piece p of every
-//                                                   chunk: layer SUMMA, fiber reduce-scatter,
-//                                                   prune on the layer grid, concatenation
+//                                                   `phases` pieces; the layer's stage pairs planned
+//                                                   once; phase p = piece p of every chunk: layer
+//                                                   numeric pass, fiber reduce-scatter, prune on the
+//                                                   layer grid, concatenation
 // Every block, stage partial and piece stays in HBM; only sizes (essentials) cross the host.
 // COMBBLAS_HIP_COMM=mpi stages the exchanges through host MPI instead of RCCL (test rehearsal of
 // several ranks sharing one GPU).
@@ -186,6 +189,96 @@ inline cbh_mat* fiber_reduce_scatter(cbh_semiring sr, cbh_mat* P, const std::vec
   return merge_all(sr, nonempty);
 }
 
+// The SUMMA stage pairs of C = A * B for a phase loop. The reference re-broadcasts the stage blocks
+// and re-multiplies them in every phase (ParFriends.h:560-669 inside its phase loop); here every
+// stage block is broadcast ONCE and kept in HBM, and each stage pair gets ONE symbolic pass
+// (cbh_plan_create), so a phase runs only the numeric pass of its columns (cbh_plan_spgemm_slots)
+// and the memory model reads the exact per-stage nnz off the plans instead of a separate
+// EstPerProcessNnzSUMMA pass.
+template <class IU, class NU1, class NU2>
+class StagePlans {
+ public:
+  StagePlans(SpDCColsDev<IU, NU1>& Aloc, combblas::CommGrid* GA, SpDCColsDev<IU, NU2>& Bloc, combblas::CommGrid* GB) {
+    int dummy;
+    GridC = ProductGrid(GA, GB, stages, dummy, dummy);  // found by ADL (a friend of CommGrid)
+    m = Aloc.getnrow();
+    auto Asizes = GetSetSizes(Aloc, GA->GetRowWorld());
+    auto Bsizes = GetSetSizes(Bloc, GB->GetColWorld());
+    const int Aself = GA->GetRankInProcRow(), Bself = GB->GetRankInProcCol();
+    for (int i = 0; i < stages; ++i) {
+      SpDCColsDev<IU, NU1>* Ai = &Aloc;
+      SpDCColsDev<IU, NU2>* Bi = &Bloc;
+      if (i != Aself) {
+        Ahold.emplace_back(new SpDCColsDev<IU, NU1>());
+        Ai = Ahold.back().get();
+      }
+      if (i != Bself) {
+        Bhold.emplace_back(new SpDCColsDev<IU, NU2>());
+        Bi = Bhold.back().get();
+      }
+      BCastMatrix(GridC->GetRowWorld(), *Ai, Asizes[i], i);
+      BCastMatrix(GridC->GetColWorld(), *Bi, Bsizes[i], i);
+      cbh_plan* p = nullptr;
+      std::vector<int64_t> jc;
+      if (Ai->getnnz() > 0 && Bi->getnnz() > 0) {
+        int rc = cbh_plan_create(context(), Ai->mat(), Bi->mat(), &p);
+        if (rc != CBH_OK) die(context(), rc, "cbh_plan_create");
+        int64_t f = 0, z = 0;
+        cbh_plan_info(p, &f, &z);
+        nnz += z;
+        jc.resize((size_t)Bi->getnzc());
+        rc = cbh_mat_copy_out(context(), Bi->mat(), nullptr, jc.data(), nullptr, nullptr, 0);
+        if (rc != CBH_OK) die(context(), rc, "cbh_mat_copy_out");
+      }
+      plans.push_back(p);
+      bjc.push_back(std::move(jc));
+    }
+  }
+  ~StagePlans() {
+    for (cbh_plan* p : plans)
+      if (p) cbh_plan_destroy(p);
+  }
+  StagePlans(const StagePlans&) = delete;
+  StagePlans& operator=(const StagePlans&) = delete;
+  // C(:, c0:c1) as an m x (c1 - c0) block with rebased column ids (a ColSplit piece of B times A,
+  // ParFriends.h:591-669), the stages' partials merged on the device
+  cbh_mat* piece(cbh_semiring sr, int dtype, int64_t vbytes, int64_t c0, int64_t c1) {
+    std::vector<cbh_mat*> parts;
+    for (size_t i = 0; i < plans.size(); ++i) {
+      if (!plans[i]) continue;
+      const std::vector<int64_t>& jc = bjc[i];
+      const int64_t s0 = std::lower_bound(jc.begin(), jc.end(), c0) - jc.begin();
+      const int64_t s1 = std::lower_bound(jc.begin(), jc.end(), c1) - jc.begin();
+      if (s1 <= s0) continue;
+      cbh_mat* C = nullptr;
+      int rc = cbh_plan_spgemm_slots(plans[i], sr, s0, s1, 0, &C);
+      if (rc != CBH_OK) die(context(), rc, "cbh_plan_spgemm_slots");
+      if (essentials(C)[0] > 0) parts.push_back(C);
+      else cbh_mat_free(context(), C);
+    }
+    cbh_mat* out = nullptr;
+    if (parts.empty()) {
+      int rc = cbh_mat_create(context(), m, c1 - c0, 0, 0, (cbh_dtype)dtype, vbytes, &out);
+      if (rc != CBH_OK) die(context(), rc, "cbh_mat_create");
+      return out;
+    }
+    out = parts.size() == 1 ? parts[0] : merge_all(sr, parts);
+    int rc = cbh_mat_rebase_cols(context(), out, c0, c1 - c0);
+    if (rc != CBH_OK) die(context(), rc, "cbh_mat_rebase_cols");
+    return out;
+  }
+  std::shared_ptr<combblas::CommGrid> GridC;
+  int stages = 0;
+  int64_t m = 0;
+  int64_t nnz = 0;  // exact nnz of the whole local product, summed over the stages
+
+ private:
+  std::vector<std::unique_ptr<SpDCColsDev<IU, NU1>>> Ahold;  // received stage blocks
+  std::vector<std::unique_ptr<SpDCColsDev<IU, NU2>>> Bhold;
+  std::vector<cbh_plan*> plans;
+  std::vector<std::vector<int64_t>> bjc;  // host column ids of every stage's B block
+};
+
 // the product 3D grid of C (ParFriends.h:3200-3203 / 3700: a fresh CommGrid3D of A's shape)
 template <class IU, class NU1, class DER>
 std::shared_ptr<combblas::CommGrid3D> product_grid3d(combblas::SpParMat3D<IU, NU1, DER>& A) {
@@ -266,8 +359,12 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
     MPI_Abort(MPI_COMM_WORLD, DIMMISMATCH);
   }
   if (phases < 1 || phases >= A.getncol()) phases = 1;
-  int stages, dummy;
-  std::shared_ptr<CommGrid> GridC = ProductGrid(A.getcommgrid().get(), B.getcommgrid().get(), stages, dummy, dummy);
+  // the plans (and their scratch) live for the phase loop only: the concatenation of the pruned
+  // pieces below needs a second copy of them in HBM
+  std::unique_ptr<combblas_hip::StagePlans<IU, NU1, NU2>> SPp(
+      new combblas_hip::StagePlans<IU, NU1, NU2>(A.seq(), A.getcommgrid().get(), B.seq(), B.getcommgrid().get()));
+  combblas_hip::StagePlans<IU, NU1, NU2>& SP = *SPp;
+  std::shared_ptr<CommGrid> GridC = SP.GridC;
   if (perProcessMemory > 0) {  // the reference's memory model (ParFriends.h:480-520), exact nnz per stage
     int p;
     MPI_Comm_size(GridC->GetWorld(), &p);
@@ -275,7 +372,8 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
     int64_t lannz = A.getlocalnnz(), gannz = 0;
     MPI_Allreduce(&lannz, &gannz, 1, MPI_INT64_T, MPI_MAX, GridC->GetWorld());
     const int64_t inputMem = gannz * perNNZMem_in * 4;
-    const int64_t asquareNNZ = EstPerProcessNnzSUMMA(A, B, false);
+    int64_t asquareNNZ = 0;  // EstPerProcessNnzSUMMA: the plans' exact nnz, max over the world
+    MPI_Allreduce(&SP.nnz, &asquareNNZ, 1, MPI_INT64_T, MPI_MAX, GridC->GetWorld());
     const int64_t asquareMem = asquareNNZ * perNNZMem_out * 2;
     const int64_t lcols = std::max<int64_t>(1, B.getlocalcols());
     const int64_t d = (int64_t)std::ceil((asquareNNZ * std::sqrt((double)p)) / lcols);
@@ -285,18 +383,18 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
     const int64_t remainingMem = perProcessMemory * 1000000000 - inputMem - outputMem;
     if (remainingMem > 0) phases = 1 + (int)((asquareMem + kselectmem) / remainingMem);
   }
-  const IU C_m = A.seq().getnrow(), C_n = B.seq().getncol();
+  const IU C_n = B.seq().getncol();
   const auto cuts = combblas_hip::colsplit_cuts(C_n, phases);
   std::vector<cbh_mat*> toconcatenate;
   for (int p = 0; p < phases; ++p) {
-    combblas_hip::SpDCColsDev<IU, NU2> piece(combblas_hip::col_slice(B.seq().mat(), cuts[p], cuts[p + 1]));
-    std::shared_ptr<CommGrid> G;
-    cbh_mat* Cp = combblas_hip::summa_blocks<SR, NUO>(A.seq(), A.getcommgrid().get(), piece, B.getcommgrid().get(), G);
+    cbh_mat* Cp = SP.piece(combblas_hip::semiring_traits<SR>::code, combblas_hip::dtype_of<NUO>::value,
+                           (int64_t)sizeof(NUO), cuts[p], cuts[p + 1]);
     SpParMat<IU, NUO, UDERO> OnePieceOfC(new UDERO(Cp), GridC);
     MCLPruneRecoverySelect(OnePieceOfC, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion);
     toconcatenate.push_back(OnePieceOfC.seq().release());
   }
-  (void)C_m;
+  SPp.reset();
+  cbh_ctx_trim(combblas_hip::context());  // the cached scratch of the phase loop back to HIP
   return SpParMat<IU, NUO, UDERO>(new UDERO(combblas_hip::col_concat(toconcatenate)), GridC);
 }
 
@@ -335,6 +433,11 @@ SpParMat3D<IU, NUO, UDERO> MemEfficientSpGEMM3D(SpParMat3D<IU, NU1, combblas_hip
   }
   if (phases < 1 || phases >= B.getncol()) phases = 1;
   auto g3 = A.getcommgrid3D();
+  // the layer SUMMA's stage pairs, planned once for every phase (freed before the concatenation)
+  std::unique_ptr<combblas_hip::StagePlans<IU, NU1, NU2>> SPp(new combblas_hip::StagePlans<IU, NU1, NU2>(
+      *A.GetLayerMat()->seqptr(), A.GetLayerMat()->getcommgrid().get(), *B.GetLayerMat()->seqptr(),
+      B.GetLayerMat()->getcommgrid().get()));
+  combblas_hip::StagePlans<IU, NU1, NU2>& SP = *SPp;
   if (perProcessMemory > 0) {  // the reference's 3D memory model (ParFriends.h:3247-3290)
     int p;
     MPI_Comm_size(g3->GetLayerWorld(), &p);
@@ -342,7 +445,8 @@ SpParMat3D<IU, NUO, UDERO> MemEfficientSpGEMM3D(SpParMat3D<IU, NU1, combblas_hip
     int64_t lannz = A.GetLayerMat()->getlocalnnz(), gannz = 0;
     MPI_Allreduce(&lannz, &gannz, 1, MPI_INT64_T, MPI_MAX, g3->GetWorld());
     const int64_t ginputMem = gannz * perNNZMem_in * 5;
-    const int64_t asquareNNZ = EstPerProcessNnzSUMMA(*A.GetLayerMat(), *B.GetLayerMat(), true);
+    int64_t asquareNNZ = 0;  // EstPerProcessNnzSUMMA on the layer: the plans' exact nnz, max over the layer
+    MPI_Allreduce(&SP.nnz, &asquareNNZ, 1, MPI_INT64_T, MPI_MAX, SP.GridC->GetWorld());
     int64_t gasquareNNZ = 0;
     MPI_Allreduce(&asquareNNZ, &gasquareNNZ, 1, MPI_INT64_T, MPI_MAX, g3->GetFiberWorld());
     const int64_t gasquareMem = gasquareNNZ * perNNZMem_out * 2;
@@ -369,21 +473,18 @@ SpParMat3D<IU, NUO, UDERO> MemEfficientSpGEMM3D(SpParMat3D<IU, NU1, combblas_hip
     piece[c] = cuts;
     c0 += div3[c];
   }
-  cbh_mat* Bl = B.GetLayerMat()->seqptr()->mat();
   std::vector<cbh_mat*> toconcatenate;
   for (int p = 0; p < phases; ++p) {
+    // OnePieceOfB = piece p of every chunk (ParFriends.h:3414-3440): the layer product of those
+    // columns is the concatenation of the chunk pieces' products
     std::vector<cbh_mat*> parts;
     std::vector<int64_t> lb(L);
     for (int c = 0; c < L; ++c) {
-      parts.push_back(combblas_hip::col_slice(Bl, piece[c][p], piece[c][p + 1]));
+      parts.push_back(SP.piece(combblas_hip::semiring_traits<SR>::code, combblas_hip::dtype_of<NUO>::value,
+                               (int64_t)sizeof(NUO), piece[c][p], piece[c][p + 1]));
       lb[c] = piece[c][p + 1] - piece[c][p];
     }
-    combblas_hip::SpDCColsDev<IU, NU2> OnePieceOfB(combblas_hip::col_concat(parts));
-    SpParMat<IU, NU2, combblas_hip::SpDCColsDev<IU, NU2>> OnePieceOfBLayer(
-        new combblas_hip::SpDCColsDev<IU, NU2>(OnePieceOfB.release()), g3->GetLayerWorld());
-    std::shared_ptr<CommGrid> G;
-    cbh_mat* P = combblas_hip::summa_blocks<SR, NUO>(*A.GetLayerMat()->seqptr(), A.GetLayerMat()->getcommgrid().get(),
-                                                     OnePieceOfBLayer.seq(), OnePieceOfBLayer.getcommgrid().get(), G);
+    cbh_mat* P = combblas_hip::col_concat(parts);
     cbh_mat* Cp = combblas_hip::fiber_reduce_scatter(combblas_hip::semiring_traits<SR>::code, P, lb,
                                                      g3->GetFiberWorld(), combblas_hip::dtype_of<NUO>::value,
                                                      (int64_t)sizeof(NUO));
@@ -392,6 +493,8 @@ SpParMat3D<IU, NUO, UDERO> MemEfficientSpGEMM3D(SpParMat3D<IU, NU1, combblas_hip
     toconcatenate.push_back(phaseResultantLayer.seq().release());
   }
   (void)me;
+  SPp.reset();
+  cbh_ctx_trim(combblas_hip::context());
   return SpParMat3D<IU, NUO, UDERO>(new UDERO(combblas_hip::col_concat(toconcatenate)),
                                     combblas_hip::product_grid3d(A), A.isColSplit(), A.isSpecial());
 }

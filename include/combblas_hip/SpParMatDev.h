@@ -153,27 +153,43 @@ inline ncclComm_t rccl_comm_for(MPI_Comm comm) {
   ncclUniqueId id;
   if (rank == 0) rccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
   MPI_Bcast(&id, (int)sizeof(id), MPI_BYTE, 0, comm);
-  context();  // the context selects this rank's device
+  // the context selects this rank's device; its cached blocks go back to HIP first, so that RCCL's
+  // own buffers find the memory (the block cache may hold a large share of the HBM)
+  cbh_ctx_trim(context());
   auto* c = new ncclComm_t;
   rccl_check(ncclCommInitRank(c, size, id, rank), "ncclCommInitRank");
   MPI_Comm_set_attr(comm, rccl_keyval(), c);
   return *c;
 }
 
-// SpParHelper::BCastMatrix (SpParHelper.cpp:581-599) on device blocks: non-root ranks allocate
-// from the essentials {nnz, m, n, nzc} (SpDCCols::Create), then cp, jc, ir and the values are
-// broadcast device to device on the context stream.
+// SpParHelper::BCastMatrix (SpParHelper.cpp:581-599) on device blocks, in two halves: non-root
+// ranks allocate from the essentials {nnz, m, n, nzc} (SpDCCols::Create), then cp, jc, ir and the
+// values are broadcast device to device on `s` (the context stream, or the overlapped drivers'
+// communication stream).
 template <class IT, class NT>
-void BCastMatrix(MPI_Comm comm, SpDCColsDev<IT, NT>& M, const std::vector<IT>& ess, int root) {
+void bcast_alloc(MPI_Comm comm, SpDCColsDev<IT, NT>& M, const std::vector<IT>& ess, int root) {
   int rank = 0;
   MPI_Comm_rank(comm, &rank);
-  cbh_ctx* ctx = context();
-  if (rank != root) {
-    cbh_mat* m = nullptr;
-    int rc = cbh_mat_create(ctx, ess[1], ess[2], ess[0], ess[3], dtype_of<NT>::value, (int64_t)sizeof(NT), &m);
-    if (rc != CBH_OK) die(ctx, rc, "cbh_mat_create");
-    M.reset(m);
-  }
+  if (rank == root) return;
+  cbh_mat* m = nullptr;
+  int rc = cbh_mat_create(context(), ess[1], ess[2], ess[0], ess[3], dtype_of<NT>::value, (int64_t)sizeof(NT), &m);
+  if (rc != CBH_OK) die(context(), rc, "cbh_mat_create");
+  M.reset(m);
+}
+template <class IT, class NT>
+void bcast_arrays(MPI_Comm comm, SpDCColsDev<IT, NT>& M, const std::vector<IT>& ess, int root, hipStream_t s,
+                  bool grouped = false);
+template <class IT, class NT>
+void BCastMatrix(MPI_Comm comm, SpDCColsDev<IT, NT>& M, const std::vector<IT>& ess, int root) {
+  bcast_alloc(comm, M, ess, root);
+  bcast_arrays(comm, M, ess, root, reinterpret_cast<hipStream_t>(cbh_ctx_stream(context())));
+}
+// grouped: the caller brackets several broadcasts in one ncclGroupStart / ncclGroupEnd
+template <class IT, class NT>
+void bcast_arrays(MPI_Comm comm, SpDCColsDev<IT, NT>& M, const std::vector<IT>& ess, int root, hipStream_t s,
+                  bool grouped) {
+  int rank = 0;
+  MPI_Comm_rank(comm, &rank);
   const int64_t *cp, *jc;
   const int32_t* ir;
   const void* num;
@@ -186,7 +202,6 @@ void BCastMatrix(MPI_Comm comm, SpDCColsDev<IT, NT>& M, const std::vector<IT>& e
                  {const_cast<int64_t*>(jc), sizeof(int64_t) * (size_t)nzc},
                  {const_cast<int32_t*>(ir), sizeof(int32_t) * (size_t)nnz},
                  {const_cast<void*>(num), sizeof(NT) * (size_t)nnz}};
-  hipStream_t s = reinterpret_cast<hipStream_t>(cbh_ctx_stream(ctx));
   if (use_mpi_transport()) {  // host-staged rehearsal transport
     for (const Piece& x : pieces) {
       if (!x.bytes) continue;
@@ -204,10 +219,10 @@ void BCastMatrix(MPI_Comm comm, SpDCColsDev<IT, NT>& M, const std::vector<IT>& e
     return;
   }
   ncclComm_t nc = rccl_comm_for(comm);
-  rccl_check(ncclGroupStart(), "ncclGroupStart");
+  if (!grouped) rccl_check(ncclGroupStart(), "ncclGroupStart");
   for (const Piece& x : pieces)
     if (x.bytes) rccl_check(ncclBroadcast(x.p, x.p, x.bytes, ncclUint8, root, nc, s), "ncclBroadcast");
-  rccl_check(ncclGroupEnd(), "ncclGroupEnd");
+  if (!grouped) rccl_check(ncclGroupEnd(), "ncclGroupEnd");
 }
 
 // SpParHelper::GetSetSizes (SpParHelper.cpp:797-808): essentials of every rank of comm1d
@@ -272,6 +287,95 @@ cbh_mat* summa_blocks(SpDCColsDev<IU, NU1>& Aloc, combblas::CommGrid* GA, SpDCCo
   return merge_all(semiring_traits<SR>::code, tomerge);
 }
 
+// The stage broadcasts of the overlapped drivers run on a stream of their own: the multiply of
+// stage i (context stream) waits only for stage i's broadcasts (an event), so later stages' RCCL
+// transfers overlap it (Mult_AnXBn_Overlap, ParFriends.h:1110-1235: MPI_Ibcast of every stage
+// up front, each multiply after MPI_Waitall of its stage).
+inline hipStream_t comm_stream() {
+  static hipStream_t s = [] {
+    hipStream_t x = nullptr;
+    if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) die(context(), CBH_E_HIP, "hipStreamCreate");
+    return x;
+  }();
+  return s;
+}
+
+// SUMMA over two device blocks with every stage's broadcasts posted up front on comm_stream():
+// receive blocks are allocated first (their memory ordered before the transfers by an event on
+// the context stream), stage i's multiply waits on stage i's event; the non-empty stage products
+// are appended to `partials` (merged by the caller). The host-staged transport
+// (COMBBLAS_HIP_COMM=mpi) runs the stages one after another.
+template <class SR, class NUO, class IU, class NU1, class NU2>
+void summa_overlap(SpDCColsDev<IU, NU1>& Aloc, combblas::CommGrid* GA, SpDCColsDev<IU, NU2>& Bloc,
+                   combblas::CommGrid* GB, std::shared_ptr<combblas::CommGrid>& GridC, std::vector<cbh_mat*>& partials) {
+  int stages, dummy;
+  GridC = ProductGrid(GA, GB, stages, dummy, dummy);  // found by ADL (a friend of CommGrid)
+  auto Asizes = GetSetSizes(Aloc, GA->GetRowWorld());
+  auto Bsizes = GetSetSizes(Bloc, GB->GetColWorld());
+  const int Aself = GA->GetRankInProcRow(), Bself = GB->GetRankInProcCol();
+  std::vector<std::unique_ptr<SpDCColsDev<IU, NU1>>> Ar(stages);
+  std::vector<std::unique_ptr<SpDCColsDev<IU, NU2>>> Br(stages);
+  auto Ai = [&](int i) -> SpDCColsDev<IU, NU1>& { return i == Aself ? Aloc : *Ar[i]; };
+  auto Bi = [&](int i) -> SpDCColsDev<IU, NU2>& { return i == Bself ? Bloc : *Br[i]; };
+  for (int i = 0; i < stages; ++i) {
+    if (i != Aself) Ar[i].reset(new SpDCColsDev<IU, NU1>());
+    if (i != Bself) Br[i].reset(new SpDCColsDev<IU, NU2>());
+    bcast_alloc(GridC->GetRowWorld(), Ai(i), Asizes[i], i);
+    bcast_alloc(GridC->GetColWorld(), Bi(i), Bsizes[i], i);
+  }
+  hipStream_t cs = comm_stream(), ks = reinterpret_cast<hipStream_t>(cbh_ctx_stream(context()));
+  const bool overlap = !use_mpi_transport();
+  std::vector<hipEvent_t> done(stages, nullptr);
+  if (overlap) {
+    MPI_Comm rw = GridC->GetRowWorld(), cw = GridC->GetColWorld();
+    (void)rccl_comm_for(rw);  // communicators exist before the grouped calls
+    (void)rccl_comm_for(cw);
+    hipEvent_t ready;
+    if (hipEventCreateWithFlags(&ready, hipEventDisableTiming) != hipSuccess) die(context(), CBH_E_HIP, "hipEventCreate");
+    (void)hipEventRecord(ready, ks);  // the receive blocks' memory: ordered after the context stream's work
+    (void)hipStreamWaitEvent(cs, ready, 0);
+    (void)hipEventDestroy(ready);
+    for (int i = 0; i < stages; ++i) {
+      rccl_check(ncclGroupStart(), "ncclGroupStart");
+      bcast_arrays(rw, Ai(i), Asizes[i], i, cs, true);
+      bcast_arrays(cw, Bi(i), Bsizes[i], i, cs, true);
+      rccl_check(ncclGroupEnd(), "ncclGroupEnd");
+      if (hipEventCreateWithFlags(&done[i], hipEventDisableTiming) != hipSuccess) die(context(), CBH_E_HIP, "hipEventCreate");
+      (void)hipEventRecord(done[i], cs);
+    }
+  }
+  for (int i = 0; i < stages; ++i) {
+    if (overlap) {
+      (void)hipStreamWaitEvent(ks, done[i], 0);
+    } else {
+      bcast_arrays(GridC->GetRowWorld(), Ai(i), Asizes[i], i, ks);
+      bcast_arrays(GridC->GetColWorld(), Bi(i), Bsizes[i], i, ks);
+    }
+    cbh_mat* Ci = local_multiply<SR, NUO, NU1, NU2>(Ai(i).mat(), Bi(i).mat());
+    int64_t nnz = 0;
+    cbh_mat_info(Ci, nullptr, nullptr, &nnz, nullptr, nullptr);
+    if (nnz > 0) partials.push_back(Ci);
+    else cbh_mat_free(context(), Ci);
+    if (i != Aself) Ar[i].reset();  // the reference's clearA / clearB = i != self
+    if (i != Bself) Br[i].reset();
+  }
+  for (hipEvent_t e : done)
+    if (e) (void)hipEventDestroy(e);
+}
+
+inline cbh_mat* merge_partials(cbh_semiring sr, std::vector<cbh_mat*>& parts, int64_t m, int64_t n, int dtype,
+                               int64_t vbytes) {
+  if (parts.empty()) {
+    cbh_mat* C = nullptr;
+    int rc = cbh_mat_create(context(), m, n, 0, 0, (cbh_dtype)dtype, vbytes, &C);
+    if (rc != CBH_OK) die(context(), rc, "cbh_mat_create");
+    return C;
+  }
+  cbh_mat* C = parts.size() == 1 ? parts[0] : merge_all(sr, parts);
+  parts.clear();
+  return C;
+}
+
 // SpParMat<.., SpDCCols> <-> SpParMat<.., SpDCColsDev>: one upload / download of the local block
 template <class IT, class NT>
 combblas::SpParMat<IT, NT, SpDCColsDev<IT, NT>> to_device(combblas::SpParMat<IT, NT, combblas::SpDCCols<IT, NT>>& A) {
@@ -307,6 +411,68 @@ SpParMat<IU, NUO, UDERO> Mult_AnXBn_Synch(SpParMat<IU, NU1, combblas_hip::SpDCCo
   cbh_mat* C = combblas_hip::summa_blocks<SR, NUO>(A.seq(), A.getcommgrid().get(), B.seq(), B.getcommgrid().get(), GridC);
   if (clearA) A.seq() = combblas_hip::SpDCColsDev<IU, NU1>();
   if (clearB) B.seq() = combblas_hip::SpDCColsDev<IU, NU2>();
+  return SpParMat<IU, NUO, UDERO>(new UDERO(C), GridC);
+}
+
+// Mult_AnXBn_Overlap (ParFriends.h:1110-1235) for device-resident operands: every stage's
+// broadcasts posted up front on the communication stream, each stage's multiply as soon as its
+// blocks have arrived, the partials merged on the device.
+template <typename SR, typename NUO, typename UDERO, typename IU, typename NU1, typename NU2>
+SpParMat<IU, NUO, UDERO> Mult_AnXBn_Overlap(SpParMat<IU, NU1, combblas_hip::SpDCColsDev<IU, NU1>>& A,
+                                            SpParMat<IU, NU2, combblas_hip::SpDCColsDev<IU, NU2>>& B,
+                                            bool clearA = false, bool clearB = false) {
+  static_assert(std::is_same<UDERO, combblas_hip::SpDCColsDev<IU, NUO>>::value,
+                "device-resident operands give a device-resident product");
+  if (!CheckSpGEMMCompliance(A, B)) return SpParMat<IU, NUO, UDERO>();
+  const IU C_m = A.seq().getnrow(), C_n = B.seq().getncol();
+  std::shared_ptr<CommGrid> GridC;
+  std::vector<cbh_mat*> parts;
+  combblas_hip::summa_overlap<SR, NUO>(A.seq(), A.getcommgrid().get(), B.seq(), B.getcommgrid().get(), GridC, parts);
+  if (clearA) A.seq() = combblas_hip::SpDCColsDev<IU, NU1>();
+  if (clearB) B.seq() = combblas_hip::SpDCColsDev<IU, NU2>();
+  cbh_mat* C = combblas_hip::merge_partials(combblas_hip::semiring_traits<SR>::code, parts, C_m, C_n,
+                                            combblas_hip::dtype_of<NUO>::value, (int64_t)sizeof(NUO));
+  return SpParMat<IU, NUO, UDERO>(new UDERO(C), GridC);
+}
+
+// Mult_AnXBn_DoubleBuff (ParFriends.h:798-997) for device-resident operands: the inner dimension
+// in two halves (SpDCCols::Split of A's columns and of the transposed B), each half a SUMMA round with overlapped broadcasts of half-blocks -- 2 * stages
+// partials, merged on the device.
+template <typename SR, typename NUO, typename UDERO, typename IU, typename NU1, typename NU2>
+SpParMat<IU, NUO, UDERO> Mult_AnXBn_DoubleBuff(SpParMat<IU, NU1, combblas_hip::SpDCColsDev<IU, NU1>>& A,
+                                               SpParMat<IU, NU2, combblas_hip::SpDCColsDev<IU, NU2>>& B,
+                                               bool clearA = false, bool clearB = false) {
+  static_assert(std::is_same<UDERO, combblas_hip::SpDCColsDev<IU, NUO>>::value,
+                "device-resident operands give a device-resident product");
+  if (!CheckSpGEMMCompliance(A, B)) return SpParMat<IU, NUO, UDERO>();
+  const IU C_m = A.seq().getnrow(), C_n = B.seq().getncol();
+  // SpDCCols::Split: columns [0, n/2) and [n/2, n) of A's block; of B's transposed block, so B's
+  // rows [0, m/2) and [m/2, m) -- each rank cuts its own block (stage i's A and B halves meet on
+  // the same k range: A_i's columns are B_i's rows)
+  const int64_t ka = A.seq().getncol(), kb = B.seq().getnrow();
+  cbh_ctx* ctx = combblas_hip::context();
+  cbh_mat *a1 = nullptr, *a2 = nullptr, *b1 = nullptr, *b2 = nullptr;
+  if (cbh_mat_col_slice(ctx, A.seq().mat(), 0, ka / 2, &a1) != CBH_OK ||
+      cbh_mat_col_slice(ctx, A.seq().mat(), ka / 2, ka, &a2) != CBH_OK ||
+      cbh_mat_row_slice(ctx, B.seq().mat(), 0, kb / 2, &b1) != CBH_OK ||
+      cbh_mat_row_slice(ctx, B.seq().mat(), kb / 2, kb, &b2) != CBH_OK)
+    combblas_hip::die(ctx, CBH_E_INTERNAL, "DoubleBuff split");
+  if (clearA) A.seq() = combblas_hip::SpDCColsDev<IU, NU1>();
+  if (clearB) B.seq() = combblas_hip::SpDCColsDev<IU, NU2>();
+  std::shared_ptr<CommGrid> GridC;
+  std::vector<cbh_mat*> parts;
+  {
+    combblas_hip::SpDCColsDev<IU, NU1> A1(a1);
+    combblas_hip::SpDCColsDev<IU, NU2> B1(b1);
+    combblas_hip::summa_overlap<SR, NUO>(A1, A.getcommgrid().get(), B1, B.getcommgrid().get(), GridC, parts);
+  }
+  {
+    combblas_hip::SpDCColsDev<IU, NU1> A2(a2);
+    combblas_hip::SpDCColsDev<IU, NU2> B2(b2);
+    combblas_hip::summa_overlap<SR, NUO>(A2, A.getcommgrid().get(), B2, B.getcommgrid().get(), GridC, parts);
+  }
+  cbh_mat* C = combblas_hip::merge_partials(combblas_hip::semiring_traits<SR>::code, parts, C_m, C_n,
+                                            combblas_hip::dtype_of<NUO>::value, (int64_t)sizeof(NUO));
   return SpParMat<IU, NUO, UDERO>(new UDERO(C), GridC);
 }
 

@@ -24,32 +24,44 @@ struct TSymSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 #ifndef CBH_SYM_U
 #define CBH_SYM_U 16
 #endif
-struct TSymLarge { static constexpr int T = 8192, BS = CBH_SYM_BS, EMAX = 512, U = CBH_SYM_U; };
+#ifndef CBH_SYM_T
+#define CBH_SYM_T 8192
+#endif
+struct TSymLarge { static constexpr int T = CBH_SYM_T, BS = CBH_SYM_BS, EMAX = 512, U = CBH_SYM_U; };
 // mid-size symbolic tasks (kSmallCap < products <= kSymMidCap): one sub-tile in a 16 KB key
 // table, five workgroups per CU, so the per-task setup latency overlaps
 constexpr int kSymMid = 2048;  // (1024 / 4096 measured no better)
-#ifndef CBH_MID_U
-#define CBH_MID_U 4
-#endif
-struct TSymMid { static constexpr int T = 2 * kSymMid, BS = 256, EMAX = 256, U = CBH_MID_U; };
+struct TSymMid { static constexpr int T = 2 * kSymMid, BS = 256, EMAX = 256, U = 4; };
 struct TNumSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 // (T = 8192 with 1024-thread groups, one per CU: 89.1 vs 98.2 GFLOP/s at scale 22)
-struct TNumLarge { static constexpr int T = 4096, BS = 512, EMAX = 512, U = 8; };
-// the library's large hash bin (MODE_TNUM; the dense windows keep TNumLarge)
+#ifndef CBH_DENSE_T
+#define CBH_DENSE_T 4096
+#endif
+#ifndef CBH_DENSE_U
+#define CBH_DENSE_U 8
+#endif
+struct TNumLarge { static constexpr int T = CBH_DENSE_T, BS = 512, EMAX = 512, U = CBH_DENSE_U; };
+// the hash sub-tile size the dense split rule prices a task's hash alternative with (dense_subtiles)
+constexpr int64_t kSplitHashT = 4096;
+// the library's large hash bin (MODE_TNUM; the dense windows keep TNumLarge): a 2048-slot table
+// and 4 products per thread per window keep a group at 53 KB of LDS and <= 80 VGPRs, so THREE
+// groups share a CU (24 waves instead of 16): hash 375 -> 360 ms per scale-22 A^2 (A/B twice,
+// DESIGN.md §4). T 4096 / U 8 (two groups per CU), 1024 threads / U 4 and 768 threads / U 5
+// (VGPR spills), and 5/8 fill of the 2048 table measured slower.
 #ifndef CBH_HASH_T
-#define CBH_HASH_T 4096
+#define CBH_HASH_T 2048
 #endif
 #ifndef CBH_HASH_BS
 #define CBH_HASH_BS 512
 #endif
 #ifndef CBH_HASH_U
-#define CBH_HASH_U 8
+#define CBH_HASH_U 4
 #endif
 struct TNumHash { static constexpr int T = CBH_HASH_T, BS = CBH_HASH_BS, EMAX = 512, U = CBH_HASH_U; };
 // mid-size hash tasks (kSmallCap < outputs <= kMidCap) of the library's A^2 path: a quarter of the
 // large kernel's LDS, so four workgroups share a CU and the per-task setup latency overlaps
 constexpr int kMidOut = 1024;  // (512 / 2048 measured no better)
-struct TNumMid { static constexpr int T = 2 * kMidOut, BS = 256, EMAX = 256, U = CBH_MID_U; };
+struct TNumMid { static constexpr int T = 2 * kMidOut, BS = 256, EMAX = 256, U = 4; };  // (U 8: flat)
 // wider accumulators (user value types) keep the large table within ~50 KB of LDS
 template <class SR>
 struct TNumLargeFor {
@@ -61,7 +73,7 @@ template <class SR>
 struct TNumMidFor {
   static constexpr int bytes = (int)(sizeof(int32_t) + sizeof(typename SR::acc_t));
   static constexpr int T = bytes <= 12 ? 2 * kMidOut : (bytes <= 24 ? kMidOut : 512);
-  static constexpr int BS = 256, EMAX = 256, U = CBH_MID_U;
+  static constexpr int BS = 256, EMAX = 256, U = 4;
 };
 template <class SR>
 struct TNumSmallFor {

@@ -38,22 +38,13 @@ constexpr int32_t kNoRow = 0x7fffffff;
 // cursor row not loaded yet (< every row range: the entry counts as active, and its first
 // segment search starts AT the cursor, whose row the search loads with the following ones)
 constexpr int32_t kUnknownRow = -2;
-#ifdef CBH_NO_ALIGN
-constexpr bool kAlignSubtiles = false;
-#else
-constexpr bool kAlignSubtiles = true;
-#endif
+constexpr bool kAlignSubtiles = true;  // sub-tiles and dense windows end on row-block boundaries
 constexpr int kSymWords = 12160;  // bitmap words of the large symbolic configuration (see TaskCfg::TA)
 // numeric sub-tile: planned outputs, in eighths of the T home slots (3/8 and 5/8 measured slower:
-// 97.6 and 93.5 vs 98.6 GFLOP/s at scale 22)
-#ifndef CBH_FILL8
-#define CBH_FILL8 4
-#endif
-#ifndef CBH_SYMFILL8
-#define CBH_SYMFILL8 4
-#endif
-constexpr int kFill8 = CBH_FILL8;
-constexpr int kSymFill8 = CBH_SYMFILL8;  // symbolic key-hash sub-tiles: keys, in eighths of TA
+// 97.6 and 93.5 vs 98.6 GFLOP/s at scale 22 with T 4096; 5/8 again with T 2048: hash 434 vs 360 ms)
+constexpr int kFill8 = 4;
+// symbolic key-hash sub-tiles: keys, in eighths of TA (6/8 measured flat: symbolic 197 vs 193 ms)
+constexpr int kSymFill8 = 4;
 // dense numeric sub-tile capacity in quarters of T: 3 = 3072 values for T = 4096 (2 and 4
 // measured slower: 98.7 / 104.5 vs 105.3 GFLOP/s at scale 22)
 constexpr int kCapD4 = 3;

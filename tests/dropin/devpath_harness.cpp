@@ -74,16 +74,28 @@ static int run_case(const char* name, SpParMat<int64_t, int64_t, SpDCCols<int64_
   SpParMat<int64_t, NT, HD> Cc = Mult_AnXBn_Synch<SRC, NT, HD>(A, B);  // stock reference path
   double cpu = MPI_Wtime() - t1;
   int ok = same(Ch.seq(), Cc.seq()) ? 1 : 0, all = 0;
+  // the overlapped drivers on the device (ParFriends.h:1110-1235, :798-997): the same C
+  SpParMat<int64_t, NT, DD> Co = Mult_AnXBn_Overlap<SRD, NT, DD>(Ad, Bd);
+  SpParMat<int64_t, NT, HD> Coh = combblas_hip::to_host(Co);
+  SpParMat<int64_t, NT, DD> Cb = Mult_AnXBn_DoubleBuff<SRD, NT, DD>(Ad, Bd);
+  SpParMat<int64_t, NT, HD> Cbh = combblas_hip::to_host(Cb);
+  const int ok_over = same(Coh.seq(), Cc.seq()) ? 1 : 0, ok_dbuf = same(Cbh.seq(), Cc.seq()) ? 1 : 0;
+  int all_over = 0, all_dbuf = 0;
+  MPI_Allreduce(&ok_over, &all_over, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
+  MPI_Allreduce(&ok_dbuf, &all_dbuf, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
   MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
   int rank = 0, np = 1;
   MPI_Comm_rank(MPI_COMM_WORLD, &rank);
   MPI_Comm_size(MPI_COMM_WORLD, &np);
   const int64_t nnz = Cc.getnnz();
-  if (rank == 0)
+  if (rank == 0) {
     std::printf("DEVPATH %s %s ranks=%d nnz=%lld hip_s=%.4f cpu_s=%.4f transport=%s\n", name, all ? "OK" : "MISMATCH",
                 np, (long long)nnz, best, cpu, combblas_hip::use_mpi_transport() ? "mpi" : "rccl");
+    std::printf("DEVPATH %s/Mult_AnXBn_Overlap %s ranks=%d\n", name, all_over ? "OK" : "MISMATCH", np);
+    std::printf("DEVPATH %s/Mult_AnXBn_DoubleBuff %s ranks=%d\n", name, all_dbuf ? "OK" : "MISMATCH", np);
+  }
   std::fflush(stdout);
-  return all ? 0 : 1;
+  return (all && all_over && all_dbuf) ? 0 : 1;
 }
 
 int main(int argc, char** argv) {

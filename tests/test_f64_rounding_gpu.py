@@ -6,7 +6,15 @@ every order guarantees is the standard recursive-summation bound: for an entry w
     |fl(sum) - sum| <= gamma_{k-1} * sum |a_ik * b_kj|,   gamma_m = m*eps / (1 - m*eps),
 so any two orders (two device runs, or device vs the CPU oracle) differ by at most twice that.
 These tests check exactly that bound on every entry, with the structure bit-exact, on an R-MAT
-pattern whose hub columns exercise the hash, dense and chunked (ne > 512) task paths."""
+pattern whose hub columns exercise the hash, dense and chunked (ne > 512) task paths.
+
+north_star's bar for double PlusTimes is 1e-12 relative. It is asserted on every entry that is not
+an ill-conditioned sum, sum |a b| <= 10^3 |c| (with that condition number, a summation-order
+difference of a few ulps of the largest partial sums stays below 1e-12 of c); the entries outside
+it (cancellation down to below 10^-3 of the magnitudes summed: 97 of 2.2 M at scale 13, 925 of
+18.8 M at scale 15) are reported and held to the bound above. For scale: the reference's own heap
+and hash kernels (the oracle's restatement of both orders) differ from its hybrid by at most
+2.2e-13 relative on the well-conditioned entries of these products."""
 import numpy as np
 import pytest
 
@@ -31,12 +39,12 @@ def _with(d, num):
 
 
 def _bound(oracle, A, B):
-    """per-entry 2 * gamma_{k-1} * sum |a b| (in the oracle's output order)"""
+    """per-entry 2 * gamma_{k-1} * sum |a b| (in the oracle's output order), and sum |a b|"""
     absC = oracle.spgemm(_with(A, np.abs(A.num)), _with(B, np.abs(B.num)), "plus_times", "hybrid", threads=8)
     cnt = oracle.spgemm(_with(A, np.ones_like(A.num)), _with(B, np.ones_like(B.num)), "plus_times", "hybrid", threads=8)
     m = np.maximum(cnt.num - 1.0, 0.0)
     gamma = m * EPS / (1.0 - m * EPS)
-    return 2.0 * gamma * absC.num * (1.0 + 4 * EPS)
+    return 2.0 * gamma * absC.num * (1.0 + 4 * EPS), absC.num
 
 
 @pytest.mark.parametrize("scale", [13, 15])
@@ -53,12 +61,20 @@ def test_f64_rounding_within_summation_bound(ctx, oracle, scale):
         runs.append(H.Dcsc(h.m, h.n, h.jc, h.cp, h.ir, h.num))
         C.free()
     ref = oracle.spgemm(A, A, "plus_times", "hybrid", threads=8)
-    bound = _bound(oracle, A, A)
+    bound, absab = _bound(oracle, A, A)
+    well = absab <= 1e3 * np.abs(ref.num)  # not an ill-conditioned (cancelling) sum
+    exempt = int((~well).sum())
+    print(f"scale {scale}: {ref.nnz} entries, {exempt} exempt from 1e-12 (sum|ab| > 1e3 |c|)")
+    assert exempt <= 1e-4 * ref.nnz
     for got in runs:
         assert np.array_equal(got.jc, ref.jc) and np.array_equal(got.cp, ref.cp) and np.array_equal(got.ir, ref.ir)
         err = np.abs(got.num - ref.num)
         worst = int(np.argmax(err - bound))
         assert np.all(err <= bound), f"entry {worst}: |dev - oracle| {err[worst]:.3e} > bound {bound[worst]:.3e}"
+        rel = err / np.maximum(np.abs(ref.num), np.finfo(np.float64).tiny)
+        w = int(np.argmax(np.where(well, rel, 0.0)))
+        assert np.all(rel[well] <= 1e-12), f"entry {w}: relative error {rel[w]:.3e} > 1e-12 (sum|ab|/|c| = " \
+                                           f"{absab[w] / abs(ref.num[w]):.1f})"
     d12 = np.abs(runs[0].num - runs[1].num)
     assert np.all(d12 <= bound)
     # single-product entries have a zero bound (bit-exact); enough entries sum several products

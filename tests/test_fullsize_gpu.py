@@ -1,0 +1,132 @@
+"""GPU: BASELINE.json's application configs at their FULL sizes, inside the -m gpu run (the bench
+scripts check them too, but the driver only runs bench.py):
+
+  C3  Galerkin R^T (A R), 27-point Poisson on 256^3 -> 128^3 (bench_galerkin.py's workload): both
+      products on the device; nnz, the closed-form value sum (R 1)^T A (R 1) and the whole result's
+      digest against tests/golden/fullsize.json (CPU oracle, make_golden_fullsize.py). Dyadic
+      values: bit-exact.
+  C5  HipMCL expansion + MCLPruneRecoverySelect at n = 2^24 (bench_mcl.py's workload: the
+      library's planted-partition generator, MemEfficientSpGEMM's phase loop with MCL.cpp's
+      default prune): 100 sampled columns of the device expansion against the CPU oracle
+      (structure exact, values within 1e-12 relative), and the device's pruned columns against
+      the oracle prune (oracle/apps_oracle.py, pinned to the reference) of the device's own
+      unpruned columns.
+  C4  TC's (L*L) .* L at R-MAT scale 22 (TC.cpp's L built on the device), dot form: the triangle
+      count and the masked product's digest equal the expand form's (an independent evaluation:
+      products looked up in the mask column), and 200 sampled mask columns recomputed on the host.
+Each test takes well under its 180 s budget on an MI355X (most of it host-side checking).
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+
+def test_c3_galerkin_256_full(ctx):
+    import combblas_amd as cb
+    from combblas_amd.apps import Transpose
+    from combblas_amd.galerkin import poisson27_csc, prolongation_csc
+
+    sys.path.insert(0, H.REPO)
+    from bench_galerkin import closed_form_sum
+
+    with open(os.path.join(H.GOLDEN, "fullsize.json")) as f:
+        g = json.load(f)["galerkin"]
+    A, R = poisson27_csc(g["nx"]), prolongation_csc(g["nx"])
+    expect_sum = closed_form_sum(A, R)
+    dA, dR = cb.SpDCCols.from_host(ctx, A), cb.SpDCCols.from_host(ctx, R)
+    del A, R
+    dS = Transpose(dR)
+    AT = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dA, dR)
+    SAT = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dS, AT)
+    vsum, dig = SAT.checksum()
+    assert (AT.nnz, SAT.nnz) == (g["nnzAT"], g["nnzSAT"])
+    assert vsum == expect_sum == g["sumSAT"]
+    assert str(dig) == g["digestSAT"]
+    for X in (AT, SAT, dA, dR, dS):
+        X.free()
+
+
+def test_c5_mcl_2_24_sampled_columns(ctx, oracle):
+    import torch
+
+    import combblas_amd as cb
+    from combblas_amd import parfriends as pf
+    from combblas_amd.backend import HipBackend
+    from combblas_amd.commgrid import CommGrid
+    from combblas_amd.mclgen import planted_partition_lib
+    from combblas_amd.spparmat import SpParMat
+
+    sys.path.insert(0, os.path.join(H.REPO, "oracle"))
+    import apps_oracle as AO
+
+    hard, select, recover, pct = 1e-4, 1100, 1400, 0.9  # MCL.cpp's defaults
+    n, ncheck = 1 << 24, 100
+    be = HipBackend(ctx)
+    gA = planted_partition_lib(ctx, n, 100, 7)
+    dA, dB = SpParMat(gA, CommGrid(), be, n, n), SpParMat(gA.clone(), CommGrid(), be, n, n)
+    rng = np.random.default_rng(11)
+    sample = np.sort(rng.choice(n, size=ncheck, replace=False))
+    samp_t = torch.as_tensor(sample, device=ctx.tdevice)
+    got = {}
+
+    def keep(C, c0, c1):
+        cp, jc, ir, num = be.arrays(C)
+        for s in torch.nonzero(torch.isin(jc, samp_t)).flatten().tolist():
+            a, b = int(cp[s].item()), int(cp[s + 1].item())
+            got[int(jc[s].item())] = (ir[a:b].cpu().numpy(), num[a:b].cpu().numpy())
+        be.free(C)
+
+    phases = pf.MemEfficientSpGEMM(cb.PlusTimesSRing, dA, dB, phases=0, hardThreshold=hard, selectNum=select,
+                                   recoverNum=recover, recoverPct=pct, on_phase=keep)
+    assert phases >= 2  # the product does not fit one phase: the phase loop is exercised
+    h = dA.seq.to_host()
+    d = H.Dcsc(h.m, h.n, h.jc, h.cp, h.ir, h.num)
+    del h
+    idx = np.concatenate([np.arange(d.cp[j], d.cp[j + 1]) for j in sample])
+    lens = np.array([d.cp[j + 1] - d.cp[j] for j in sample])
+    Bs = H.Dcsc(n, ncheck, np.arange(ncheck), np.concatenate([[0], np.cumsum(lens)]), d.ir[idx], d.num[idx])
+    dev = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dA.seq,
+                               cb.SpDCCols.from_host(ctx, cb.HostDcsc(Bs.m, Bs.n, Bs.jc, Bs.cp, Bs.ir, Bs.num))).to_host()
+    devC = H.Dcsc(dev.m, dev.n, dev.jc, dev.cp, dev.ir, dev.num)
+    ora = oracle.spgemm(d, Bs, "plus_times", "hybrid", threads=8)
+    H.assert_dcsc_equal(devC, ora, rtol=1e-12, msg="C5 expansion, sampled columns")
+    pruned = AO.mcl_prune_recovery_select(devC, hard, select, recover, pct)
+    for i, j in enumerate(sample):
+        s = np.searchsorted(pruned.jc, i)
+        present = s < pruned.jc.size and pruned.jc[s] == i
+        er = pruned.ir[pruned.cp[s]:pruned.cp[s + 1]] if present else np.zeros(0, np.int32)
+        ev = pruned.num[pruned.cp[s]:pruned.cp[s + 1]] if present else np.zeros(0)
+        gr, gv = got.get(int(j), (np.zeros(0, np.int32), np.zeros(0)))
+        assert np.array_equal(gr, er), f"column {j}: pruned rows differ ({gr.size} vs {er.size})"
+        assert np.allclose(gv, ev, rtol=1e-12, atol=0), f"column {j}: pruned values differ"
+    for X in (dA.seq, dB.seq):
+        be.free(X)
+
+
+def test_c4_tc_scale22_dot_vs_expand(ctx):
+    from combblas_amd.apps import MaskedSpGEMM, TCLower
+    from combblas_amd.semirings import PlusTimesSRing
+
+    sys.path.insert(0, H.REPO)
+    from bench_tc import host_check
+
+    L, L2 = TCLower(ctx, 22, 16), TCLower(ctx, 22, 16)
+    Cd = MaskedSpGEMM(PlusTimesSRing, L, L2, L, method="dot")
+    tri = int(Cd.tensors()[3].sum().item())
+    sd, dd = Cd.checksum()
+    Ce = MaskedSpGEMM(PlusTimesSRing, L, L2, L, method="expand")
+    se, de = Ce.checksum()
+    assert (Cd.nnz, tri, sd, dd) == (Ce.nnz, int(Ce.tensors()[3].sum().item()), se, de)
+    assert tri > 0
+    Ce.free()
+    checked, bad = host_check(L, Cd, 200)
+    assert checked == 200 and bad == 0
+    for X in (Cd, L, L2):
+        X.free()

@@ -2,15 +2,15 @@
 that faulted ("What's weak" 2):
 
 1. A large numeric HASH sub-tile that inserts without a probe overflow but occupies more slots
-   than the commit queue holds (WIN = U*BS = 4096 of the TA = 4160 slots). It must be retried with
-   half the row range from the cursors BEFORE the segment scan (fixed in 633d2f2; before, the
-   retry read out of range). Construction, for TNumLarge (T 4096, 512 threads, U 8):
-     one output column with 4101 outputs: rows 64*m (m < 4100) plus one row at 3*X - 1,
-     X = 4100*64 = 262400 -> one task (4101 products <= kTaskFlops) spanning 787200 rows;
-     dense_subtiles(4101, 787200, ...) = 0 (6 bitmap sub-tiles > 5/4 of 3 hash sub-tiles), so it
-     runs on the hash kernel with R = ceil(4101 / 2048) = 3 sub-tiles of 262400 rows; the first
-     holds all 4100 evenly spaced rows (slot = 64*m*4096/262400: at most 2 rows per home slot,
-     probes of 1-2) -> 4100 occupied slots > 4096 queue entries, no probe overflow -> retry.
+   than the commit queue holds (the queue holds WIN = U*BS entries, the table T + 64 slots). It
+   must be retried with half the row range from the cursors BEFORE the segment scan (fixed in
+   633d2f2; before, the retry read out of range). Construction from the shipped configuration
+   (cbh_hash_config; T 2048, 512 threads, U 4 -> WIN 2048 of 2112 slots): K = WIN + 4 rows
+   64*m (m < K) plus one row at 3*X - 1, X = 64*K -> one task of K + 1 outputs spanning 3X rows,
+   R = ceil((K + 1) / (T / 2)) = 3 hash sub-tiles of X rows (dense_subtiles prices it hash: the
+   bitmap form needs more sub-tiles); the first holds the K evenly spaced rows (slot =
+   64*m*T/X = m*T/K: at most 2 rows per home slot) -> K occupied slots > WIN queue entries, no
+   probe overflow -> retry (the counter cbh_ctx_take_retries must see it).
    Variants: the column's products from ONE B entry (cursors in LDS) and from 600 B entries
    (> EMAX = 512: chunked, cursors double-buffered in HBM); f64 and int64 values.
 2. The TC dot-form piece kernels are wave-strided with a capped grid (an AQL dispatch counts
@@ -28,14 +28,26 @@ import helpers as H
 
 pytestmark = pytest.mark.gpu
 
-X = 4100 * 64  # rows of the first hash sub-tile
+def _queue_rows():
+    """K = the commit queue + 4 (see the module docstring), from the library's configuration"""
+    import ctypes
+
+    from combblas_amd._lib import lib
+
+    T, bs, u = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    lib().cbh_hash_config(ctypes.byref(T), ctypes.byref(bs), ctypes.byref(u))
+    K = bs.value * u.value + 4
+    assert K <= T.value + 64 and -(-(K + 1) // (T.value // 2)) == 3, (T.value, bs.value, u.value)
+    return K
 
 
 def _queue_overflow_operands(nentries, dtype, seed):
     rng = np.random.default_rng(seed)
+    K = _queue_rows()
+    X = 64 * K  # rows of the first hash sub-tile
     m = 3 * X
-    rows = np.concatenate([np.arange(4100, dtype=np.int64) * 64, [m - 1]])
-    owner = np.concatenate([np.arange(4100) % nentries, [nentries - 1]])  # A column of each row
+    rows = np.concatenate([np.arange(K, dtype=np.int64) * 64, [m - 1]])
+    owner = np.concatenate([np.arange(K) % nentries, [nentries - 1]])  # A column of each row
     order = np.lexsort((rows, owner))
     rows, owner = rows[order], owner[order]
     vals = rng.integers(1, 9, rows.size).astype(dtype) * (1 if dtype == np.int64 else 0.5)
@@ -61,9 +73,9 @@ def test_hash_commit_queue_only_overflow(ctx, oracle, nentries, dtype):
     h = C.to_host()
     got = H.Dcsc(h.m, h.n, h.jc, h.cp, h.ir, h.num)
     exp = oracle.spgemm(A, B, "plus_times", "hybrid")
-    assert exp.nnz == 4101
+    assert exp.nnz == _queue_rows() + 1
     H.assert_dcsc_equal(got, exp, msg=f"queue-only overflow, {nentries} B entries, {np.dtype(dtype).name}")
-    # the retry path fired: the first sub-tile (4100 occupied slots > the 4096-entry queue) was
+    # the retry path fired: the first sub-tile (K occupied slots > the K - 4 queue entries) was
     # redone with half its rows
     assert retries >= 1, "the commit-queue overflow did not trigger a sub-tile retry"
     for S in (C, dA, dB):

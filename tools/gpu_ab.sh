@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of runtime switches on the default bench line: one bench run (3 timed steps, no CPU baseline,
 # no merge sample) per argument, each argument a space-separated list of VAR=value settings.
-#   gpurun -- bash tools/gpu_ab.sh TAG "CBH_DRATIO4=4" "CBH_DRATIO4=6"
+#   gpurun -- bash tools/gpu_ab.sh TAG "" "CBH_LIB=h2048"   (product vs a build variant, combblas_amd/build.py --variant)
 set -o pipefail
 TAG=$1
 shift
