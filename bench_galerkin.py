@@ -17,7 +17,7 @@ roofline: the task-kernel class with the most HIP-event time over the timed step
 bytes (12 B per B entry, product and output, + 16 B per task) / its duration.
 CPU baseline ("reference"): GalerkinNew.cpp's own two PSpGEMM calls (oracle/_ref/ref_harness
 galerkin, built from the reference sources) on a column sample of R (every --cpu-stride-th coarse
-column: SAT(:, J) = Rᵀ(A R(:, J)) exactly), one warm-up and the median of 3, 1 rank x host cores.
+column: SAT(:, J) = Rᵀ(A R(:, J)) exactly), one warm-up and the median of 5, 1 rank x host cores.
     python bench_galerkin.py [--nx 256] [--steps 3] [--warmup 1] [--cpu-stride 4]
 """
 from __future__ import annotations
@@ -46,7 +46,7 @@ def closed_form_sum(A, R):
     return float(np.dot(s, t))
 
 
-def reference_baseline(A, R, stride, reps=3):
+def reference_baseline(A, R, stride, reps=5):
     """GalerkinNew.cpp:99-106 (S = R', AT = PSpGEMM(A, R_s), SAT = PSpGEMM(S, AT)) by the reference
     itself on R's columns c % stride == 0, 1 rank x host cores; None when oracle/_ref is absent"""
     import subprocess

@@ -19,7 +19,7 @@ split long columns into different chunk sums).
 roofline: the task-kernel class with the most HIP-event time over the timed steps (bench.py's
 kernel_roofline). CPU baseline ("reference"): MCL.cpp's own expansion call MemEfficientSpGEMM
 with MCLPruneRecoverySelect (oracle/_ref/ref_harness mclexp, built from the reference sources) on
-every --cpu-stride-th column of the right operand, 1 rank x host cores, median of 3 after a warm-up.
+every --cpu-stride-th column of the right operand, 1 rank x host cores, median of 5 after a warm-up.
     python bench_mcl.py [--log2n 24] [--deg 100] [--steps 2] [--warmup 1] [--host-gen]
 """
 from __future__ import annotations
@@ -62,7 +62,7 @@ def reference_baseline(A, flops, stride):
         fa = os.path.join(td, "A.cbm")
         H.write_cbm(fa, H.Dcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num))
         env = dict(os.environ, OMP_NUM_THREADS=str(cores), LD_LIBRARY_PATH="/usr/lib/x86_64-linux-gnu:/opt/conda/lib")
-        r = subprocess.run([ref, "mclexp", fa, str(stride), "3", str(HARD), str(SELECT), str(RECOVER), str(PCT)],
+        r = subprocess.run([ref, "mclexp", fa, str(stride), "5", str(HARD), str(SELECT), str(RECOVER), str(PCT)],
                            env=env, cwd="/tmp", capture_output=True, text=True, timeout=900)
     line = [x for x in r.stdout.splitlines() if x.startswith("{")]
     if r.returncode != 0 or not line:
@@ -119,7 +119,7 @@ def cpp_line(args):
                             "sample": f"the reference's stock MemEfficientSpGEMM + MCLPruneRecoverySelect (OpenMP "
                                       f"kernels, same harness, 1 rank) on B = A's {d['cpu_cols']} columns c % "
                                       f"{d['cpu_stride']} == 0 ({d['cpu_flops']} multiplies, {d['cpu_kept']} kept): "
-                                      f"median of 3 after 1 warm-up = {d['cpu_s']:.3f} s"},
+                                      f"median of 5 after 1 warm-up = {d['cpu_s']:.3f} s"},
            "check": {"sample_columns": d["check_cols"], "reference": "stock MemEfficientSpGEMM + prune on the sampled "
                                                                        "columns (rows exact, values 1e-12 relative)",
                      "row_mismatches": d["row_mismatches"], "value_mismatches": d["value_mismatches"],

@@ -82,7 +82,7 @@ def cpu_baseline(scale):
         return None
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     env = dict(os.environ, OMP_NUM_THREADS=str(cores), LD_LIBRARY_PATH="/usr/lib/x86_64-linux-gnu:/opt/conda/lib")
-    r = subprocess.run([ref, "tc", str(scale), "-", "-"], env=env, cwd="/tmp", capture_output=True, text=True,
+    r = subprocess.run([ref, "tc", str(scale), "-", "-", "5"], env=env, cwd="/tmp", capture_output=True, text=True,
                        timeout=900)
     line = [x for x in r.stdout.splitlines() if x.startswith("{")]
     if r.returncode != 0 or not line:
@@ -108,7 +108,8 @@ def cpu_baseline(scale):
     return {"value": round(probes / d["tc_s"] / 1e9, 6), "unit": "Gprobe/s", "cores": d["threads"],
             "kind": "reference",
             "sample": f"TC.cpp's flow at R-MAT scale {scale} (Mult_AnXBn_Synch(L, L) + EWiseMult + Reduce, 1 rank x "
-                      f"{d['threads']} threads, oracle/_ref built from the reference sources): {d['tc_s']:.3f} s "
+                      f"{d['threads']} threads, oracle/_ref built from the reference sources): median of {d.get('reps', 1)} after 1 warm-up = "
+                      f"{d['tc_s']:.3f} s "
                       f"({flops} unmasked products = {2.0 * flops / d['tc_s'] / 1e9:.4f} GFLOP/s; that problem has "
                       f"{probes} dot-form probes), triangles {d['triangles']}",
             "same_size": {"scale": scale, "gpu_ms_per_step": round(gdt * 1e3, 3), "gpu_triangles": tri,

@@ -894,9 +894,11 @@ static int launch_task_diag(cbh_ctx* ctx, const TaskArgs& a, const BinLists& bl,
                    hs[12], tot / std::max(1ull, hs[12]), 100 * hs[0] / tot, 100 * hs[1] / tot, 100 * hs[2] / tot,
                    100 * hs[3] / tot, 100 * hs[4] / tot, 100 * hs[5] / tot, 100 * hs[8] / tot, 100 * hs[9] / tot,
                    100 * hs[10] / tot, 100 * hs[6] / tot, 100 * hs[7] / tot);
-      std::fprintf(stderr, "[cbh stamps]   entry-visits=%llu active=%llu (%.1f%%) short=%llu (%.1f%% of active) short-products=%llu (%.1f%%) committed=%llu\n",
+      char pshare[48] = "n/a: dense windows count no products";  // (products are counted by the hash kernels)
+      if (hs[15]) std::snprintf(pshare, sizeof(pshare), "%.1f%%", 100.0 * hs[19] / hs[15]);
+      std::fprintf(stderr, "[cbh stamps]   entry-visits=%llu active=%llu (%.1f%%) short=%llu (%.1f%% of active) short-products=%llu (%s) committed=%llu\n",
                    hs[16], hs[17], 100.0 * hs[17] / std::max(1ull, hs[16]), hs[18], 100.0 * hs[18] / std::max(1ull, hs[17]),
-                   hs[19], 100.0 * hs[19] / std::max(1ull, hs[15]), hs[20]);
+                   hs[19], pshare, hs[20]);
     }
 #endif
     (void)hipEventDestroy(e0);

@@ -62,6 +62,15 @@ class Context:
     """One HIP device + stream for the hot path (the reference's one-rank-one-thread model)."""
 
     def __init__(self, device: int = 0, torch_allocator: bool = True, stream=None):
+        # torch ships its own HIP runtime (torch/lib/libamdhip64.so) beside the one this library links
+        # (/opt/rocm): torch's must initialise first, or its later first use in the process finds no
+        # device (seen on the GPU box: torch.cuda.Stream after a torch-free Context)
+        try:
+            torch = _torch()
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except ImportError:
+            pass
         L = lib()
         h = ctypes.c_void_p()
         check(L.cbh_ctx_create(device, ctypes.byref(h)))

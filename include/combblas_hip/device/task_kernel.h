@@ -296,8 +296,13 @@ __device__ __forceinline__ int rank_commit_batch(const int32_t* keys, const type
   const bool valid = q < qtot;
   const int sq = valid ? (int)Q[q] : -4;
   const int32_t key = valid ? keys[sq] : kNoRow;
+#ifdef CBH_RANK_DPP
+  const int sup = __builtin_amdgcn_update_dpp(-10, sq, 0x138, 0xf, 0xf, false);
+  const int sdn = __builtin_amdgcn_update_dpp(-10, sq, 0x130, 0xf, 0xf, false);
+#else
   const int sup = __shfl_up(sq, 1);
   const int sdn = __shfl_down(sq, 1);
+#endif
   const int sprev = lane == 0 ? (b0 > 0 ? (int)Q[b0 - 1] : -10) : sup;
   const int snext = (q + 1 < qtot) ? (lane == 63 ? (int)Q[q + 1] : sdn) : -10;
   const uint64_t mstart = __ballot(valid && sq != sprev + 1);
@@ -311,6 +316,20 @@ __device__ __forceinline__ int rank_commit_batch(const int32_t* keys, const type
   // keys of the run inside the batch: four shuffles in flight per exit test (runs average
   // 2.5 slots, but the batch's longest -- about 11 at fill 1/2 -- sets the trip count)
   int rank = 0;
+#ifdef CBH_RANK_DPP
+  // the run's other keys arrive by whole-wave DPP shifts (v_mov_dpp wave_shr:1 / wave_shl:1: VALU
+  // moves, no LDS round trip): at distance d, lane l compares the keys of lanes l - d and l + d
+  {
+    int32_t up = key, dn = key;
+    for (int d = 1;; ++d) {
+      if (__ballot(valid && (lane - d >= lo_l || lane + d <= hi_l)) == 0ull) break;
+      up = __builtin_amdgcn_update_dpp(kNoRow, up, 0x138, 0xf, 0xf, false);  // from lane - 1
+      dn = __builtin_amdgcn_update_dpp(kNoRow, dn, 0x130, 0xf, 0xf, false);  // from lane + 1
+      rank += (valid && lane - d >= lo_l && up < key) ? 1 : 0;
+      rank += (valid && lane + d <= hi_l && dn < key) ? 1 : 0;
+    }
+  }
+#else
   for (int j = 0;; j += 4) {
     if (__ballot(valid && lo_l + j <= hi_l) == 0ull) break;
     const int32_t k0 = __shfl(key, (lo_l + j) & 63);
@@ -324,6 +343,7 @@ __device__ __forceinline__ int rank_commit_batch(const int32_t* keys, const type
       rank += (lo_l + j + 3 <= hi_l && k3 < key) ? 1 : 0;
     }
   }
+#endif
   int rstart = b0 + lo_l;
   if (valid && rs < 0) {  // the run began in an earlier batch
     int qq = b0 - 1;

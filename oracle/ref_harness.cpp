@@ -17,7 +17,8 @@
 //                                                     Mult_AnXBn_Synch on any square rank count; JSON
 //   digest <scale> <ef> <block> <sr>                 digest + value sum of the whole C = A*A by column
 //                                                     blocks of B (LocalHybridSpGEMM), one JSON line per block
-//   tc    <scale> <L.cbm> <C.cbm>                     Applications/TC.cpp:62-121 on one rank (C = (L*L).*L)
+//   tc    <scale> <L.cbm> <C.cbm> [reps]              Applications/TC.cpp:62-121 on one rank (C = (L*L).*L);
+//                                                     reps: warm-up + median of reps timed passes
 //   mcl   <A.cbm> <out.cbm> <hard> <select> <recover> <pct>
 //                                                     MCLPruneRecoverySelect (ParFriends.h:185-353)
 //   galerkin <A.cbm> <R.cbm> <stride> <reps>          CPU baseline of C3: GalerkinNew.cpp:99-106's
@@ -345,7 +346,7 @@ static int do_digest(int scale, int ef, int64_t block) {
 // Applications/TC.cpp:62-121 on one rank (global = local indices): symmetrise, set values to 1,
 // L = tril with the upper entries kept as explicit zeros, C = (L*L) .* L, triangles = sum(C).
 // Writes L and C, prints the triangle count.
-static int do_tc(int scale, const std::string& fl, const std::string& fc) {
+static int do_tc(int scale, const std::string& fl, const std::string& fc, int reps) {
   typedef SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>> Mat;
   Mat* A = gen_rmat(scale, 16);
   A->RemoveLoops();
@@ -358,19 +359,34 @@ static int do_tc(int scale, const std::string& fl, const std::string& fc) {
     for (auto nzit = L.seq().begnz(colit); nzit != L.seq().endnz(colit); ++nzit)
       if (nzit.rowid() < colit.colid()) nzit.value() = 0;
   Mat Lt = L;
-  // TC.cpp:108-115 timed: the product, the mask and the reduction (the CPU baseline of bench_tc.py)
-  MPI_Barrier(MPI_COMM_WORLD);
-  const double t0 = MPI_Wtime();
-  Mat C = Mult_AnXBn_Synch<PlusTimesSRing<int64_t, int64_t>, int64_t, SpDCCols<int64_t, int64_t>>(L, Lt);
-  C.EWiseMult(L, false);
-  FullyDistVec<int64_t, int64_t> tri = C.Reduce(Column, std::plus<int64_t>(), static_cast<int64_t>(0));
-  const int64_t result = tri.Reduce(std::plus<int64_t>(), static_cast<int64_t>(0));
-  MPI_Barrier(MPI_COMM_WORLD);
-  const double tc_s = MPI_Wtime() - t0;
+  // TC.cpp:108-115 timed: the product, the mask and the reduction (the CPU baseline of bench_tc.py);
+  // reps > 0: one untimed warm-up pass, then the median of `reps` timed passes
+  auto pass = [&](Mat& C, int64_t& result) {
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double t0 = MPI_Wtime();
+    C = Mult_AnXBn_Synch<PlusTimesSRing<int64_t, int64_t>, int64_t, SpDCCols<int64_t, int64_t>>(L, Lt);
+    C.EWiseMult(L, false);
+    FullyDistVec<int64_t, int64_t> tri = C.Reduce(Column, std::plus<int64_t>(), static_cast<int64_t>(0));
+    result = tri.Reduce(std::plus<int64_t>(), static_cast<int64_t>(0));
+    MPI_Barrier(MPI_COMM_WORLD);
+    return MPI_Wtime() - t0;
+  };
+  Mat C;
+  int64_t result = 0;
+  std::vector<double> ts;
+  if (reps > 0) pass(C, result);
+  for (int r = 0; r < (reps > 0 ? reps : 1); ++r) {
+    Mat Cr;
+    ts.push_back(pass(Cr, result));
+    if (r == 0) C = Cr;
+  }
+  std::sort(ts.begin(), ts.end());
+  const double tc_s = ts[ts.size() / 2];
   if (!fl.empty() && fl != "-") cbm::write(fl, from_spdccols<int64_t>(L.seq()));
   if (!fc.empty() && fc != "-") cbm::write(fc, from_spdccols<int64_t>(C.seq()));
-  std::printf("{\"triangles\": %lld, \"nnzL\": %lld, \"nnzC\": %lld, \"tc_s\": %.6f, \"threads\": %d}\n",
-              (long long)result, (long long)L.getnnz(), (long long)C.getnnz(), tc_s, omp_get_max_threads());
+  std::printf("{\"triangles\": %lld, \"nnzL\": %lld, \"nnzC\": %lld, \"tc_s\": %.6f, \"reps\": %d, \"threads\": %d}\n",
+              (long long)result, (long long)L.getnnz(), (long long)C.getnnz(), tc_s, (int)ts.size(),
+              omp_get_max_threads());
   delete A;
   return 0;
 }
@@ -563,7 +579,8 @@ static int run(int argc, char** argv) {
     std::string sr = argv[5];
     DISPATCH_SR(sr, (do_digest<SR, NT>(std::atoi(argv[2]), std::atoi(argv[3]), std::atoll(argv[4]))));
   }
-  if (mode == "tc" && argc == 5) return do_tc(std::atoi(argv[2]), argv[3], argv[4]);
+  if (mode == "tc" && (argc == 5 || argc == 6))
+    return do_tc(std::atoi(argv[2]), argv[3], argv[4], argc == 6 ? std::atoi(argv[5]) : 0);
   if (mode == "mcl" && argc == 8)
     return do_mcl(argv[2], argv[3], std::atof(argv[4]), std::atoll(argv[5]), std::atoll(argv[6]), std::atof(argv[7]));
   if (mode == "galerkin" && argc == 6) return do_galerkin(argv[2], argv[3], std::atoll(argv[4]), std::atoi(argv[5]));
