@@ -1074,7 +1074,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
     }
   }
   if (!count_only) {  // stored row bitmaps of the dense candidates, within CBH_BMP_FRAC (default 0.4) of the HBM
-    using CD = TaskCfg<PlusTimesD<double>, TNumLarge::T, TNumLarge::BS, TNumLarge::EMAX, TNumLarge::U, MODE_TDENSE>;
+    using CD = TaskCfg<PlusTimesD<double>, kSplitHashT, TNumLarge::BS, TNumLarge::EMAX, TNumLarge::U, MODE_TDENSE>;  // split pricing
     int64_t* bw;
     unsigned long long* cw;
     CBH_TRY(S.get(&bw, nt + 1));
@@ -1152,7 +1152,7 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
   if (t1 <= t0) return CBH_OK;
   // tasks whose sub-tiles fit a bitmap run the dense (bitmap-rank) kernel, the rest the hash
   // kernels (task_kernel.h dense_subtiles: the same plan the kernel re-derives)
-  using CD = TaskCfg<SR, TNumLarge::T, TNumLarge::BS, TNumLarge::EMAX, TNumLarge::U, MODE_TDENSE>;
+  using CD = TaskCfg<SR, kSplitHashT, TNumLarge::BS, TNumLarge::EMAX, TNumLarge::U, MODE_TDENSE>;  // split pricing
   const int64_t nt = t1 - t0;
   int64_t *wd, *wh;
   CBH_TRY(S.get(&wd, nt));
@@ -2023,7 +2023,7 @@ int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   CBH_TRY(new_result(ctx, p->S, P, p->A->m, p->B->n, P.total_nnz, P.nzcB, dtype, C, value_bytes));
   // bins: dense (built-in, lock-free semirings only), then hash large / small
-  using CD = TaskCfg<PlusTimesD<double>, TNumLarge::T, TNumLarge::BS, TNumLarge::EMAX, TNumLarge::U, MODE_TDENSE>;
+  using CD = TaskCfg<PlusTimesD<double>, kSplitHashT, TNumLarge::BS, TNumLarge::EMAX, TNumLarge::U, MODE_TDENSE>;  // split pricing
   const int64_t nt = P.ntasks;
   int64_t *wd, *wh;
   CBH_TRY(p->S.get(&wd, nt));

@@ -41,7 +41,8 @@ struct TNumSmall { static constexpr int T = 512, BS = 128, EMAX = 256, U = 4; };
 #define CBH_DENSE_U 8
 #endif
 struct TNumLarge { static constexpr int T = CBH_DENSE_T, BS = 512, EMAX = 512, U = CBH_DENSE_U; };
-// the hash sub-tile size the dense split rule prices a task's hash alternative with (dense_subtiles)
+// the table size the dense split rule prices a task with (dense_subtiles: the hash alternative's
+// sub-tiles and the dense windows' CAPD / NWB), independent of the kernels' own table sizes
 constexpr int64_t kSplitHashT = 4096;
 // the library's large hash bin (MODE_TNUM; the dense windows keep TNumLarge): a 2048-slot table
 // and 4 products per thread per window keep a group at 53 KB of LDS and <= 80 VGPRs, so THREE
@@ -57,7 +58,10 @@ constexpr int64_t kSplitHashT = 4096;
 #ifndef CBH_HASH_U
 #define CBH_HASH_U 4
 #endif
-struct TNumHash { static constexpr int T = CBH_HASH_T, BS = CBH_HASH_BS, EMAX = 512, U = CBH_HASH_U; };
+#ifndef CBH_HASH_EMAX
+#define CBH_HASH_EMAX 512
+#endif
+struct TNumHash { static constexpr int T = CBH_HASH_T, BS = CBH_HASH_BS, EMAX = CBH_HASH_EMAX, U = CBH_HASH_U; };
 // mid-size hash tasks (kSmallCap < outputs <= kMidCap) of the library's A^2 path: a quarter of the
 // large kernel's LDS, so four workgroups share a CU and the per-task setup latency overlaps
 constexpr int kMidOut = 1024;  // (512 / 2048 measured no better)
@@ -101,7 +105,7 @@ constexpr int64_t kMidCap = kMidOut;  // ... with <= kMidCap the mid kernel (lib
 constexpr int64_t kSymMidCap = kSymMid;  // symbolic tasks with <= kSymMidCap products: the mid kernel
 static_assert(kChunkMin <= TSymSmall::EMAX && kChunkMin <= TSymMid::EMAX && kChunkMin <= TSymLarge::EMAX &&
                   kChunkMin <= TNumSmall::EMAX && kChunkMin <= TNumMid::EMAX &&
-                  kChunkMin <= TNumLarge::EMAX,
+                  kChunkMin <= TNumLarge::EMAX && kChunkMin <= TNumHash::EMAX,
               "every chunked task needs HBM cursor state");
 
 // Launches task_kernel<SR, CFG, MODE> over order[first, first+count) on `stream`, in grid slices

@@ -14,7 +14,7 @@ echo "== $(date +%T) C5 python"
 timeout -k 10 600 python -u bench_mcl.py --no-cpu-baseline > $OUT/bench_mcl_py.json 2> $OUT/bench_mcl_py.err || { tail -30 $OUT/bench_mcl_py.err; exit 1; }
 cat $OUT/bench_mcl_py.json
 echo "== $(date +%T) A/B"
-bash tools/gpu_ab.sh r4e "" "CBH_LIB=dpp" "CBH_LIB=tf64k" "CBH_LIB=tf256k" "CBH_LIB=dr4" "CBH_LIB=dr7"
+bash tools/gpu_ab.sh r4e "" "CBH_LIB=dpp" "CBH_LIB=tf64k" "CBH_LIB=tf256k" "CBH_LIB=dr4" "CBH_LIB=dr7" "CBH_LIB=e256" "CBH_LIB=e256u2" "CBH_LIB=d2k" "CBH_LIB=d2ku8"
 echo "== $(date +%T) stamps"
 bash tools/gpu_stamps.sh r4e/st stamps 22
 echo "== $(date +%T) done"
