@@ -139,6 +139,8 @@ SIGNATURES = {
                                          ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_mat_col_concat": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                           ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_mat_col_concat_consume": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                                  ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_tuples_to_dcsc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                           ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),

@@ -638,7 +638,10 @@ static int check_err(cbh_ctx* ctx) {
 // with about kTaskFlops products each (S_j = 1 for light columns). Tasks of a column are
 // consecutive and in row order, so the exclusive scan of the per-task counts gives every task
 // its output offset and C's column pointers are the offsets of each column's first task.
-constexpr int64_t kTaskFlops = 131072;  // (65536 / 262144: 121.8 / 124.9 vs 124.8 GFLOP/s at scale 22)
+// (round 3: 65536 / 262144 vs 131072 -> 121.8 / 124.9 vs 124.8 GFLOP/s at scale 22; round 4 with the
+// 2048-slot hash table: 133.7 / 140.3 vs 139.5, symbolic 221 / 184 vs 194 ms)
+constexpr int64_t kTaskFlops = 262144;
+constexpr int64_t kMergeTaskFlops = 131072;  // merge tasks (list entries per task; not re-measured)
 
 // Row blocks: C's rows are cut into blocks of RB rows (kRowBlocks blocks); interior task
 // boundaries of a split column sit on block boundaries, where the row-block table of A gives
@@ -2238,7 +2241,7 @@ int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* p
     hipLaunchKernelGGL(merge_work_kernel, dim3(blocks_for(ncols, 256)), dim3(256), 0, ctx->stream, seg_start, seg_len,
                        nlists, lr, ncols, work, rmin, rmax);
     CBH_HIP(ctx, hipGetLastError());
-    // task-parallel merge: every union column becomes row-range tasks of ~kTaskFlops list
+    // task-parallel merge: every union column becomes row-range tasks of ~kMergeTaskFlops list
     // entries (as the SpGEMM's columns), symbolic -> scan -> numeric on the task kernels in
     // merge mode (entries = the lists' segments of the column; task_kernel.h MERGE)
     const int32_t RB = (int32_t)std::max<int64_t>(1, (P0->m + kRowBlocks - 1) / kRowBlocks);
@@ -2249,7 +2252,7 @@ int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* p
     hipLaunchKernelGGL(iota_scaled_kernel, dim3(blocks_for(ncols + 1, 256)), dim3(256), 0, ctx->stream, bcp, ncols + 1,
                        (int64_t)nlists);
     hipLaunchKernelGGL(task_count_kernel, dim3(blocks_for(ncols, 256)), dim3(256), 0, ctx->stream, work, rmin, rmax,
-                       ncols, kTaskFlops, RB, scnt);
+                       ncols, kMergeTaskFlops, RB, scnt);
     CBH_HIP(ctx, hipMemsetAsync(scnt + ncols, 0, sizeof(int64_t), ctx->stream));
     CBH_TRY(exclusive_scan_i64(ctx, S, scnt, tstart, ncols + 1));
     int64_t ntasks = 0;
@@ -2884,6 +2887,94 @@ int cbh_mat_col_concat(cbh_ctx* ctx, int k, const cbh_mat* const* parts, cbh_mat
   CBH_HIP(ctx, hipMemcpyAsync(C->cp + nzc, &nnz, sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // nnz is a host local
   CBH_HIP(ctx, hipGetLastError());
+  *out = C;
+  return CBH_OK;
+}
+
+// cbh_mat_col_concat that releases the parts as it goes, one array kind at a time (pointers, then
+// rows, then values): the peak is the parts plus the largest output array, not twice the matrix
+// (a C5 step's pruned pieces are 148 GB; a copying concatenation would need 296 GB beside A and B)
+int cbh_mat_col_concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** out) {
+  if (!ctx || !out || k < 1 || !parts) return fail(ctx, CBH_E_ARG, "bad concat arguments");
+  *out = nullptr;
+  int64_t m = 0, n = 0, nnz = 0, nzc = 0;
+  for (int i = 0; i < k; ++i) {
+    if (!parts[i]) return fail(ctx, CBH_E_ARG, "null block");
+    if (parts[i]->dtype != parts[0]->dtype || parts[i]->vbytes != parts[0]->vbytes)
+      return fail(ctx, CBH_E_ARG, "blocks of different value types");
+    m = std::max(m, parts[i]->m);
+    n += parts[i]->n;
+    nnz += parts[i]->nnz;
+    nzc += parts[i]->nzc;
+  }
+  cbh_mat* C = new cbh_mat;
+  C->m = m;
+  C->n = n;
+  C->nnz = nnz;
+  C->nzc = nzc;
+  C->dtype = parts[0]->dtype;
+  C->vbytes = parts[0]->vbytes;
+  const int64_t vb = C->vbytes;
+  auto release = [&](auto member) {
+    for (int i = 0; i < k; ++i)
+      if (parts[i]->owned) {
+        dfree(ctx, parts[i]->*member);
+        parts[i]->*member = nullptr;
+      }
+  };
+  int rc = dalloc(ctx, &C->cp, nzc + 1);
+  if (rc == CBH_OK) rc = dalloc(ctx, &C->jc, nzc);
+  if (rc != CBH_OK) {
+    cbh_mat_free(ctx, C);
+    return rc;
+  }
+  int64_t coff = 0, eoff = 0, zoff = 0;
+  for (int i = 0; i < k; ++i) {
+    const cbh_mat* P = parts[i];
+    if (P->nzc > 0) {
+      hipLaunchKernelGGL(add_const_i64_kernel, dim3(blocks_for(P->nzc, 256)), dim3(256), 0, ctx->stream, P->cp, P->nzc,
+                         eoff, C->cp + zoff);
+      hipLaunchKernelGGL(add_const_i64_kernel, dim3(blocks_for(P->nzc, 256)), dim3(256), 0, ctx->stream, P->jc, P->nzc,
+                         coff, C->jc + zoff);
+    }
+    coff += P->n;
+    eoff += P->nnz;
+    zoff += P->nzc;
+  }
+  CBH_HIP(ctx, hipGetLastError());
+  release(&cbh_mat::cp);
+  release(&cbh_mat::jc);
+  if ((rc = dalloc(ctx, &C->ir, nnz)) != CBH_OK) {
+    cbh_mat_free(ctx, C);
+    return rc;
+  }
+  eoff = 0;
+  for (int i = 0; i < k; ++i) {
+    if (parts[i]->nnz > 0)
+      CBH_HIP(ctx, hipMemcpyAsync(C->ir + eoff, parts[i]->ir, sizeof(int32_t) * parts[i]->nnz, hipMemcpyDeviceToDevice,
+                                  ctx->stream));
+    eoff += parts[i]->nnz;
+  }
+  release(&cbh_mat::ir);
+  if ((rc = dalloc(ctx, reinterpret_cast<char**>(&C->num), nnz * vb)) != CBH_OK) {
+    cbh_mat_free(ctx, C);
+    return rc;
+  }
+  eoff = 0;
+  for (int i = 0; i < k; ++i) {
+    if (parts[i]->nnz > 0)
+      CBH_HIP(ctx, hipMemcpyAsync(static_cast<char*>(C->num) + eoff * vb, parts[i]->num, (size_t)(parts[i]->nnz * vb),
+                                  hipMemcpyDeviceToDevice, ctx->stream));
+    eoff += parts[i]->nnz;
+  }
+  release(&cbh_mat::num);
+  CBH_HIP(ctx, hipMemcpyAsync(C->cp + nzc, &nnz, sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // nnz is a host local
+  CBH_HIP(ctx, hipGetLastError());
+  for (int i = 0; i < k; ++i) {
+    cbh_mat_free(ctx, parts[i]);
+    parts[i] = nullptr;
+  }
   *out = C;
   return CBH_OK;
 }

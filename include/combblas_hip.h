@@ -333,6 +333,10 @@ int cbh_mcl_prune_recovery_select(cbh_ctx* ctx, const cbh_mat* A, double hardThr
  *                       rows = the largest m, columns offset by the earlier blocks' n            */
 int cbh_mat_col_slice(cbh_ctx* ctx, const cbh_mat* M, int64_t c0, int64_t c1, cbh_mat** out);
 int cbh_mat_col_concat(cbh_ctx* ctx, int k, const cbh_mat* const* parts, cbh_mat** out);
+/* The same, releasing the parts as they are consumed (one array kind at a time: pointers, rows,
+ * values), so the peak is the parts plus the largest output array instead of twice the matrix;
+ * on success every parts[i] is freed and set to NULL. ColConcatenate also empties its inputs. */
+int cbh_mat_col_concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** out);
 /* Rows [r0, r1) of the block as an (r1 - r0) x n block, row ids rebased, empty columns dropped
  * (Mult_AnXBn_DoubleBuff's row halves of B). */
 int cbh_mat_row_slice(cbh_ctx* ctx, const cbh_mat* M, int64_t r0, int64_t r1, cbh_mat** out);

@@ -40,12 +40,11 @@ inline cbh_mat* col_slice(const cbh_mat* M, int64_t c0, int64_t c1) {
   if (rc != CBH_OK) die(context(), rc, "cbh_mat_col_slice");
   return out;
 }
-// ColConcatenate of the blocks (freed)
+// ColConcatenate of the blocks, released as they are consumed (peak: the blocks + one output array)
 inline cbh_mat* col_concat(std::vector<cbh_mat*>& parts) {
   cbh_mat* out = nullptr;
-  int rc = cbh_mat_col_concat(context(), (int)parts.size(), parts.data(), &out);
-  if (rc != CBH_OK) die(context(), rc, "cbh_mat_col_concat");
-  for (cbh_mat* p : parts) cbh_mat_free(context(), p);
+  int rc = cbh_mat_col_concat_consume(context(), (int)parts.size(), parts.data(), &out);
+  if (rc != CBH_OK) die(context(), rc, "cbh_mat_col_concat_consume");
   parts.clear();
   return out;
 }

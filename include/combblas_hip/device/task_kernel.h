@@ -48,9 +48,10 @@ constexpr int kSymFill8 = 4;
 // dense numeric sub-tile capacity in quarters of T: 3 = 3072 values for T = 4096 (2 and 4
 // measured slower: 98.7 / 104.5 vs 105.3 GFLOP/s at scale 22)
 constexpr int kCapD4 = 3;
-// a task runs dense when its dense sub-tiles are at most kDRatio4/4 of its hash sub-tiles (4, 6,
-// 8 and 12 measured no better)
-constexpr int kDRatio4 = 5;
+// a task runs dense when its dense sub-tiles are at most kDRatio4/4 of its hash sub-tiles. Round 4
+// (2048-slot hash table, 262144-flop tasks): 5/6/7/8/10 -> 140.3/142.3/142.7/142.1/141.4 GFLOP/s at
+// scale 22; rounds 2-3 had found 4..12 flat around 5 with the 4096-slot hash table
+constexpr int kDRatio4 = 7;
 
 // Diagnostic build only (-DCBH_STAMPS, libcombblas_hip_stamps.so): thread 0 of every workgroup
 // adds the s_memtime cycles of each kernel phase (delimited by block barriers) into g_stamps.
@@ -296,13 +297,8 @@ __device__ __forceinline__ int rank_commit_batch(const int32_t* keys, const type
   const bool valid = q < qtot;
   const int sq = valid ? (int)Q[q] : -4;
   const int32_t key = valid ? keys[sq] : kNoRow;
-#ifdef CBH_RANK_DPP
-  const int sup = __builtin_amdgcn_update_dpp(-10, sq, 0x138, 0xf, 0xf, false);
-  const int sdn = __builtin_amdgcn_update_dpp(-10, sq, 0x130, 0xf, 0xf, false);
-#else
   const int sup = __shfl_up(sq, 1);
   const int sdn = __shfl_down(sq, 1);
-#endif
   const int sprev = lane == 0 ? (b0 > 0 ? (int)Q[b0 - 1] : -10) : sup;
   const int snext = (q + 1 < qtot) ? (lane == 63 ? (int)Q[q + 1] : sdn) : -10;
   const uint64_t mstart = __ballot(valid && sq != sprev + 1);
@@ -316,20 +312,6 @@ __device__ __forceinline__ int rank_commit_batch(const int32_t* keys, const type
   // keys of the run inside the batch: four shuffles in flight per exit test (runs average
   // 2.5 slots, but the batch's longest -- about 11 at fill 1/2 -- sets the trip count)
   int rank = 0;
-#ifdef CBH_RANK_DPP
-  // the run's other keys arrive by whole-wave DPP shifts (v_mov_dpp wave_shr:1 / wave_shl:1: VALU
-  // moves, no LDS round trip): at distance d, lane l compares the keys of lanes l - d and l + d
-  {
-    int32_t up = key, dn = key;
-    for (int d = 1;; ++d) {
-      if (__ballot(valid && (lane - d >= lo_l || lane + d <= hi_l)) == 0ull) break;
-      up = __builtin_amdgcn_update_dpp(kNoRow, up, 0x138, 0xf, 0xf, false);  // from lane - 1
-      dn = __builtin_amdgcn_update_dpp(kNoRow, dn, 0x130, 0xf, 0xf, false);  // from lane + 1
-      rank += (valid && lane - d >= lo_l && up < key) ? 1 : 0;
-      rank += (valid && lane + d <= hi_l && dn < key) ? 1 : 0;
-    }
-  }
-#else
   for (int j = 0;; j += 4) {
     if (__ballot(valid && lo_l + j <= hi_l) == 0ull) break;
     const int32_t k0 = __shfl(key, (lo_l + j) & 63);
@@ -343,7 +325,6 @@ __device__ __forceinline__ int rank_commit_batch(const int32_t* keys, const type
       rank += (lo_l + j + 3 <= hi_l && k3 < key) ? 1 : 0;
     }
   }
-#endif
   int rstart = b0 + lo_l;
   if (valid && rs < 0) {  // the run began in an earlier batch
     int qq = b0 - 1;

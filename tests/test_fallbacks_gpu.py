@@ -126,3 +126,40 @@ def _consumer_checks(ctx, cb, A, exp, dA, dB, parts, keep, budget):
     # the context is usable afterwards
     st2 = cb.PhasedSpGEMM(cb.PlusTimesSRing, dA, dB, checksum=True, budget_bytes=budget)
     assert (st2["value_sum"], st2["digest"]) == H.digest(exp)
+
+
+def test_consuming_col_concat_matches_copy(ctx):
+    """cbh_mat_col_concat_consume (the C++ phased drivers' ColConcatenate: parts released array kind
+    by array kind, so a C5 step's 148 GB of pruned pieces concatenate within HBM) builds the same
+    block as the copying cbh_mat_col_concat, and frees and clears every part."""
+    import ctypes
+
+    import combblas_amd as cb
+    from combblas_amd._lib import check, lib
+
+    A = cb.rmat(12)
+    dA = cb.SpDCCols.from_host(ctx, A)
+    cuts = [0, 700, 701, 2500, A.n]
+
+    def pieces():
+        out = []
+        for c0, c1 in zip(cuts[:-1], cuts[1:]):
+            h = ctypes.c_void_p()
+            check(lib().cbh_mat_col_slice(ctx.h, dA.h, c0, c1, ctypes.byref(h)), ctx.h)
+            out.append(h.value)
+        return (ctypes.c_void_p * len(out))(*out)
+
+    k = len(cuts) - 1
+    p1, p2 = pieces(), pieces()
+    o1, o2 = ctypes.c_void_p(), ctypes.c_void_p()
+    check(lib().cbh_mat_col_concat(ctx.h, k, p1, ctypes.byref(o1)), ctx.h)
+    check(lib().cbh_mat_col_concat_consume(ctx.h, k, p2, ctypes.byref(o2)), ctx.h)
+    assert all(p2[i] is None for i in range(k)), "consumed parts must be cleared"
+    for i in range(k):
+        check(lib().cbh_mat_free(ctx.h, ctypes.c_void_p(p1[i])), ctx.h)
+    C1, C2 = cb.SpDCCols(ctx, o1), cb.SpDCCols(ctx, o2)
+    h1, h2 = C1.to_host(), C2.to_host()
+    for a, b, ref in ((h1.jc, h2.jc, A.jc), (h1.cp, h2.cp, A.cp), (h1.ir, h2.ir, A.ir), (h1.num, h2.num, A.num)):
+        assert np.array_equal(a, b) and np.array_equal(b, ref)
+    for S in (C1, C2, dA):
+        S.free()

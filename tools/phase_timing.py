@@ -21,10 +21,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     scale = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     ncalls = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-    if os.environ.get("PT_TORCH"):
-        import torch
+    # torch's bundled HIP runtime must initialise before the library's (combblas_amd.Context)
+    import torch
 
-        torch.cuda.set_device(0)
+    torch.cuda.set_device(0)
     import combblas_amd as cb
 
     A = cb.rmat(scale, 16, dtype=np.float64)
