@@ -640,7 +640,10 @@ static int check_err(cbh_ctx* ctx) {
 // its output offset and C's column pointers are the offsets of each column's first task.
 // (round 3: 65536 / 262144 vs 131072 -> 121.8 / 124.9 vs 124.8 GFLOP/s at scale 22; round 4 with the
 // 2048-slot hash table: 133.7 / 140.3 vs 139.5, symbolic 221 / 184 vs 194 ms)
-constexpr int64_t kTaskFlops = 262144;
+#ifndef CBH_TASK_FLOPS  // (A/B hook: build variants only)
+#define CBH_TASK_FLOPS 262144
+#endif
+constexpr int64_t kTaskFlops = CBH_TASK_FLOPS;
 constexpr int64_t kMergeTaskFlops = 131072;  // merge tasks (list entries per task; not re-measured)
 
 // Row blocks: C's rows are cut into blocks of RB rows (kRowBlocks blocks); interior task

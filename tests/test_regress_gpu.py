@@ -6,10 +6,11 @@ that faulted ("What's weak" 2):
    must be retried with half the row range from the cursors BEFORE the segment scan (fixed in
    633d2f2; before, the retry read out of range). Construction from the shipped configuration
    (cbh_hash_config; T 2048, 512 threads, U 4 -> WIN 2048 of 2112 slots): K = WIN + 4 rows
-   64*m (m < K) plus one row at 3*X - 1, X = 64*K -> one task of K + 1 outputs spanning 3X rows,
-   R = ceil((K + 1) / (T / 2)) = 3 hash sub-tiles of X rows (dense_subtiles prices it hash: the
-   bitmap form needs more sub-tiles); the first holds the K evenly spaced rows (slot =
-   64*m*T/X = m*T/K: at most 2 rows per home slot) -> K occupied slots > WIN queue entries, no
+   128*m (m < K) plus one row at 3*X - 1, X = 128*K -> one task of K + 1 outputs spanning 3X rows,
+   R = ceil((K + 1) / (T / 2)) = 3 hash sub-tiles of X rows (dense_subtiles prices it hash: its
+   788 K rows need 6 bitmap windows of 135 K rows, more than 7/4 of the hash sub-tiles); the
+   first holds the K evenly spaced rows (slot = 128*m*T/X = m*T/K: at most 2 rows per home
+   slot) -> K occupied slots > WIN queue entries, no
    probe overflow -> retry (the counter cbh_ctx_take_retries must see it).
    Variants: the column's products from ONE B entry (cursors in LDS) and from 600 B entries
    (> EMAX = 512: chunked, cursors double-buffered in HBM); f64 and int64 values.
@@ -44,9 +45,9 @@ def _queue_rows():
 def _queue_overflow_operands(nentries, dtype, seed):
     rng = np.random.default_rng(seed)
     K = _queue_rows()
-    X = 64 * K  # rows of the first hash sub-tile
+    X = 128 * K  # rows of the first hash sub-tile
     m = 3 * X
-    rows = np.concatenate([np.arange(K, dtype=np.int64) * 64, [m - 1]])
+    rows = np.concatenate([np.arange(K, dtype=np.int64) * 128, [m - 1]])
     owner = np.concatenate([np.arange(K) % nentries, [nentries - 1]])  # A column of each row
     order = np.lexsort((rows, owner))
     rows, owner = rows[order], owner[order]
