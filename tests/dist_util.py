@@ -10,6 +10,7 @@ and returns what rank 0's fn returned.
 """
 from __future__ import annotations
 
+import datetime
 import os
 import socket
 import sys
@@ -182,7 +183,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, fn, args, outdir):
+def _worker(rank, world, port, fn, args, outdir, coll_timeout=200):
     import pickle
 
     import torch.distributed as dist
@@ -190,7 +191,9 @@ def _worker(rank, world, port, fn, args, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     res = None
     try:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # a collective times out (and the rank reports where) before the world's deadline, instead
+        # of waiting gloo's default 30 minutes
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=coll_timeout))
         res = ("ok", fn(rank, world, *args))
         dist.barrier()
         dist.destroy_process_group()
@@ -209,16 +212,29 @@ def run_world(fn, world, *args, timeout=240):
     with tempfile.TemporaryDirectory() as d:
         ctx = mp.get_context("spawn")
         port = _free_port()
-        procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, d)) for r in range(world)]
+        coll_timeout = max(30, timeout - 40)
+        procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, d, coll_timeout)) for r in range(world)]
         for p in procs:
             p.start()
         deadline = time.monotonic() + timeout  # one budget for the whole world, not per rank
         for p in procs:
             p.join(max(0.0, deadline - time.monotonic()))
-        for p in procs:
-            if p.is_alive():
-                p.kill()
-                raise TimeoutError("distributed test timed out")
+        alive = [r for r, p in enumerate(procs) if p.is_alive()]
+        if alive:  # kill EVERY straggler: a live rank left behind blocks the interpreter's exit
+            for r in alive:
+                procs[r].kill()
+            for r in alive:
+                procs[r].join(10)
+            errs = []
+            for r in range(world):
+                path = os.path.join(d, f"r{r}.pkl")
+                if os.path.exists(path):
+                    with open(path, "rb") as f:
+                        st, v = pickle.load(f)
+                    if st != "ok":
+                        errs.append(f"rank {r}: {v}")
+            raise TimeoutError(f"distributed test timed out; ranks still running: {alive}" +
+                               ("".join("\n" + e for e in errs)))
         results = []
         for r in range(world):
             path = os.path.join(d, f"r{r}.pkl")

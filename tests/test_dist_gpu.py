@@ -13,6 +13,18 @@ from dist_util import run_world
 pytestmark = pytest.mark.gpu
 
 
+def _trace(rank, msg):
+    """CBH_TRACE_DIR: each rank appends its progress (flushed) to rank<r>.log there"""
+    import os
+    import time
+
+    d = os.environ.get("CBH_TRACE_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"rank{rank}.log"), "a") as f:
+            f.write(f"{time.time():.3f} {msg}\n")
+
+
 def _gpu_worker(rank, world, scale, tag, mode, phases, budget, layers):
     import torch
 
@@ -23,9 +35,11 @@ def _gpu_worker(rank, world, scale, tag, mode, phases, budget, layers):
     from combblas_amd.semirings import ALL
     from combblas_amd.spparmat import SpParMat, SpParMat3D
 
+    _trace(rank, f"start {tag} {mode}")
     torch.cuda.set_device(0)
     ctx = cb.Context(0)
     be = HipBackend(ctx)
+    _trace(rank, "context")
     A = cb.rmat(scale)
     d = H.values_for(tag, H.Dcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num))
     h = cb.HostDcsc(d.m, d.n, d.jc, d.cp, d.ir, d.num)
@@ -41,6 +55,7 @@ def _gpu_worker(rank, world, scale, tag, mode, phases, budget, layers):
         dA = SpParMat.distribute(h, grid, be)
         dB = SpParMat.distribute(h, grid, be)
         if mode == "synch":
+            _trace(rank, "distributed")
             C = pf.Mult_AnXBn_Synch(SR, dA, dB)
         elif mode == "overlap":
             C = pf.Mult_AnXBn_Overlap(SR, dA, dB)
@@ -48,8 +63,10 @@ def _gpu_worker(rank, world, scale, tag, mode, phases, budget, layers):
             C = pf.Mult_AnXBn_DoubleBuff(SR, dA, dB)
         else:
             C = pf.MemEfficientSpGEMM(SR, dA, dB, phases=phases, perProcessMemory=budget)
+    _trace(rank, "product")
     g = C.gather_host()
     torch.cuda.synchronize()
+    _trace(rank, "gathered")
     ctx.close()
     if rank == 0:
         return (g.m, g.n, g.jc, g.cp, g.ir, g.num)
