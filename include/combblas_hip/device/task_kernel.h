@@ -48,6 +48,18 @@ constexpr int kSymFill8 = 4;
 // dense numeric sub-tile capacity in quarters of T: 3 = 3072 values for T = 4096 (2 and 4
 // measured slower: 98.7 / 104.5 vs 105.3 GFLOP/s at scale 22)
 constexpr int kCapD4 = 3;
+// dense windows keep one int16 prefix popcount per 4 bitmap words instead of per word (4.5 instead
+// of 6 LDS bytes per word: 14 % wider windows; a rank adds the popcounts of up to 3 words of the
+// word's aligned group, read with the word in one 16-byte LDS load)
+#ifdef CBH_DPRE4
+constexpr bool kDensePre4 = true;
+#else
+constexpr bool kDensePre4 = false;
+#endif
+// LDS bytes of a dense window of wl bitmap words with their prefix popcounts
+__host__ __device__ constexpr int64_t dense_window_bytes(int64_t wl) {
+  return kDensePre4 ? 4 * wl + 2 * ((wl + 3) / 4) : 6 * wl;
+}
 // a task runs dense when its dense sub-tiles are at most kDRatio4/4 of its hash sub-tiles. Round 4
 // (2048-slot hash table, 262144-flop tasks): 5/6/7/8/10 -> 140.3/142.3/142.7/142.1/141.4 GFLOP/s at
 // scale 22; rounds 2-3 had found 4..12 flat around 5 with the 4096-slot hash table
@@ -382,8 +394,8 @@ struct TaskCfg {
   static constexpr int CAPD = T / 4 * kCapD4;
   static constexpr size_t o_dvals = o_keys;
   static constexpr size_t o_dbits = al(o_dvals + sizeof(acc_t) * CAPD);
-  static constexpr int NWB = NUM ? (int)((o_pos - o_dbits) / 6) / 8 * 8 : 0;
-  static_assert(!DENSE || o_dbits + 6 * NWB <= o_pos, "dense bitmap and prefix fit the tables");
+  static constexpr int NWB = NUM ? (int)((o_pos - o_dbits) * 2 / (kDensePre4 ? 9 : 12)) / 8 * 8 : 0;
+  static_assert(!DENSE || o_dbits + dense_window_bytes(NWB) <= o_pos, "dense bitmap and prefix fit the tables");
   static constexpr size_t o_end = al(o_pos + sizeof(int64_t) * EMAX);
   static constexpr size_t o_scale = al(o_end + sizeof(int64_t) * EMAX);
   static constexpr size_t o_next = al(o_scale + (NUM ? sizeof(b_t) * EMAX : 0));
@@ -729,7 +741,8 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
     const uint32_t* __restrict__ tb = a.bmp + bw0;
     __shared__ int32_t s_cut;
     constexpr int64_t TB = (int64_t)C::o_pos;
-    int64_t wdes = TB * nwt / ((int64_t)sizeof(acc_t) * work + 6 * nwt);  // words whose outputs fill the rest
+    // words whose outputs fill the rest
+    int64_t wdes = 2 * TB * nwt / (2 * (int64_t)sizeof(acc_t) * work + (kDensePre4 ? 9 : 12) * nwt);
     wdes = wdes < 64 ? 64 : (wdes > C::NWB ? C::NWB : wdes);
     // window ends snap to row-block boundaries when that keeps >= 3/4 of the window
     const bool dalign = kAlignSubtiles && a.RB > 0 && (a.RB & 31) == 0 && (tlo & 31) == 0;
@@ -741,7 +754,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
     int64_t w0 = 0;
     while (w0 < nwt) {
       const int wl = (int)((nwt - w0) < wdes ? (nwt - w0) : wdes);
-      const int dbase = (int)((TB - 6 * wl) & ~int64_t(15));
+      const int dbase = (int)((TB - dense_window_bytes(wl)) & ~int64_t(15));
       uint32_t* dw = reinterpret_cast<uint32_t*>(smem + dbase);
       int16_t* dp = reinterpret_cast<int16_t*>(smem + dbase + 4 * wl);
       const int capv = dbase / (int)sizeof(acc_t);
@@ -771,7 +784,8 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
         const int x = tid * kw + k;
         if (x < wl) {
           const int pc = __popc(dw[x]);
-          dp[x] = (int16_t)(ex < 32767 ? ex : 32767);
+          if (!kDensePre4) dp[x] = (int16_t)(ex < 32767 ? ex : 32767);
+          else if ((x & 3) == 0) dp[x >> 2] = (int16_t)(ex < 32767 ? ex : 32767);
           if (ex <= capv && ex + pc > capv) s_cut = x;
           ex += pc;
         }
@@ -783,7 +797,17 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
         const int64_t cb = (w0 + cut) / dbw * dbw - w0;
         if (cb > 0 && cb * 4 >= 3ll * cut) cut = (int)cb;
       }
-      const int dtotal = cut < wl ? (int)dp[cut] : wtotal;
+      // output rank of the first row of word x (x < the cut: no clamping)
+      auto word_rank = [&](int x) -> int {
+        if constexpr (!kDensePre4) {
+          return dp[x];
+        } else {
+          int r = dp[x >> 2];
+          for (int i = x & ~3; i < x; ++i) r += __popc(dw[i]);
+          return r;
+        }
+      };
+      const int dtotal = cut < wl ? word_rank(cut) : wtotal;
       {  // the next window's words: their loads overlap this window's entry loads
         const int64_t w0n = w0 + cut;
         if (w0n < nwt) {
@@ -806,9 +830,19 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
             bad |= 1 << 8;
             return;
           }
-          const uint32_t wv = dw[d >> 5];
+          uint32_t wv;
+          int wr;
+          if constexpr (!kDensePre4) {
+            wv = dw[d >> 5];
+            wr = dp[d >> 5];
+          } else {  // the word's aligned group of 4 in one LDS load, the group prefix beside it
+            const uint4 q = reinterpret_cast<const uint4*>(dw)[d >> 7];
+            const int wi = (d >> 5) & 3;
+            wv = wi == 0 ? q.x : (wi == 1 ? q.y : (wi == 2 ? q.z : q.w));
+            wr = dp[d >> 7] + (wi > 0 ? __popc(q.x) : 0) + (wi > 1 ? __popc(q.y) : 0) + (wi > 2 ? __popc(q.z) : 0);
+          }
           if (!((wv >> (d & 31)) & 1u)) bad |= 1 << 11;  // a product row the symbolic pass did not mark
-          const int slot = dp[d >> 5] + __popc(wv & ((1u << (d & 31)) - 1u));
+          const int slot = wr + __popc(wv & ((1u << (d & 31)) - 1u));
           SR::lds_acc(&vals[slot], av[u]);
         };
         for (int ch = 0; ch < nchunks; ++ch) {
@@ -841,7 +875,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
             reinterpret_cast<val_t*>(a.Cnum)[out_pos + q] = SR::finalize(vals[q]);
           for (int x = tid; x < cut; x += BS) {
             uint32_t wv = dw[x];
-            int32_t* cr = a.Cir + out_pos + dp[x];
+            int32_t* cr = a.Cir + out_pos + word_rank(x);
             while (wv) {
               *cr++ = lo + 32 * x + __builtin_ctz(wv);
               wv &= wv - 1u;
