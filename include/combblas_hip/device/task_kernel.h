@@ -48,18 +48,6 @@ constexpr int kSymFill8 = 4;
 // dense numeric sub-tile capacity in quarters of T: 3 = 3072 values for T = 4096 (2 and 4
 // measured slower: 98.7 / 104.5 vs 105.3 GFLOP/s at scale 22)
 constexpr int kCapD4 = 3;
-// dense windows keep one int16 prefix popcount per 4 bitmap words instead of per word (4.5 instead
-// of 6 LDS bytes per word: 14 % wider windows; a rank adds the popcounts of up to 3 words of the
-// word's aligned group, read with the word in one 16-byte LDS load)
-#ifdef CBH_DPRE4
-constexpr bool kDensePre4 = true;
-#else
-constexpr bool kDensePre4 = false;
-#endif
-// LDS bytes of a dense window of wl bitmap words with their prefix popcounts
-__host__ __device__ constexpr int64_t dense_window_bytes(int64_t wl) {
-  return kDensePre4 ? 4 * wl + 2 * ((wl + 3) / 4) : 6 * wl;
-}
 // a task runs dense when its dense sub-tiles are at most kDRatio4/4 of its hash sub-tiles. Round 4
 // (2048-slot hash table, 262144-flop tasks): 5/6/7/8/10 -> 140.3/142.3/142.7/142.1/141.4 GFLOP/s at
 // scale 22; rounds 2-3 had found 4..12 flat around 5 with the 4096-slot hash table
@@ -365,6 +353,102 @@ __device__ __forceinline__ int rank_commit_batch(const int32_t* keys, const type
   return bad;
 }
 
+// Run-aligned batches: a wave commits a contiguous queue range [b0, qend) whose ends are run
+// starts, in batches that also end where a run starts, so no run crosses a batch edge and no lane
+// walks LDS key by key (those dependent walks at the edges of fixed 64-entry batches are the
+// longest chains of the commit). `used` returns the entries this batch committed.
+#ifdef CBH_RUNALIGN
+constexpr bool kRunAlign = true;
+#else
+constexpr bool kRunAlign = false;
+#endif
+template <class SR>
+__device__ __forceinline__ int rank_commit_run_batch(const int32_t* keys, const typename SR::acc_t* vals,
+                                                     const int16_t* Q, int qtot, int qend, int b0, int& used,
+                                                     int64_t out_pos, int64_t out_end, int64_t ccap,
+                                                     int32_t* __restrict__ Cir, typename SR::val_t* __restrict__ Cnum) {
+  const int lane = threadIdx.x & 63;
+  int bad = 0;
+  const int q = b0 + lane;
+  // entries are loaded up to the queue's end, so that runs (and their ends) are seen across the
+  // wave's range end; this batch commits the ones before qend and before `limit`
+  const bool loaded = q < qtot;
+  const bool inq = q < qend;
+  const int sq = loaded ? (int)Q[q] : -4;
+  const int32_t key = loaded ? keys[sq] : kNoRow;
+  const int sup = __shfl_up(sq, 1);
+  const int sdn = __shfl_down(sq, 1);
+  const int sprev = lane == 0 ? (b0 > 0 ? (int)Q[b0 - 1] : -10) : sup;
+  const int snext = (q + 1 < qtot) ? (lane == 63 ? (int)Q[q + 1] : sdn) : -10;
+  const uint64_t mstart = __ballot(loaded && sq != sprev + 1);
+  const uint64_t mend = __ballot(loaded && snext != sq + 1);
+  // a full batch inside the range whose last run goes on past it stops where that run starts
+  int limit = 64;
+  if (b0 + 64 <= qend && ((mend >> 63) & 1ull) == 0ull && mstart != 0ull) {
+    const int last = 63 - __clzll(mstart);
+    if (last > 0) limit = last;
+  }
+  used = qend - b0 < limit ? qend - b0 : limit;
+  const bool valid = inq && lane < limit;
+  const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+  const uint64_t below = mstart & upto;
+  const uint64_t above = mend & ~((1ull << lane) - 1ull);
+  const int rs = below ? 63 - __clzll(below) : -1;  // run start lane (-1: before the batch)
+  const int re = above ? __ffsll((long long)above) - 1 : 64;  // run end lane (64: after it)
+  const int lo_l = rs < 0 ? 0 : rs, hi_l = re > 63 ? 63 : re;
+  int rank = 0;
+  for (int j = 0;; j += 4) {
+    if (__ballot(valid && lo_l + j <= hi_l) == 0ull) break;
+    const int32_t k0 = __shfl(key, (lo_l + j) & 63);
+    const int32_t k1 = __shfl(key, (lo_l + j + 1) & 63);
+    const int32_t k2 = __shfl(key, (lo_l + j + 2) & 63);
+    const int32_t k3 = __shfl(key, (lo_l + j + 3) & 63);
+    if (valid) {
+      rank += (lo_l + j <= hi_l && k0 < key) ? 1 : 0;
+      rank += (lo_l + j + 1 <= hi_l && k1 < key) ? 1 : 0;
+      rank += (lo_l + j + 2 <= hi_l && k2 < key) ? 1 : 0;
+      rank += (lo_l + j + 3 <= hi_l && k3 < key) ? 1 : 0;
+    }
+  }
+  int rstart = b0 + lo_l;
+  if (valid && rs < 0) {  // (only when no run start lay near a wave's nominal cut)
+    int qq = b0 - 1;
+    while (qq >= 0 && (int)Q[qq] == (int)Q[qq + 1] - 1) {
+      rank += keys[Q[qq]] < key ? 1 : 0;
+      --qq;
+    }
+    rstart = qq + 1;
+  }
+  if (valid && re > 63) {  // the run goes on past the batch (longer than 64 entries)
+    int qq = b0 + 64;
+    while (qq < qtot && (int)Q[qq] == (int)Q[qq - 1] + 1) {
+      rank += keys[Q[qq]] < key ? 1 : 0;
+      ++qq;
+    }
+  }
+  if (valid) {
+    const int64_t pos = out_pos + rstart + rank;
+    if (pos >= out_end || pos >= ccap || pos < out_pos) {
+      bad |= 1 << 5;
+    } else {
+      Cir[pos] = key;
+      Cnum[pos] = SR::finalize(vals[sq]);
+    }
+  }
+  return bad;
+}
+// the first run start at or after queue index nom (wave-uniform); nom itself when none lies within
+// 64 entries (the batches then walk across that edge)
+__device__ __forceinline__ int queue_run_start(const int16_t* Q, int qtot, int nom) {
+  if (nom <= 0) return 0;
+  if (nom >= qtot) return qtot;
+  const int lane = threadIdx.x & 63;
+  const int x = nom + lane;
+  const bool st = x >= qtot || (int)Q[x] != (int)Q[x - 1] + 1;
+  const uint64_t m = __ballot(st);
+  return m ? nom + __ffsll((long long)m) - 1 : nom;
+}
+
 template <class SR, int T, int BS, int EMAX, int U, int MODE>
 struct TaskCfg {
   static constexpr bool NUM = MODE != MODE_TSYM;
@@ -394,8 +478,8 @@ struct TaskCfg {
   static constexpr int CAPD = T / 4 * kCapD4;
   static constexpr size_t o_dvals = o_keys;
   static constexpr size_t o_dbits = al(o_dvals + sizeof(acc_t) * CAPD);
-  static constexpr int NWB = NUM ? (int)((o_pos - o_dbits) * 2 / (kDensePre4 ? 9 : 12)) / 8 * 8 : 0;
-  static_assert(!DENSE || o_dbits + dense_window_bytes(NWB) <= o_pos, "dense bitmap and prefix fit the tables");
+  static constexpr int NWB = NUM ? (int)((o_pos - o_dbits) / 6) / 8 * 8 : 0;
+  static_assert(!DENSE || o_dbits + 6 * NWB <= o_pos, "dense bitmap and prefix fit the tables");
   static constexpr size_t o_end = al(o_pos + sizeof(int64_t) * EMAX);
   static constexpr size_t o_scale = al(o_end + sizeof(int64_t) * EMAX);
   static constexpr size_t o_next = al(o_scale + (NUM ? sizeof(b_t) * EMAX : 0));
@@ -741,8 +825,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
     const uint32_t* __restrict__ tb = a.bmp + bw0;
     __shared__ int32_t s_cut;
     constexpr int64_t TB = (int64_t)C::o_pos;
-    // words whose outputs fill the rest
-    int64_t wdes = 2 * TB * nwt / (2 * (int64_t)sizeof(acc_t) * work + (kDensePre4 ? 9 : 12) * nwt);
+    int64_t wdes = TB * nwt / ((int64_t)sizeof(acc_t) * work + 6 * nwt);  // words whose outputs fill the rest
     wdes = wdes < 64 ? 64 : (wdes > C::NWB ? C::NWB : wdes);
     // window ends snap to row-block boundaries when that keeps >= 3/4 of the window
     const bool dalign = kAlignSubtiles && a.RB > 0 && (a.RB & 31) == 0 && (tlo & 31) == 0;
@@ -754,7 +837,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
     int64_t w0 = 0;
     while (w0 < nwt) {
       const int wl = (int)((nwt - w0) < wdes ? (nwt - w0) : wdes);
-      const int dbase = (int)((TB - dense_window_bytes(wl)) & ~int64_t(15));
+      const int dbase = (int)((TB - 6 * wl) & ~int64_t(15));
       uint32_t* dw = reinterpret_cast<uint32_t*>(smem + dbase);
       int16_t* dp = reinterpret_cast<int16_t*>(smem + dbase + 4 * wl);
       const int capv = dbase / (int)sizeof(acc_t);
@@ -784,8 +867,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
         const int x = tid * kw + k;
         if (x < wl) {
           const int pc = __popc(dw[x]);
-          if (!kDensePre4) dp[x] = (int16_t)(ex < 32767 ? ex : 32767);
-          else if ((x & 3) == 0) dp[x >> 2] = (int16_t)(ex < 32767 ? ex : 32767);
+          dp[x] = (int16_t)(ex < 32767 ? ex : 32767);
           if (ex <= capv && ex + pc > capv) s_cut = x;
           ex += pc;
         }
@@ -797,17 +879,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
         const int64_t cb = (w0 + cut) / dbw * dbw - w0;
         if (cb > 0 && cb * 4 >= 3ll * cut) cut = (int)cb;
       }
-      // output rank of the first row of word x (x < the cut: no clamping)
-      auto word_rank = [&](int x) -> int {
-        if constexpr (!kDensePre4) {
-          return dp[x];
-        } else {
-          int r = dp[x >> 2];
-          for (int i = x & ~3; i < x; ++i) r += __popc(dw[i]);
-          return r;
-        }
-      };
-      const int dtotal = cut < wl ? word_rank(cut) : wtotal;
+      const int dtotal = cut < wl ? (int)dp[cut] : wtotal;
       {  // the next window's words: their loads overlap this window's entry loads
         const int64_t w0n = w0 + cut;
         if (w0n < nwt) {
@@ -830,19 +902,9 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
             bad |= 1 << 8;
             return;
           }
-          uint32_t wv;
-          int wr;
-          if constexpr (!kDensePre4) {
-            wv = dw[d >> 5];
-            wr = dp[d >> 5];
-          } else {  // the word's aligned group of 4 in one LDS load, the group prefix beside it
-            const uint4 q = reinterpret_cast<const uint4*>(dw)[d >> 7];
-            const int wi = (d >> 5) & 3;
-            wv = wi == 0 ? q.x : (wi == 1 ? q.y : (wi == 2 ? q.z : q.w));
-            wr = dp[d >> 7] + (wi > 0 ? __popc(q.x) : 0) + (wi > 1 ? __popc(q.y) : 0) + (wi > 2 ? __popc(q.z) : 0);
-          }
+          const uint32_t wv = dw[d >> 5];
           if (!((wv >> (d & 31)) & 1u)) bad |= 1 << 11;  // a product row the symbolic pass did not mark
-          const int slot = wr + __popc(wv & ((1u << (d & 31)) - 1u));
+          const int slot = dp[d >> 5] + __popc(wv & ((1u << (d & 31)) - 1u));
           SR::lds_acc(&vals[slot], av[u]);
         };
         for (int ch = 0; ch < nchunks; ++ch) {
@@ -875,7 +937,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
             reinterpret_cast<val_t*>(a.Cnum)[out_pos + q] = SR::finalize(vals[q]);
           for (int x = tid; x < cut; x += BS) {
             uint32_t wv = dw[x];
-            int32_t* cr = a.Cir + out_pos + word_rank(x);
+            int32_t* cr = a.Cir + out_pos + dp[x];
             while (wv) {
               *cr++ = lo + 32 * x + __builtin_ctz(wv);
               wv &= wv - 1u;
@@ -1096,9 +1158,21 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
         }
       }
       __syncthreads();
-      for (int b0 = wid * 64; b0 < qtot; b0 += NW * 64)
-        bad |= rank_commit_batch<SR>(keys, vals, Q, qtot, b0, out_pos, out_end, a.ccap, a.Cir,
-                                     reinterpret_cast<val_t*>(a.Cnum));
+      if constexpr (kRunAlign) {
+        const int per = (qtot + NW - 1) / NW;
+        const int qs = queue_run_start(Q, qtot, wid * per);
+        const int qe = wid == NW - 1 ? qtot : queue_run_start(Q, qtot, (wid + 1) * per);
+        for (int b0 = qs; b0 < qe;) {
+          int used = 0;
+          bad |= rank_commit_run_batch<SR>(keys, vals, Q, qtot, qe, b0, used, out_pos, out_end, a.ccap, a.Cir,
+                                           reinterpret_cast<val_t*>(a.Cnum));
+          b0 += used;
+        }
+      } else {
+        for (int b0 = wid * 64; b0 < qtot; b0 += NW * 64)
+          bad |= rank_commit_batch<SR>(keys, vals, Q, qtot, b0, out_pos, out_end, a.ccap, a.Cir,
+                                       reinterpret_cast<val_t*>(a.Cnum));
+      }
       out_pos += qtot;
 #ifdef CBH_STAMPS
       if (tid == 0) atomicAdd(&g_stamps[20], (unsigned long long)qtot);
