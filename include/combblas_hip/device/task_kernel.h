@@ -280,93 +280,23 @@ __host__ __device__ inline int64_t dense_subtiles(int64_t work, int64_t span, in
   return 4 * Rd <= dratio4 * R ? Rd : 0;
 }
 
-// Rank commit of one 64-entry batch [b0, b0+64) of the queue Q[0, qtot) of occupied slots of an
-// order-preserving table (slot order), by one wave: a run of occupied slots is a
-// run of queue entries with consecutive slots, so slot Q[q] goes to output out_pos + (start of its
-// run in the queue) + (keys of its run smaller than its key). Run boundaries come from comparing
-// each slot with its queue neighbours (shuffles), run extents from two ballots, ranks from
-// shuffling the run's keys; only runs that cross a batch edge read further keys from LDS.
+// Rank commit of one batch of the queue Q[0, qtot) of occupied slots of an order-preserving table
+// (slot order), by one wave: a run of occupied slots is a run of queue entries with
+// consecutive slots, so slot Q[q] goes to output out_pos + (start of its run in the queue) + (keys of
+// its run smaller than its key). Run boundaries come from comparing each slot with its queue
+// neighbours (shuffles), run extents from two ballots, ranks from shuffling the run's keys.
+// A wave commits a contiguous queue range [b0, qend) whose ends are run starts (queue_run_start),
+// in batches of up to 64 entries that also end where a run starts (`used` returns the entries a
+// batch committed), so no run crosses a batch edge: the dependent LDS walks across the edges of
+// fixed 64-entry batches -- the longest chains of the commit -- remain only for runs longer than a
+// batch and for a wave edge with no run start within 64 entries (round 4: hash 292 -> 284 ms at
+// scale 22; tests/test_commit_logic.py replays the algorithm against a sort on random queues).
 // Returns guard bits (1 << 5: an output position outside the task).
 template <class SR>
-__device__ __forceinline__ int rank_commit_batch(const int32_t* keys, const typename SR::acc_t* vals, const int16_t* Q,
-                                                 int qtot, int b0, int64_t out_pos, int64_t out_end, int64_t ccap,
+__device__ __forceinline__ int rank_commit_batch(const int32_t* keys, const typename SR::acc_t* vals,
+                                                 const int16_t* Q, int qtot, int qend, int b0, int& used,
+                                                 int64_t out_pos, int64_t out_end, int64_t ccap,
                                                  int32_t* __restrict__ Cir, typename SR::val_t* __restrict__ Cnum) {
-  const int lane = threadIdx.x & 63;
-  int bad = 0;
-  const int q = b0 + lane;
-  const bool valid = q < qtot;
-  const int sq = valid ? (int)Q[q] : -4;
-  const int32_t key = valid ? keys[sq] : kNoRow;
-  const int sup = __shfl_up(sq, 1);
-  const int sdn = __shfl_down(sq, 1);
-  const int sprev = lane == 0 ? (b0 > 0 ? (int)Q[b0 - 1] : -10) : sup;
-  const int snext = (q + 1 < qtot) ? (lane == 63 ? (int)Q[q + 1] : sdn) : -10;
-  const uint64_t mstart = __ballot(valid && sq != sprev + 1);
-  const uint64_t mend = __ballot(valid && snext != sq + 1);
-  const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-  const uint64_t below = mstart & upto;
-  const uint64_t above = mend & ~((1ull << lane) - 1ull);
-  const int rs = below ? 63 - __clzll(below) : -1;  // run start lane (-1: before the batch)
-  const int re = above ? __ffsll((long long)above) - 1 : 64;  // run end lane (64: after it)
-  const int lo_l = rs < 0 ? 0 : rs, hi_l = re > 63 ? 63 : re;
-  // keys of the run inside the batch: four shuffles in flight per exit test (runs average
-  // 2.5 slots, but the batch's longest -- about 11 at fill 1/2 -- sets the trip count)
-  int rank = 0;
-  for (int j = 0;; j += 4) {
-    if (__ballot(valid && lo_l + j <= hi_l) == 0ull) break;
-    const int32_t k0 = __shfl(key, (lo_l + j) & 63);
-    const int32_t k1 = __shfl(key, (lo_l + j + 1) & 63);
-    const int32_t k2 = __shfl(key, (lo_l + j + 2) & 63);
-    const int32_t k3 = __shfl(key, (lo_l + j + 3) & 63);
-    if (valid) {
-      rank += (lo_l + j <= hi_l && k0 < key) ? 1 : 0;
-      rank += (lo_l + j + 1 <= hi_l && k1 < key) ? 1 : 0;
-      rank += (lo_l + j + 2 <= hi_l && k2 < key) ? 1 : 0;
-      rank += (lo_l + j + 3 <= hi_l && k3 < key) ? 1 : 0;
-    }
-  }
-  int rstart = b0 + lo_l;
-  if (valid && rs < 0) {  // the run began in an earlier batch
-    int qq = b0 - 1;
-    while (qq >= 0 && (int)Q[qq] == (int)Q[qq + 1] - 1) {
-      rank += keys[Q[qq]] < key ? 1 : 0;
-      --qq;
-    }
-    rstart = qq + 1;
-  }
-  if (valid && re > 63) {  // the run goes on in a later batch
-    int qq = b0 + 64;
-    while (qq < qtot && (int)Q[qq] == (int)Q[qq - 1] + 1) {
-      rank += keys[Q[qq]] < key ? 1 : 0;
-      ++qq;
-    }
-  }
-  if (valid) {
-    const int64_t pos = out_pos + rstart + rank;
-    if (pos >= out_end || pos >= ccap || pos < out_pos) {
-      bad |= 1 << 5;
-    } else {
-      Cir[pos] = key;
-      Cnum[pos] = SR::finalize(vals[sq]);
-    }
-  }
-  return bad;
-}
-
-// Run-aligned batches: a wave commits a contiguous queue range [b0, qend) whose ends are run
-// starts, in batches that also end where a run starts, so no run crosses a batch edge and no lane
-// walks LDS key by key (those dependent walks at the edges of fixed 64-entry batches are the
-// longest chains of the commit). `used` returns the entries this batch committed.
-#ifdef CBH_RUNALIGN
-constexpr bool kRunAlign = true;
-#else
-constexpr bool kRunAlign = false;
-#endif
-template <class SR>
-__device__ __forceinline__ int rank_commit_run_batch(const int32_t* keys, const typename SR::acc_t* vals,
-                                                     const int16_t* Q, int qtot, int qend, int b0, int& used,
-                                                     int64_t out_pos, int64_t out_end, int64_t ccap,
-                                                     int32_t* __restrict__ Cir, typename SR::val_t* __restrict__ Cnum) {
   const int lane = threadIdx.x & 63;
   int bad = 0;
   const int q = b0 + lane;
@@ -1141,10 +1071,10 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
       // rank commit. The occupied slots are compacted in slot order into a queue Q (the owner
       // map's LDS, dead here): queue index q = occupied slots before Q[q]. A run of occupied
       // slots is a run of consecutive queue entries with consecutive slots, so slot Q[q] goes
-      // to (start of its run in the queue) + (keys of its run smaller than its key). Waves take
-      // 64 queue entries at a time: run boundaries come from comparing each slot with its queue
-      // neighbours (shuffles), run extents from two ballots, ranks from shuffling the run's keys
-      // (runs are short at fill 1/2); only runs that cross a batch edge read further keys from LDS.
+      // to (start of its run in the queue) + (keys of its run smaller than its key). Each wave
+      // takes a queue range cut at run starts, in batches of <= 64 entries that end at run starts
+      // (rank_commit_batch: boundaries by shuffles, extents by ballots, ranks by shuffling the
+      // run's keys; runs are short at fill 1/2).
       int16_t* Q = reinterpret_cast<int16_t*>(own);
       {
         const int sb = wid * SPW < TA ? wid * SPW : TA;
@@ -1158,20 +1088,16 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
         }
       }
       __syncthreads();
-      if constexpr (kRunAlign) {
+      {  // wave w commits the queue range between the run starts nearest w and w + 1 NW-ths of it
         const int per = (qtot + NW - 1) / NW;
         const int qs = queue_run_start(Q, qtot, wid * per);
         const int qe = wid == NW - 1 ? qtot : queue_run_start(Q, qtot, (wid + 1) * per);
         for (int b0 = qs; b0 < qe;) {
           int used = 0;
-          bad |= rank_commit_run_batch<SR>(keys, vals, Q, qtot, qe, b0, used, out_pos, out_end, a.ccap, a.Cir,
-                                           reinterpret_cast<val_t*>(a.Cnum));
+          bad |= rank_commit_batch<SR>(keys, vals, Q, qtot, qe, b0, used, out_pos, out_end, a.ccap, a.Cir,
+                                       reinterpret_cast<val_t*>(a.Cnum));
           b0 += used;
         }
-      } else {
-        for (int b0 = wid * 64; b0 < qtot; b0 += NW * 64)
-          bad |= rank_commit_batch<SR>(keys, vals, Q, qtot, b0, out_pos, out_end, a.ccap, a.Cir,
-                                       reinterpret_cast<val_t*>(a.Cnum));
       }
       out_pos += qtot;
 #ifdef CBH_STAMPS
