@@ -39,6 +39,62 @@ __device__ __forceinline__ void guard_fail(int* err, int site, int64_t v0 = 0, i
   }
 }
 
+// Inclusive scans across a wavefront. CBH_DPPSCAN: DPP row shifts 1/2/4/8 and the GFX9 row
+// broadcasts 15/31 (the sequence LLVM's atomic optimizer emits for gfx9): VALU moves instead of
+// six ds_bpermute round trips through LDS. Lanes without a source read `ident`.
+__device__ __forceinline__ int wave_incl_sum(int v) {
+#ifdef CBH_DPPSCAN
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+#else
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(v, d);
+    if (lane >= d) v += y;
+  }
+#endif
+  return v;
+}
+__device__ __forceinline__ int wave_incl_max(int v, int ident) {
+#ifdef CBH_DPPSCAN
+  int y;
+  y = __builtin_amdgcn_update_dpp(ident, v, 0x111, 0xf, 0xf, false);
+  v = y > v ? y : v;
+  y = __builtin_amdgcn_update_dpp(ident, v, 0x112, 0xf, 0xf, false);
+  v = y > v ? y : v;
+  y = __builtin_amdgcn_update_dpp(ident, v, 0x114, 0xf, 0xf, false);
+  v = y > v ? y : v;
+  y = __builtin_amdgcn_update_dpp(ident, v, 0x118, 0xf, 0xf, false);
+  v = y > v ? y : v;
+  y = __builtin_amdgcn_update_dpp(ident, v, 0x142, 0xa, 0xf, false);
+  v = y > v ? y : v;
+  y = __builtin_amdgcn_update_dpp(ident, v, 0x143, 0xc, 0xf, false);
+  v = y > v ? y : v;
+#else
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(v, d);
+    if (lane >= d) v = y > v ? y : v;
+  }
+#endif
+  return v;
+}
+// the previous lane's value (lane 0: ident)
+__device__ __forceinline__ int wave_prev(int v, int ident) {
+#ifdef CBH_DPPSCAN
+  return __builtin_amdgcn_update_dpp(ident, v, 0x138, 0xf, 0xf, false);  // wave_shr:1
+#else
+  const int y = __shfl_up(v, 1);
+  return (threadIdx.x & 63) == 0 ? ident : y;
+#endif
+}
+
 template <int NW>
 __device__ __forceinline__ int block_sum_int(int v, int* red) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -62,12 +118,7 @@ __device__ __forceinline__ void block_scan_excl(int32_t* x, int n, int* red) {
   for (int base = 0; base < n; base += BS) {
     const int i = base + tid;
     const int v = i < n ? x[i] : 0;
-    int s = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      int y = __shfl_up(s, d);
-      if (lane >= d) s += y;
-    }
+    const int s = wave_incl_sum(v);
     if (lane == 63) red[wid] = s;
     __syncthreads();
     int wpre = 0, tot = 0;
@@ -98,15 +149,9 @@ __device__ __forceinline__ void block_max_scan(OT* own, int* red) {
     m = x > m ? x : m;
     v[e] = m;
   }
-  int s = m;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(s, d);
-    if (lane >= d) s = y > s ? y : s;
-  }
+  const int s = wave_incl_max(m, -1);
   if (lane == 63) red[wid] = s;
-  int ex = __shfl_up(s, 1);
-  if (lane == 0) ex = -1;
+  const int ex = wave_prev(s, -1);
   __syncthreads();
   int wpre = -1;
 #pragma unroll

@@ -243,12 +243,7 @@ template <int BS>
 __device__ __forceinline__ int block_excl_sum(int v, int* red, int& total) {
   constexpr int NW = BS / 64;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int s = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(s, d);
-    if (lane >= d) s += y;
-  }
+  const int s = wave_incl_sum(v);
   __syncthreads();  // red may still be read by a previous user
   if (lane == 63) red[wid] = s;
   __syncthreads();
