@@ -39,29 +39,20 @@ __device__ __forceinline__ void guard_fail(int* err, int site, int64_t v0 = 0, i
   }
 }
 
-// Inclusive scans across a wavefront. CBH_DPPSCAN: DPP row shifts 1/2/4/8 and the GFX9 row
-// broadcasts 15/31 (the sequence LLVM's atomic optimizer emits for gfx9): VALU moves instead of
-// six ds_bpermute round trips through LDS. Lanes without a source read `ident`.
+// Inclusive scans across a wavefront: DPP row shifts 1/2/4/8 and the GFX9 row broadcasts 15/31
+// (the sequence LLVM's atomic optimizer emits for gfx9) -- VALU moves instead of six ds_bpermute
+// round trips through LDS (round 4: A^2 144.3 -> 150.1 GFLOP/s, every task kernel faster).
+// Lanes without a source read `ident`.
 __device__ __forceinline__ int wave_incl_sum(int v) {
-#ifdef CBH_DPPSCAN
   v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
   v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
   v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
   v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
   v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
   v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
-#else
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(v, d);
-    if (lane >= d) v += y;
-  }
-#endif
   return v;
 }
 __device__ __forceinline__ int wave_incl_max(int v, int ident) {
-#ifdef CBH_DPPSCAN
   int y;
   y = __builtin_amdgcn_update_dpp(ident, v, 0x111, 0xf, 0xf, false);
   v = y > v ? y : v;
@@ -75,31 +66,28 @@ __device__ __forceinline__ int wave_incl_max(int v, int ident) {
   v = y > v ? y : v;
   y = __builtin_amdgcn_update_dpp(ident, v, 0x143, 0xc, 0xf, false);
   v = y > v ? y : v;
-#else
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(v, d);
-    if (lane >= d) v = y > v ? y : v;
-  }
-#endif
   return v;
 }
 // the previous lane's value (lane 0: ident)
 __device__ __forceinline__ int wave_prev(int v, int ident) {
-#ifdef CBH_DPPSCAN
   return __builtin_amdgcn_update_dpp(ident, v, 0x138, 0xf, 0xf, false);  // wave_shr:1
-#else
-  const int y = __shfl_up(v, 1);
-  return (threadIdx.x & 63) == 0 ? ident : y;
-#endif
 }
+// the next lane's value (lane 63: ident)
+__device__ __forceinline__ int wave_next(int v, int ident) {
+  return __builtin_amdgcn_update_dpp(ident, v, 0x130, 0xf, 0xf, false);  // wave_shl:1
+}
+// the wavefront's sum, in every lane
+__device__ __forceinline__ int wave_total(int v) { return __builtin_amdgcn_readlane(wave_incl_sum(v), 63); }
 
 template <int NW>
 __device__ __forceinline__ int block_sum_int(int v, int* red) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#ifdef CBH_DPP2
+  v = wave_total(v);
+#else
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+#endif
   __syncthreads();
   if (lane == 0) red[wid] = v;
   __syncthreads();

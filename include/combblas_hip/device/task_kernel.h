@@ -301,8 +301,13 @@ __device__ __forceinline__ int rank_commit_batch(const int32_t* keys, const type
   const bool inq = q < qend;
   const int sq = loaded ? (int)Q[q] : -4;
   const int32_t key = loaded ? keys[sq] : kNoRow;
+#ifdef CBH_DPP2
+  const int sup = wave_prev(sq, -10);
+  const int sdn = wave_next(sq, -10);
+#else
   const int sup = __shfl_up(sq, 1);
   const int sdn = __shfl_down(sq, 1);
+#endif
   const int sprev = lane == 0 ? (b0 > 0 ? (int)Q[b0 - 1] : -10) : sup;
   const int snext = (q + 1 < qtot) ? (lane == 63 ? (int)Q[q + 1] : sdn) : -10;
   const uint64_t mstart = __ballot(loaded && sq != sprev + 1);
