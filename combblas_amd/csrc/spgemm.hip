@@ -41,9 +41,6 @@ struct cbh_ctx {
   bool timing = false;
   cbh_kernel_times times{-1, -1, -1, 0};
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  // second stream: a phase's dense-window kernel runs beside its hash kernels (kOverlapDense)
-  hipStream_t stream2 = nullptr;
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   int* d_err = nullptr;  // 32 ints: [0..15] device-side error flags (check_err), [16] sub-tile retries
   void* ws = nullptr;  // persistent phase workspace (hipMalloc'd once, grow-only): a ~150 GB
   int64_t ws_bytes = 0;  // buffer must not be re-mapped on every product
@@ -1155,21 +1152,6 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
 }
 
 // numeric over the tasks of column slots [c0, c1) (task ids [t0, t1)) writing C entries at toff-cbase
-// The dense-window kernel (HBM-bound on its traffic) and the hash kernels (latency-bound) of one
-// phase run on two streams at once: their workgroups share the CUs (80 + 53 KB of LDS fit one CU).
-#ifdef CBH_OVERLAP_DENSE
-constexpr bool kOverlapDense = true;
-#else
-constexpr bool kOverlapDense = false;
-#endif
-static int ensure_stream2(cbh_ctx* ctx) {
-  if (ctx->stream2) return CBH_OK;
-  CBH_HIP(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
-  CBH_HIP(ctx, hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
-  CBH_HIP(ctx, hipEventCreateWithFlags(&ctx->join_ev, hipEventDisableTiming));
-  return CBH_OK;
-}
-
 template <class SR>
 static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat* B, Plan& P, int64_t t0, int64_t t1,
                        int64_t cbase, int32_t* Cir, void* Cnum, int64_t* launches, int64_t ccap) {
@@ -1238,21 +1220,8 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
     CBH_TRY((launch_task_diag<SR, TNumLarge, MODE_TDENSE>(ctx, a, bd, "numeric dense")));
     CBH_TRY((launch_task_diag<SR, TNumHash, MODE_TNUM>(ctx, a, bl, "numeric hash")));
   }
-  const bool overlap = kOverlapDense && !diag_enabled() && bd.large_count > 0 &&
-                       bl.large_count + bl.mid_count + bl.small_count > 0;
   if (!diag_enabled()) {
-    if (overlap) {  // fork: the dense kernel on the second stream, after everything before it
-      CBH_TRY(ensure_stream2(ctx));
-      CBH_HIP(ctx, hipEventRecord(ctx->fork_ev, ctx->stream));
-      CBH_HIP(ctx, hipStreamWaitEvent(ctx->stream2, ctx->fork_ev, 0));
-      std::swap(ctx->stream, ctx->stream2);
-      const int rc = launch_task<SR, TNumLarge, MODE_TDENSE>(ctx, a, bd.large_first, bd.large_count, CBH_K_NUM_DENSE, nb_d);
-      std::swap(ctx->stream, ctx->stream2);
-      CBH_TRY(rc);
-      CBH_HIP(ctx, hipEventRecord(ctx->join_ev, ctx->stream2));
-    } else {
-      CBH_TRY((launch_task<SR, TNumLarge, MODE_TDENSE>(ctx, a, bd.large_first, bd.large_count, CBH_K_NUM_DENSE, nb_d)));
-    }
+    CBH_TRY((launch_task<SR, TNumLarge, MODE_TDENSE>(ctx, a, bd.large_first, bd.large_count, CBH_K_NUM_DENSE, nb_d)));
     CBH_TRY((launch_task<SR, TNumHash, MODE_TNUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
   }
   CBH_TRY((launch_task<SR, TNumMid, MODE_TNUM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_NUM_MID, nb_m)));
@@ -1260,7 +1229,6 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
     CBH_TRY(timed_launch(ctx, CBH_K_NUM_SMALL, nb_s, [&] {
       return launch_small_numeric<SR, TNumSmall>(a, bl.small_first, bl.small_count, ctx->stream);
     }));
-  if (overlap) CBH_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->join_ev, 0));  // join
   if (launches) *launches += (bd.large_count > 0);
   if (launches) *launches += (bl.large_count > 0) + (bl.mid_count > 0) + (bl.small_count > 0);
   return CBH_OK;
@@ -1409,9 +1377,6 @@ int cbh_ctx_destroy(cbh_ctx* ctx) {
   release_cache(ctx);
   for (auto& kv : ctx->live) (void)hipFree(kv.first);  // matrices not freed by the caller
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
-  if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
-  if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
-  if (ctx->join_ev) (void)hipEventDestroy(ctx->join_ev);
   delete ctx;
   return CBH_OK;
 }

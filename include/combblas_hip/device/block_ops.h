@@ -72,22 +72,12 @@ __device__ __forceinline__ int wave_incl_max(int v, int ident) {
 __device__ __forceinline__ int wave_prev(int v, int ident) {
   return __builtin_amdgcn_update_dpp(ident, v, 0x138, 0xf, 0xf, false);  // wave_shr:1
 }
-// the next lane's value (lane 63: ident)
-__device__ __forceinline__ int wave_next(int v, int ident) {
-  return __builtin_amdgcn_update_dpp(ident, v, 0x130, 0xf, 0xf, false);  // wave_shl:1
-}
-// the wavefront's sum, in every lane
-__device__ __forceinline__ int wave_total(int v) { return __builtin_amdgcn_readlane(wave_incl_sum(v), 63); }
 
 template <int NW>
 __device__ __forceinline__ int block_sum_int(int v, int* red) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#ifdef CBH_DPP2
-  v = wave_total(v);
-#else
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-#endif
   __syncthreads();
   if (lane == 0) red[wid] = v;
   __syncthreads();
@@ -148,6 +138,37 @@ __device__ __forceinline__ void block_max_scan(OT* own, int* red) {
   const int carry = ex > wpre ? ex : wpre;
 #pragma unroll
   for (int e = 0; e < E; ++e) own[tid * E + e] = (OT)(v[e] > carry ? v[e] : carry);
+  __syncthreads();
+}
+
+// The same over a generation-tagged owner map (CBH_OWNGEN): entries are (tag | entry), tag = the
+// window's generation << 9; entries of other generations are stale (read as none), so the map is
+// never cleared between windows. `carry` (the owner before the window) seeds thread 0; the
+// result is written back tagged.
+template <int BS, int WIN, class OT = int32_t>
+__device__ __forceinline__ void block_max_scan_gen(OT* own, int* red, int tag, int carry) {
+  constexpr int E = WIN / BS, NW = BS / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int v[E];
+  int m = tid == 0 ? carry : -1;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int x = own[tid * E + e];
+    const int y = (x & ~511) == tag ? (x & 511) : -1;
+    m = y > m ? y : m;
+    v[e] = m;
+  }
+  const int s = wave_incl_max(m, -1);
+  if (lane == 63) red[wid] = s;
+  const int ex = wave_prev(s, -1);
+  __syncthreads();
+  int wpre = -1;
+#pragma unroll
+  for (int w = 0; w < NW; ++w)
+    if (w < wid) wpre = red[w] > wpre ? red[w] : wpre;
+  const int c = ex > wpre ? ex : wpre;
+#pragma unroll
+  for (int e = 0; e < E; ++e) own[tid * E + e] = (OT)(tag | ((v[e] > c ? v[e] : c) & 511));
   __syncthreads();
 }
 

@@ -116,10 +116,6 @@ __global__ __launch_bounds__(64 * WPB) void wave_kernel(TaskArgs a) {
         if constexpr (NUM) escale[lane] = reinterpret_cast<const b_t*>(a.Bnum)[e0 + i];
       }
     }
-#ifdef CBH_DPP2
-    const int incl = wave_incl_sum(len);
-    const int total = __builtin_amdgcn_readlane(incl, 63);
-#else
     int incl = len;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -127,7 +123,6 @@ __global__ __launch_bounds__(64 * WPB) void wave_kernel(TaskArgs a) {
       if (lane >= d) incl += y;
     }
     const int total = __shfl(incl, 63);
-#endif
     const int excl = incl - len;
     ebase[lane] = pos - excl;  // product p of this entry reads A at ebase + p
     wave_lds_sync();
@@ -182,13 +177,9 @@ __global__ __launch_bounds__(64 * WPB) void wave_kernel(TaskArgs a) {
   }
 
   if constexpr (!NUM) {
-#ifdef CBH_DPP2
-    const int t = wave_total(my_count);
-#else
     int t = my_count;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
-#endif
     if (lane == 0) a.cnt[task] = t;
   } else {
     // occupied keys (and their slots) compacted into a list; a key's output position is the
