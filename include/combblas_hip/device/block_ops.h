@@ -108,10 +108,20 @@ __device__ __forceinline__ void block_scan_excl(int32_t* x, int n, int* red) {
     }
     if (i < n) x[i] = carry + wpre + s - v;
     carry += tot;
+#ifdef CBH_FEWBAR
+    if (base + BS >= n && tid == 0) x[n] = carry;  // the total, ordered by this chunk's barrier
+#endif
     __syncthreads();
   }
+#ifdef CBH_FEWBAR
+  if (n <= 0) {
+    if (tid == 0) x[0] = 0;
+    __syncthreads();
+  }
+#else
   if (tid == 0) x[n] = carry;
   __syncthreads();
+#endif
 }
 
 // In-place inclusive prefix-max of own[0..WIN) (LDS); each thread owns E = WIN/BS contiguous slots.
@@ -138,37 +148,6 @@ __device__ __forceinline__ void block_max_scan(OT* own, int* red) {
   const int carry = ex > wpre ? ex : wpre;
 #pragma unroll
   for (int e = 0; e < E; ++e) own[tid * E + e] = (OT)(v[e] > carry ? v[e] : carry);
-  __syncthreads();
-}
-
-// The same over a generation-tagged owner map (CBH_OWNGEN): entries are (tag | entry), tag = the
-// window's generation << 9; entries of other generations are stale (read as none), so the map is
-// never cleared between windows. `carry` (the owner before the window) seeds thread 0; the
-// result is written back tagged.
-template <int BS, int WIN, class OT = int32_t>
-__device__ __forceinline__ void block_max_scan_gen(OT* own, int* red, int tag, int carry) {
-  constexpr int E = WIN / BS, NW = BS / 64;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  int v[E];
-  int m = tid == 0 ? carry : -1;
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const int x = own[tid * E + e];
-    const int y = (x & ~511) == tag ? (x & 511) : -1;
-    m = y > m ? y : m;
-    v[e] = m;
-  }
-  const int s = wave_incl_max(m, -1);
-  if (lane == 63) red[wid] = s;
-  const int ex = wave_prev(s, -1);
-  __syncthreads();
-  int wpre = -1;
-#pragma unroll
-  for (int w = 0; w < NW; ++w)
-    if (w < wid) wpre = red[w] > wpre ? red[w] : wpre;
-  const int c = ex > wpre ? ex : wpre;
-#pragma unroll
-  for (int e = 0; e < E; ++e) own[tid * E + e] = (OT)(tag | ((v[e] > c ? v[e] : c) & 511));
   __syncthreads();
 }
 

@@ -39,11 +39,6 @@ constexpr int32_t kNoRow = 0x7fffffff;
 // segment search starts AT the cursor, whose row the search loads with the following ones)
 constexpr int32_t kUnknownRow = -2;
 constexpr bool kAlignSubtiles = true;  // sub-tiles and dense windows end on row-block boundaries
-#ifdef CBH_OWNGEN
-constexpr bool kOwnGen = true;  // generation-tagged owner maps (block_max_scan_gen)
-#else
-constexpr bool kOwnGen = false;
-#endif
 constexpr int kSymWords = 12160;  // bitmap words of the large symbolic configuration (see TaskCfg::TA)
 // numeric sub-tile: planned outputs, in eighths of the T home slots (3/8 and 5/8 measured slower:
 // 97.6 and 93.5 vs 98.6 GFLOP/s at scale 22 with T 4096; 5/8 again with T 2048: hash 434 vs 360 ms)
@@ -396,7 +391,6 @@ struct TaskCfg {
   // owner map entries are entry indices (< EMAX): 16 bits leave LDS room for larger windows
   using own_t = int16_t;
   static_assert(EMAX < 32768, "owner map entries are 16-bit");
-  static_assert(!kOwnGen || EMAX <= 512, "tagged owner map entries hold 9-bit entry ids");
   static constexpr size_t al(size_t x) { return (x + 15) & ~size_t(15); }
   static constexpr size_t o_keys = 0;
   static constexpr size_t o_vals = al(o_keys + sizeof(int32_t) * TA);
@@ -675,13 +669,14 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
       }
 #endif
     }
+#ifndef CBH_FEWBAR  // (the scan reads each eoff[i] in the thread that wrote it)
     __syncthreads();
+#endif
     CBH_STAMP(2);
     block_scan_excl<BS>(eoff, nec, red);
     for (int i = tid; i < nec; i += BS) epos[i] -= eoff[i];
     return eoff[nec];
   };
-  int own_gen = 7;  // kOwnGen: the owner map's generation (the first window uses 8)
   // the U products of the current window this thread holds
   int32_t r[U];
   val_t av[U];  // numeric: A value * B value (the product), once values are gathered
@@ -691,34 +686,15 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
     int carry = -1;  // owner of the product just before the window
     for (int w0 = 0; w0 < P; w0 += WIN) {
       const int wn = (P - w0) < WIN ? (P - w0) : WIN;
-      if constexpr (kOwnGen) {
-        // generation-tagged owner map: no clearing pass (and no barrier) per window; the map is
-        // cleared only when the generation wraps (tags 8..63: the commit queue's slot ids, which
-        // reuse this LDS, carry tags 0..4)
-        if (++own_gen > 63) {
-          own_gen = 8;
-          for (int x = tid; x < WIN; x += BS) own[x] = (typename C::own_t)0;
-          __syncthreads();
-        }
-        const int tag = own_gen << 9;
-        for (int i = tid; i < nec; i += BS) {
-          const int s0 = eoff[i];
-          if (s0 >= w0 && s0 < w0 + wn && eoff[i + 1] > s0) own[s0 - w0] = (typename C::own_t)(tag | i);
-        }
-        __syncthreads();
-        block_max_scan_gen<BS, WIN>(own, red, tag, carry);
-        carry = own[wn - 1] & 511;
-      } else {
-        for (int x = tid; x < WIN; x += BS) own[x] = (typename C::own_t)((x == 0) ? carry : -1);
-        __syncthreads();
-        for (int i = tid; i < nec; i += BS) {
-          const int s0 = eoff[i];
-          if (s0 >= w0 && s0 < w0 + wn && eoff[i + 1] > s0) own[s0 - w0] = (typename C::own_t)i;
-        }
-        __syncthreads();
-        block_max_scan<BS, WIN>(own, red);
-        carry = own[wn - 1];
+      for (int x = tid; x < WIN; x += BS) own[x] = (typename C::own_t)((x == 0) ? carry : -1);
+      __syncthreads();
+      for (int i = tid; i < nec; i += BS) {
+        const int s0 = eoff[i];
+        if (s0 >= w0 && s0 < w0 + wn && eoff[i + 1] > s0) own[s0 - w0] = (typename C::own_t)i;
       }
+      __syncthreads();
+      block_max_scan<BS, WIN>(own, red);
+      carry = own[wn - 1];
       CBH_STAMP(4);
       if (__hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
       // branch-free gather: lanes past the window re-read product 0 and are masked afterwards
@@ -726,7 +702,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
       for (int u = 0; u < U; ++u) {
         const int x0 = tid + u * BS;
         const int x = x0 < wn ? x0 : 0;
-        const int i = kOwnGen ? (own[x] & 511) : own[x];
+        const int i = own[x];
         const int64_t q = epos[i] + w0 + x;
         r[u] = rowsA[q];
         if constexpr (NUM && MERGE) {
@@ -747,8 +723,6 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
   if (!chunked) {
     load_entries(0, (int)ne, tlo, thi, (full & 1) != 0, false);
   }
-  if constexpr (kOwnGen)  // a previous workgroup's map in this LDS must not read as current
-    for (int x = tid; x < WIN; x += BS) own[x] = (typename C::own_t)0;
   __syncthreads();
   CBH_STAMP(0);
 
