@@ -108,20 +108,10 @@ __device__ __forceinline__ void block_scan_excl(int32_t* x, int n, int* red) {
     }
     if (i < n) x[i] = carry + wpre + s - v;
     carry += tot;
-#ifdef CBH_FEWBAR
-    if (base + BS >= n && tid == 0) x[n] = carry;  // the total, ordered by this chunk's barrier
-#endif
     __syncthreads();
   }
-#ifdef CBH_FEWBAR
-  if (n <= 0) {
-    if (tid == 0) x[0] = 0;
-    __syncthreads();
-  }
-#else
   if (tid == 0) x[n] = carry;
   __syncthreads();
-#endif
 }
 
 // In-place inclusive prefix-max of own[0..WIN) (LDS); each thread owns E = WIN/BS contiguous slots.

@@ -669,9 +669,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
       }
 #endif
     }
-#ifndef CBH_FEWBAR  // (the scan reads each eoff[i] in the thread that wrote it)
     __syncthreads();
-#endif
     CBH_STAMP(2);
     block_scan_excl<BS>(eoff, nec, red);
     for (int i = tid; i < nec; i += BS) epos[i] -= eoff[i];
