@@ -172,7 +172,13 @@ static int dalloc(cbh_ctx* ctx, T** p, size_t count) {
   }
   if (e != hipSuccess) {
     (void)hipGetLastError();
-    return fail(ctx, CBH_E_OOM, "hipMalloc(" + std::to_string(cls) + "): " + hipGetErrorString(e));
+    size_t fr = 0, tot = 0;
+    (void)hipMemGetInfo(&fr, &tot);
+    size_t live = 0;
+    for (auto& kv : ctx->live) live += kv.second;
+    return fail(ctx, CBH_E_OOM, "hipMalloc(" + std::to_string(cls) + "): " + hipGetErrorString(e) + " (device free " +
+                                    std::to_string(fr) + " of " + std::to_string(tot) + ", context live " +
+                                    std::to_string(live) + ", workspace " + std::to_string(ctx->ws_bytes) + ")");
   }
   ctx->live[q] = cls;
   *p = reinterpret_cast<T*>(q);
