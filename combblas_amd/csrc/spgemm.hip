@@ -1432,6 +1432,20 @@ int cbh_hash_config(int64_t* table_slots, int64_t* threads, int64_t* per_thread)
   return CBH_OK;
 }
 
+int cbh_ctx_memory(cbh_ctx* ctx, int64_t* live_bytes, int64_t* cached_bytes, int64_t* device_free,
+                   int64_t* device_total) {
+  if (!ctx) return CBH_E_ARG;
+  size_t live = 0;
+  for (auto& kv : ctx->live) live += kv.second;
+  size_t fr = 0, tot = 0;
+  CBH_HIP(ctx, hipMemGetInfo(&fr, &tot));
+  if (live_bytes) *live_bytes = (int64_t)live;
+  if (cached_bytes) *cached_bytes = (int64_t)ctx->cached_bytes;
+  if (device_free) *device_free = (int64_t)fr;
+  if (device_total) *device_total = (int64_t)tot;
+  return CBH_OK;
+}
+
 int cbh_ctx_take_retries(cbh_ctx* ctx, int64_t* subtile_retries) {
   if (!ctx || !subtile_retries) return CBH_E_ARG;
   int h = 0;

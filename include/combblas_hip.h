@@ -97,6 +97,10 @@ const char* cbh_last_error(cbh_ctx* ctx);
 /* Sub-tiles the task kernels retried with half the row range (table overflow, commit queue) since
  * the last call; resets the counter (diagnostics and tests). */
 int cbh_ctx_take_retries(cbh_ctx* ctx, int64_t* subtile_retries);
+/* Memory held by the context's default allocator (live blocks, cached free blocks) and the
+ * device's free / total memory (hipMemGetInfo); any pointer may be NULL. */
+int cbh_ctx_memory(cbh_ctx* ctx, int64_t* live_bytes, int64_t* cached_bytes, int64_t* device_free,
+                   int64_t* device_total);
 /* The large numeric hash kernel's configuration: table slots T (plus 64 guard slots), threads per
  * workgroup and products per thread per window (the commit queue holds threads * per_thread). */
 int cbh_hash_config(int64_t* table_slots, int64_t* threads, int64_t* per_thread);

@@ -48,6 +48,15 @@ inline cbh_mat* col_concat(std::vector<cbh_mat*>& parts) {
   parts.clear();
   return out;
 }
+// COMBBLAS_HIP_MEMDIAG=1: the device memory state at the phased drivers' milestones (stderr)
+inline void memdiag(const char* where) {
+  static const bool on = std::getenv("COMBBLAS_HIP_MEMDIAG") != nullptr;
+  if (!on) return;
+  int64_t live = 0, cached = 0, fr = 0, tot = 0;
+  cbh_ctx_memory(context(), &live, &cached, &fr, &tot);
+  std::fprintf(stderr, "[memdiag] %-28s live %.2f GB, cached %.2f GB, device free %.2f of %.2f GB\n", where, live / 1e9,
+               cached / 1e9, fr / 1e9, tot / 1e9);
+}
 inline std::vector<int64_t> essentials(const cbh_mat* M) {  // {nnz, m, n, nzc}
   int64_t m = 0, n = 0, nnz = 0, nzc = 0;
   cbh_mat_info(M, &m, &n, &nnz, &nzc, nullptr);
@@ -385,15 +394,19 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
   const IU C_n = B.seq().getncol();
   const auto cuts = combblas_hip::colsplit_cuts(C_n, phases);
   std::vector<cbh_mat*> toconcatenate;
+  combblas_hip::memdiag("phase loop start");
   for (int p = 0; p < phases; ++p) {
     cbh_mat* Cp = SP.piece(combblas_hip::semiring_traits<SR>::code, combblas_hip::dtype_of<NUO>::value,
                            (int64_t)sizeof(NUO), cuts[p], cuts[p + 1]);
+    combblas_hip::memdiag("phase product");
     SpParMat<IU, NUO, UDERO> OnePieceOfC(new UDERO(Cp), GridC);
     MCLPruneRecoverySelect(OnePieceOfC, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion);
     toconcatenate.push_back(OnePieceOfC.seq().release());
+    combblas_hip::memdiag("phase pruned");
   }
   SPp.reset();
   cbh_ctx_trim(combblas_hip::context());  // the cached scratch of the phase loop back to HIP
+  combblas_hip::memdiag("before concatenation");
   return SpParMat<IU, NUO, UDERO>(new UDERO(combblas_hip::col_concat(toconcatenate)), GridC);
 }
 
