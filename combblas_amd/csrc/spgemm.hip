@@ -2968,6 +2968,12 @@ int cbh_mat_col_concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** o
   CBH_HIP(ctx, hipGetLastError());
   release(&cbh_mat::cp);
   release(&cbh_mat::jc);
+  if (std::getenv("CBH_MEMDIAG")) {
+    size_t fr = 0, tot = 0;
+    (void)hipMemGetInfo(&fr, &tot);
+    std::fprintf(stderr, "[cbh memdiag] concat: %d parts, device free %.2f GB, rows need %.2f GB\n", k, fr / 1e9,
+                 nnz * 4 / 1e9);
+  }
   if ((rc = dalloc(ctx, &C->ir, nnz)) != CBH_OK) {
     cbh_mat_free(ctx, C);
     return rc;
@@ -2980,6 +2986,13 @@ int cbh_mat_col_concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** o
     eoff += parts[i]->nnz;
   }
   release(&cbh_mat::ir);
+  release_cache(ctx);  // the parts' rows back to HIP before the largest allocation
+  if (std::getenv("CBH_MEMDIAG")) {
+    size_t fr = 0, tot = 0;
+    (void)hipMemGetInfo(&fr, &tot);
+    std::fprintf(stderr, "[cbh memdiag] concat: rows copied and released, device free %.2f GB, values need %.2f GB\n",
+                 fr / 1e9, nnz * vb / 1e9);
+  }
   if ((rc = dalloc(ctx, reinterpret_cast<char**>(&C->num), nnz * vb)) != CBH_OK) {
     cbh_mat_free(ctx, C);
     return rc;
