@@ -94,6 +94,9 @@ def cpp_line(args):
     cmd = [harness, str(args.log2n), str(args.deg), str(args.steps), str(args.phases), str(args.check_cols),
            str(args.cpu_stride)]
     r = subprocess.run(cmd, env=env, cwd="/tmp", capture_output=True, text=True, timeout=1100)
+    for l in r.stdout.splitlines():
+        if l.startswith("[memdiag]"):
+            print(l, file=sys.stderr)
     line = [l for l in r.stdout.splitlines() if l.startswith("BENCHC5CPP ")]
     if not line:
         sys.exit(f"harness failed (rc {r.returncode}):\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}")

@@ -136,12 +136,20 @@ SIGNATURES = {
                                                      ctypes.c_int64, ctypes.c_int64, ctypes.c_double,
                                                      ctypes.c_void_p, ctypes.c_void_p,
                                                      ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_mcl_prune_recovery_select_arena": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double,
+                                                           ctypes.c_int64, ctypes.c_int64, ctypes.c_double,
+                                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                           ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_mat_col_slice": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                          ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_mat_col_concat": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                           ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_mat_col_concat_consume": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                                   ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_arena_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_arena_destroy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "cbh_arena_concat": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_tuples_to_dcsc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                           ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),

@@ -90,6 +90,18 @@ struct cbh_mat {
   int32_t* ir = nullptr;
   void* num = nullptr;
   bool owned = true;
+  bool borrowed_rows = false;  // ir / num live in a cbh_arena (not freed with the block)
+};
+
+// Output arena of the phased MCL drivers: the pruned pieces of every phase are written back to
+// back into one pair of row / value arrays, which then become the concatenated result's arrays
+// without a copy (cbh_arena_concat) -- a near-capacity product never holds the pieces and their
+// concatenation at once.
+struct cbh_arena {
+  int32_t* ir = nullptr;
+  char* num = nullptr;
+  int64_t cap = 0, used = 0, vbytes = 8;
+  bool overflow = false;  // a piece did not fit: it was allocated on its own (cbh_arena_concat copies)
 };
 
 static size_t dtype_size(int dt) {
@@ -137,11 +149,38 @@ static size_t alloc_class(size_t bytes) {
 }
 static void release_cache(cbh_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
-  for (auto& kv : ctx->cache) (void)hipFree(kv.second);
+  static const bool diag = std::getenv("CBH_MEMDIAG") != nullptr;
+  int nerr = 0;
+  hipError_t last = hipSuccess;
+  for (auto& kv : ctx->cache) {
+    const hipError_t e = hipFree(kv.second);
+    if (e != hipSuccess) {
+      ++nerr;
+      last = e;
+    }
+  }
+  if (diag && !ctx->cache.empty())
+    std::fprintf(stderr, "[cbh memdiag] release_cache: %zu blocks, %.2f GB, %d hipFree errors (%s)\n", ctx->cache.size(),
+                 ctx->cached_bytes / 1e9, nerr, hipGetErrorString(last));
+  (void)hipGetLastError();
   ctx->cache.clear();
   ctx->cached_bytes = 0;
   for (void* q : ctx->quarantine) (void)hipFree(q);
   ctx->quarantine.clear();
+}
+// frees cached blocks, largest first, until the cache holds at most `keep` bytes (round 4: a
+// near-capacity product re-maps only what it must; releasing the whole cache made the C5 C++
+// driver re-map ~150 GB per step, 30 ms per GB)
+static void shrink_cache(cbh_ctx* ctx, size_t keep) {
+  if (ctx->cached_bytes <= keep || ctx->cache.empty()) return;
+  (void)hipStreamSynchronize(ctx->stream);
+  while (ctx->cached_bytes > keep && !ctx->cache.empty()) {
+    auto it = std::prev(ctx->cache.end());
+    (void)hipFree(it->second);
+    ctx->cached_bytes -= it->first;
+    ctx->cache.erase(it);
+  }
+  (void)hipGetLastError();
 }
 template <class T>
 static int dalloc(cbh_ctx* ctx, T** p, size_t count) {
@@ -165,10 +204,19 @@ static int dalloc(cbh_ctx* ctx, T** p, size_t count) {
   }
   void* q = nullptr;
   hipError_t e = hipMalloc(&q, cls);
-  if (e != hipSuccess && !ctx->cache.empty()) {
+  if (e != hipSuccess && !ctx->cache.empty()) {  // give back cached blocks, largest first, until it fits
     (void)hipGetLastError();
-    release_cache(ctx);
+    size_t fr = 0, tot = 0;
+    (void)hipMemGetInfo(&fr, &tot);
+    const size_t margin = size_t(1) << 30;
+    const size_t need = cls + margin > fr ? cls + margin - fr : 0;
+    shrink_cache(ctx, ctx->cached_bytes > need ? ctx->cached_bytes - need : 0);
     e = hipMalloc(&q, cls);
+    if (e != hipSuccess && !ctx->cache.empty()) {
+      (void)hipGetLastError();
+      release_cache(ctx);
+      e = hipMalloc(&q, cls);
+    }
   }
   if (e != hipSuccess) {
     (void)hipGetLastError();
@@ -201,7 +249,7 @@ static void dfree(cbh_ctx* ctx, void* p) {
   ctx->cache.emplace(it->second, p);
   ctx->cached_bytes += it->second;
   ctx->live.erase(it);
-  if (ctx->cached_bytes > ctx->cache_cap) release_cache(ctx);
+  if (ctx->cached_bytes > ctx->cache_cap) shrink_cache(ctx, ctx->cache_cap);
 }
 
 // RAII holder for scratch allocations of one call.
@@ -1691,8 +1739,10 @@ int cbh_mat_free(cbh_ctx* ctx, cbh_mat* M) {
   if (M->owned && ctx) {
     dfree(ctx, M->cp);
     dfree(ctx, M->jc);
-    dfree(ctx, M->ir);
-    dfree(ctx, M->num);
+    if (!M->borrowed_rows) {
+      dfree(ctx, M->ir);
+      dfree(ctx, M->num);
+    }
   }
   delete M;
   return CBH_OK;
@@ -2740,7 +2790,11 @@ int cbh_kselect_cols(cbh_ctx* ctx, const cbh_mat* A, const int32_t* active_index
   return CBH_OK;
 }
 
+static int prune_columns_impl(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, cbh_arena* ar, cbh_mat** C);
 int cbh_prune_columns(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, cbh_mat** C) {
+  return prune_columns_impl(ctx, A, thresh, nullptr, C);
+}
+static int prune_columns_impl(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, cbh_arena* ar, cbh_mat** C) {
   CBH_TRY(need_f64(ctx, A));
   if (!thresh || !C) return fail(ctx, CBH_E_ARG, "null argument");
   *C = nullptr;
@@ -2765,7 +2819,19 @@ int cbh_prune_columns(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, cbh_
   CBH_HIP(ctx, hipMemcpyAsync(&h[1], pos + nz, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   cbh_mat* out;
-  CBH_TRY(new_mat(ctx, A->m, A->n, h[0], h[1], A->dtype, &out));
+  if (ar && !ar->overflow && ar->vbytes == 8 && ar->used + h[0] <= ar->cap) {  // rows and values into the arena
+    CBH_TRY(new_mat(ctx, A->m, A->n, 0, h[1], A->dtype, &out));
+    dfree(ctx, out->ir);
+    dfree(ctx, out->num);
+    out->nnz = h[0];
+    out->ir = ar->ir + ar->used;
+    out->num = ar->num + ar->used * ar->vbytes;
+    out->borrowed_rows = true;
+    ar->used += h[0];
+  } else {
+    if (ar) ar->overflow = true;
+    CBH_TRY(new_mat(ctx, A->m, A->n, h[0], h[1], A->dtype, &out));
+  }
   hipLaunchKernelGGL(prune_col_kernel<true>, dim3(blocks_for(nz, 4)), dim3(256), 0, ctx->stream, A->jc, A->cp, A->ir,
                      num, nz, thresh, kept, off, out->ir, reinterpret_cast<double*>(out->num));
   hipLaunchKernelGGL(compact_cols_kernel, dim3(blocks_for(nz, 256)), dim3(256), 0, ctx->stream, kept, pos, A->jc, off,
@@ -2939,9 +3005,9 @@ int cbh_mat_col_concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** o
   C->dtype = parts[0]->dtype;
   C->vbytes = parts[0]->vbytes;
   const int64_t vb = C->vbytes;
-  auto release = [&](auto member) {
+  auto release = [&](auto member, bool rows) {  // rows: ir / num, which arena pieces only borrow
     for (int i = 0; i < k; ++i)
-      if (parts[i]->owned) {
+      if (parts[i]->owned && !(rows && parts[i]->borrowed_rows)) {
         dfree(ctx, parts[i]->*member);
         parts[i]->*member = nullptr;
       }
@@ -2966,8 +3032,8 @@ int cbh_mat_col_concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** o
     zoff += P->nzc;
   }
   CBH_HIP(ctx, hipGetLastError());
-  release(&cbh_mat::cp);
-  release(&cbh_mat::jc);
+  release(&cbh_mat::cp, false);
+  release(&cbh_mat::jc, false);
   if (std::getenv("CBH_MEMDIAG")) {
     size_t fr = 0, tot = 0;
     (void)hipMemGetInfo(&fr, &tot);
@@ -2985,8 +3051,7 @@ int cbh_mat_col_concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** o
                                   ctx->stream));
     eoff += parts[i]->nnz;
   }
-  release(&cbh_mat::ir);
-  release_cache(ctx);  // the parts' rows back to HIP before the largest allocation
+  release(&cbh_mat::ir, true);
   if (std::getenv("CBH_MEMDIAG")) {
     size_t fr = 0, tot = 0;
     (void)hipMemGetInfo(&fr, &tot);
@@ -3004,9 +3069,96 @@ int cbh_mat_col_concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** o
                                   hipMemcpyDeviceToDevice, ctx->stream));
     eoff += parts[i]->nnz;
   }
-  release(&cbh_mat::num);
+  release(&cbh_mat::num, true);
   CBH_HIP(ctx, hipMemcpyAsync(C->cp + nzc, &nnz, sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // nnz is a host local
+  CBH_HIP(ctx, hipGetLastError());
+  for (int i = 0; i < k; ++i) {
+    cbh_mat_free(ctx, parts[i]);
+    parts[i] = nullptr;
+  }
+  *out = C;
+  return CBH_OK;
+}
+
+int cbh_arena_create(cbh_ctx* ctx, int64_t capacity, int64_t value_bytes, cbh_arena** out) {
+  if (!ctx || !out || capacity < 0 || value_bytes <= 0) return fail(ctx, CBH_E_ARG, "bad arena arguments");
+  *out = nullptr;
+  cbh_arena* a = new cbh_arena;
+  a->cap = capacity;
+  a->vbytes = value_bytes;
+  int rc = dalloc(ctx, &a->ir, (size_t)capacity);
+  if (rc == CBH_OK) rc = dalloc(ctx, &a->num, (size_t)(capacity * value_bytes));
+  if (rc != CBH_OK) {
+    dfree(ctx, a->ir);
+    delete a;
+    return rc;
+  }
+  *out = a;
+  return CBH_OK;
+}
+int cbh_arena_destroy(cbh_ctx* ctx, cbh_arena* a) {
+  if (!a) return CBH_OK;
+  if (ctx) {
+    dfree(ctx, a->ir);
+    dfree(ctx, a->num);
+  }
+  delete a;
+  return CBH_OK;
+}
+// The pieces side by side (as cbh_mat_col_concat_consume). When they were all pruned into the arena,
+// back to back in order, their rows and values already form the result's arrays: the result takes
+// the arena's arrays over (the arena is left empty) and only the column pointers and ids are built.
+int cbh_arena_concat(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_arena* a, cbh_mat** out) {
+  if (!ctx || !out || k < 1 || !parts || !a) return fail(ctx, CBH_E_ARG, "bad arena concat arguments");
+  bool contiguous = !a->overflow;
+  int64_t off = 0, m = 0, n = 0, nzc = 0;
+  for (int i = 0; i < k && contiguous; ++i) {
+    const cbh_mat* P = parts[i];
+    if (!P) return fail(ctx, CBH_E_ARG, "null block");
+    if (P->nnz > 0 && (!P->borrowed_rows || P->ir != a->ir + off || static_cast<char*>(P->num) != a->num + off * a->vbytes))
+      contiguous = false;
+    off += P->nnz;
+  }
+  if (!contiguous || off != a->used) return cbh_mat_col_concat_consume(ctx, k, parts, out);
+  for (int i = 0; i < k; ++i) {
+    m = std::max(m, parts[i]->m);
+    n += parts[i]->n;
+    nzc += parts[i]->nzc;
+  }
+  cbh_mat* C = new cbh_mat;
+  C->m = m;
+  C->n = n;
+  C->nnz = off;
+  C->nzc = nzc;
+  C->dtype = parts[0]->dtype;
+  C->vbytes = parts[0]->vbytes;
+  int rc = dalloc(ctx, &C->cp, nzc + 1);
+  if (rc == CBH_OK) rc = dalloc(ctx, &C->jc, nzc);
+  if (rc != CBH_OK) {
+    cbh_mat_free(ctx, C);
+    return rc;
+  }
+  int64_t coff = 0, eoff = 0, zoff = 0;
+  for (int i = 0; i < k; ++i) {
+    const cbh_mat* P = parts[i];
+    if (P->nzc > 0) {
+      hipLaunchKernelGGL(add_const_i64_kernel, dim3(blocks_for(P->nzc, 256)), dim3(256), 0, ctx->stream, P->cp, P->nzc,
+                         eoff, C->cp + zoff);
+      hipLaunchKernelGGL(add_const_i64_kernel, dim3(blocks_for(P->nzc, 256)), dim3(256), 0, ctx->stream, P->jc, P->nzc,
+                         coff, C->jc + zoff);
+    }
+    coff += P->n;
+    eoff += P->nnz;
+    zoff += P->nzc;
+  }
+  C->ir = a->ir;  // the arena's arrays become the result's (capacity >= nnz)
+  C->num = a->num;
+  a->ir = nullptr;
+  a->num = nullptr;
+  a->cap = a->used = 0;
+  CBH_HIP(ctx, hipMemcpyAsync(C->cp + nzc, &off, sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // off is a host local
   CBH_HIP(ctx, hipGetLastError());
   for (int i = 0; i < k; ++i) {
     cbh_mat_free(ctx, parts[i]);
@@ -3065,9 +3217,20 @@ static int mcl_kselect(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const int64_t
   return CBH_OK;
 }
 
+static int mcl_prune_impl(cbh_ctx* ctx, const cbh_mat* A, double hardThreshold, int64_t selectNum, int64_t recoverNum,
+                          double recoverPct, cbh_allreduce_fn colsum, void* user, cbh_arena* ar, cbh_mat** C);
 extern "C" int cbh_mcl_prune_recovery_select(cbh_ctx* ctx, const cbh_mat* A, double hardThreshold, int64_t selectNum,
                                              int64_t recoverNum, double recoverPct, cbh_allreduce_fn colsum,
                                              void* user, cbh_mat** C) {
+  return mcl_prune_impl(ctx, A, hardThreshold, selectNum, recoverNum, recoverPct, colsum, user, nullptr, C);
+}
+extern "C" int cbh_mcl_prune_recovery_select_arena(cbh_ctx* ctx, const cbh_mat* A, double hardThreshold,
+                                                   int64_t selectNum, int64_t recoverNum, double recoverPct,
+                                                   cbh_allreduce_fn colsum, void* user, cbh_arena* ar, cbh_mat** C) {
+  return mcl_prune_impl(ctx, A, hardThreshold, selectNum, recoverNum, recoverPct, colsum, user, ar, C);
+}
+static int mcl_prune_impl(cbh_ctx* ctx, const cbh_mat* A, double hardThreshold, int64_t selectNum, int64_t recoverNum,
+                          double recoverPct, cbh_allreduce_fn colsum, void* user, cbh_arena* ar, cbh_mat** C) {
   CBH_TRY(need_f64(ctx, A));
   if (!C) return fail(ctx, CBH_E_ARG, "null output");
   *C = nullptr;
@@ -3106,7 +3269,7 @@ extern "C" int cbh_mcl_prune_recovery_select(cbh_ctx* ctx, const cbh_mat* A, dou
       CBH_TRY(mcl_kselect(ctx, S, A, s2, cnt, recoverNum, colsum, user, thresh));
     }
   }
-  return cbh_prune_columns(ctx, A, thresh, C);  // PruneColumn(pruneCols, less, true) (:343)
+  return prune_columns_impl(ctx, A, thresh, ar, C);  // PruneColumn(pruneCols, less, true) (:343)
 }
 
 // ============================================================================ format conversions

@@ -329,6 +329,22 @@ typedef int (*cbh_allreduce_fn)(void* user, void* dev_buf, int64_t count, int ty
 int cbh_mcl_prune_recovery_select(cbh_ctx* ctx, const cbh_mat* A, double hardThreshold, int64_t selectNum,
                                   int64_t recoverNum, double recoverPct, cbh_allreduce_fn colsum, void* user,
                                   cbh_mat** C);
+/* Output arena of the phased MCL drivers (MemEfficientSpGEMM, ParFriends.h:449-730): the pruned
+ * pieces of every phase are written back to back into one pair of row / value arrays of
+ * `capacity` entries, which cbh_arena_concat hands to the concatenated result without a copy -- a
+ * near-capacity product never holds its pieces and their concatenation at once (C5: 148 GB).
+ *   cbh_mcl_prune_recovery_select_arena  as cbh_mcl_prune_recovery_select; C's rows and values are
+ *       written into the arena when they fit (C then borrows them), else allocated as usual
+ *   cbh_arena_concat  the k pieces side by side (cbh_mat_col_concat_consume semantics: the parts are
+ *       freed and cleared); without a copy of rows and values when the parts tile the arena in order
+ *   cbh_arena_destroy frees whatever the arena still owns                                       */
+typedef struct cbh_arena cbh_arena;
+int cbh_arena_create(cbh_ctx* ctx, int64_t capacity, int64_t value_bytes, cbh_arena** out);
+int cbh_arena_destroy(cbh_ctx* ctx, cbh_arena* arena);
+int cbh_mcl_prune_recovery_select_arena(cbh_ctx* ctx, const cbh_mat* A, double hardThreshold, int64_t selectNum,
+                                        int64_t recoverNum, double recoverPct, cbh_allreduce_fn colsum, void* user,
+                                        cbh_arena* arena, cbh_mat** C);
+int cbh_arena_concat(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_arena* arena, cbh_mat** out);
 
 /* ---------------------------------------------------------------- block column operations
  *   cbh_mat_col_slice   columns [c0, c1) of M as a new m x (c1-c0) block, ids rebased

@@ -52,10 +52,15 @@ inline cbh_mat* col_concat(std::vector<cbh_mat*>& parts) {
 inline void memdiag(const char* where) {
   static const bool on = std::getenv("COMBBLAS_HIP_MEMDIAG") != nullptr;
   if (!on) return;
+  static double last = 0;
+  cbh_ctx_synchronize(context());
+  const double now = MPI_Wtime();
   int64_t live = 0, cached = 0, fr = 0, tot = 0;
   cbh_ctx_memory(context(), &live, &cached, &fr, &tot);
-  std::fprintf(stderr, "[memdiag] %-28s live %.2f GB, cached %.2f GB, device free %.2f of %.2f GB\n", where, live / 1e9,
-               cached / 1e9, fr / 1e9, tot / 1e9);
+  std::printf("[memdiag] %-28s +%8.1f ms  live %.2f GB, cached %.2f GB, device free %.2f of %.2f GB\n", where,
+              last > 0 ? (now - last) * 1e3 : 0.0, live / 1e9, cached / 1e9, fr / 1e9, tot / 1e9);
+  std::fflush(stdout);
+  last = now;
 }
 inline std::vector<int64_t> essentials(const cbh_mat* M) {  // {nnz, m, n, nzc}
   int64_t m = 0, n = 0, nnz = 0, nzc = 0;
@@ -93,13 +98,13 @@ inline int comm_allreduce_sum(void* user, void* buf, int64_t count, int type) {
 
 // MCLPruneRecoverySelect of a device block whose columns are split over `colworld`
 inline cbh_mat* mcl_prune_block(const cbh_mat* A, MPI_Comm colworld, double hard, int64_t selectNum,
-                                int64_t recoverNum, double recoverPct) {
+                                int64_t recoverNum, double recoverPct, cbh_arena* arena = nullptr) {
   int size = 1;
   MPI_Comm_size(colworld, &size);
   MPI_Comm comm = colworld;
   cbh_mat* C = nullptr;
-  int rc = cbh_mcl_prune_recovery_select(context(), A, hard, selectNum, recoverNum, recoverPct,
-                                         size > 1 ? comm_allreduce_sum : nullptr, &comm, &C);
+  int rc = cbh_mcl_prune_recovery_select_arena(context(), A, hard, selectNum, recoverNum, recoverPct,
+                                               size > 1 ? comm_allreduce_sum : nullptr, &comm, arena, &C);
   if (rc != CBH_OK) die(context(), rc, "cbh_mcl_prune_recovery_select");
   return C;
 }
@@ -369,9 +374,11 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
   if (phases < 1 || phases >= A.getncol()) phases = 1;
   // the plans (and their scratch) live for the phase loop only: the concatenation of the pruned
   // pieces below needs a second copy of them in HBM
+  combblas_hip::memdiag("MemEfficientSpGEMM start");
   std::unique_ptr<combblas_hip::StagePlans<IU, NU1, NU2>> SPp(
       new combblas_hip::StagePlans<IU, NU1, NU2>(A.seq(), A.getcommgrid().get(), B.seq(), B.getcommgrid().get()));
   combblas_hip::StagePlans<IU, NU1, NU2>& SP = *SPp;
+  combblas_hip::memdiag("stage plans");
   std::shared_ptr<CommGrid> GridC = SP.GridC;
   if (perProcessMemory > 0) {  // the reference's memory model (ParFriends.h:480-520), exact nnz per stage
     int p;
@@ -394,20 +401,48 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
   const IU C_n = B.seq().getncol();
   const auto cuts = combblas_hip::colsplit_cuts(C_n, phases);
   std::vector<cbh_mat*> toconcatenate;
+  // the pruned pieces go back to back into one arena whose arrays become C's: the memory beside
+  // A, B, the plans and the largest phase product (its share of the plans' nnz, 1.25x for uneven
+  // cuts and the prune's scratch), at most the unpruned nnz
+  cbh_arena* arena = nullptr;
+  {
+    cbh_ctx* ctx = combblas_hip::context();
+    int64_t live = 0, cached = 0, fr = 0, tot = 0;
+    cbh_ctx_memory(ctx, &live, &cached, &fr, &tot);
+    const int64_t eb = (int64_t)(sizeof(int32_t) + sizeof(NUO));
+    const int64_t phase_bytes = (int64_t)(1.25 * (double)SP.nnz / phases) * eb;
+    int64_t cap = (fr + cached - phase_bytes - (int64_t(8) << 30)) / eb;
+    cap = std::min<int64_t>(cap, SP.nnz);
+    if (cap > 0 && sizeof(NUO) == 8 && cbh_arena_create(ctx, cap, (int64_t)sizeof(NUO), &arena) != CBH_OK)
+      arena = nullptr;  // (no room: the pieces are allocated one by one and concatenated)
+  }
   combblas_hip::memdiag("phase loop start");
   for (int p = 0; p < phases; ++p) {
     cbh_mat* Cp = SP.piece(combblas_hip::semiring_traits<SR>::code, combblas_hip::dtype_of<NUO>::value,
                            (int64_t)sizeof(NUO), cuts[p], cuts[p + 1]);
     combblas_hip::memdiag("phase product");
     SpParMat<IU, NUO, UDERO> OnePieceOfC(new UDERO(Cp), GridC);
-    MCLPruneRecoverySelect(OnePieceOfC, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion);
+    // MCLPruneRecoverySelect (ParFriends.h:185-353) with its rows and values written into the arena
+    cbh_mat* Cpr = combblas_hip::mcl_prune_block(OnePieceOfC.seq().mat(), GridC->GetColWorld(), hardThreshold,
+                                                 (int64_t)selectNum, (int64_t)recoverNum, recoverPct, arena);
+    OnePieceOfC.seq().reset(Cpr);
     toconcatenate.push_back(OnePieceOfC.seq().release());
     combblas_hip::memdiag("phase pruned");
   }
   SPp.reset();
-  cbh_ctx_trim(combblas_hip::context());  // the cached scratch of the phase loop back to HIP
   combblas_hip::memdiag("before concatenation");
-  return SpParMat<IU, NUO, UDERO>(new UDERO(combblas_hip::col_concat(toconcatenate)), GridC);
+  cbh_mat* Cm = nullptr;
+  if (arena) {
+    const int rc = cbh_arena_concat(combblas_hip::context(), (int)toconcatenate.size(), toconcatenate.data(), arena, &Cm);
+    cbh_arena_destroy(combblas_hip::context(), arena);
+    if (rc != CBH_OK) combblas_hip::die(combblas_hip::context(), rc, "cbh_arena_concat");
+    toconcatenate.clear();
+  } else {
+    Cm = combblas_hip::col_concat(toconcatenate);
+  }
+  combblas_hip::memdiag("concatenated");
+  (void)kselectVersion;
+  return SpParMat<IU, NUO, UDERO>(new UDERO(Cm), GridC);
 }
 
 template <typename SR, typename NUO, typename UDERO, typename IU, typename NU1, typename NU2>
@@ -506,7 +541,6 @@ SpParMat3D<IU, NUO, UDERO> MemEfficientSpGEMM3D(SpParMat3D<IU, NU1, combblas_hip
   }
   (void)me;
   SPp.reset();
-  cbh_ctx_trim(combblas_hip::context());
   return SpParMat3D<IU, NUO, UDERO>(new UDERO(combblas_hip::col_concat(toconcatenate)),
                                     combblas_hip::product_grid3d(A), A.isColSplit(), A.isSpecial());
 }

@@ -92,7 +92,7 @@ int main(int argc, char** argv) {
   const int log2n = argc > 1 ? std::atoi(argv[1]) : 16;
   const int64_t deg = argc > 2 ? std::atoll(argv[2]) : 100;
   const int steps = argc > 3 ? std::atoi(argv[3]) : 2;
-  int phases = argc > 4 ? std::atoi(argv[4]) : 0;  // MCL.cpp's -phases; 0: C's phase blocks within 0.4 of free HBM
+  int phases = argc > 4 ? std::atoi(argv[4]) : 0;  // MCL.cpp's -phases; 0: C's phase blocks within 0.25 of free HBM
   const int ncheck = argc > 5 ? std::atoi(argv[5]) : 100;
   const int64_t stride = argc > 6 ? std::atoll(argv[6]) : 0;
   const int64_t n = int64_t(1) << log2n;
@@ -112,7 +112,7 @@ int main(int argc, char** argv) {
     if (phases <= 0) {  // as the Python mirror plans them (parfriends._budget_entries): 12-byte entries
       size_t fr = 0, tot = 0;
       (void)hipMemGetInfo(&fr, &tot);
-      const double budget = 0.4 * (double)fr / 12.0;
+      const double budget = 0.25 * (double)fr / 12.0;  // (room beside each phase for the output arena)
       phases = std::max(1, (int)std::ceil((double)nnzC / budget));
     }
     std::shared_ptr<CommGrid> grid(new CommGrid(MPI_COMM_WORLD, 1, 1));
@@ -135,7 +135,9 @@ int main(int argc, char** argv) {
         DMat Cs = run();
         cbh_ctx_synchronize(ctx);
         total += MPI_Wtime() - t0;
+        combblas_hip::memdiag("step returned");
       }
+      combblas_hip::memdiag("step result freed");
     }
     const double step_s = total / steps;
     cbh_ctx_enable_timing(ctx, 0);

@@ -163,3 +163,66 @@ def test_consuming_col_concat_matches_copy(ctx):
         assert np.array_equal(a, b) and np.array_equal(b, ref)
     for S in (C1, C2, dA):
         S.free()
+
+
+@pytest.mark.parametrize("cap_frac", [1.0, 0.3])
+def test_arena_prune_concat_matches_copying_path(ctx, cap_frac):
+    """The C++ phased MCL driver prunes each phase's piece into one output arena and hands the
+    arena's arrays to the concatenated result (cbh_mcl_prune_recovery_select_arena +
+    cbh_arena_concat); the result equals the copying path (separate pieces + consuming
+    concatenation). cap_frac 0.3: the arena overflows after the first piece(s) and the concat falls
+    back to copying, with the same result."""
+    import ctypes
+
+    import combblas_amd as cb
+    from combblas_amd._lib import check, lib
+
+    rng = np.random.default_rng(5)
+    A = cb.rmat(12)
+    h = cb.HostDcsc(A.m, A.n, A.jc, A.cp, A.ir, rng.integers(1, 1 << 20, A.nnz) / float(1 << 20))
+    dA, dB = cb.SpDCCols.from_host(ctx, h), cb.SpDCCols.from_host(ctx, h)
+    P = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dA, dB)
+    cuts = [0, 1000, 2500, A.n]
+    k = len(cuts) - 1
+    hard, sel, rec, pct = 1e-3, 40, 60, 0.9
+
+    def pieces():
+        out = []
+        for c0, c1 in zip(cuts[:-1], cuts[1:]):
+            s = ctypes.c_void_p()
+            check(lib().cbh_mat_col_slice(ctx.h, P.h, c0, c1, ctypes.byref(s)), ctx.h)
+            out.append(s.value)
+        return out
+
+    def pruned(arena):
+        res = []
+        for s in pieces():
+            o = ctypes.c_void_p()
+            if arena is None:
+                check(lib().cbh_mcl_prune_recovery_select(ctx.h, ctypes.c_void_p(s), hard, sel, rec, pct, None, None,
+                                                          ctypes.byref(o)), ctx.h)
+            else:
+                check(lib().cbh_mcl_prune_recovery_select_arena(ctx.h, ctypes.c_void_p(s), hard, sel, rec, pct, None,
+                                                                None, arena, ctypes.byref(o)), ctx.h)
+            check(lib().cbh_mat_free(ctx.h, ctypes.c_void_p(s)), ctx.h)
+            res.append(o.value)
+        return (ctypes.c_void_p * k)(*res)
+
+    p1 = pruned(None)
+    o1 = ctypes.c_void_p()
+    check(lib().cbh_mat_col_concat_consume(ctx.h, k, p1, ctypes.byref(o1)), ctx.h)
+    ar = ctypes.c_void_p()
+    nnz1 = cb.SpDCCols(ctx, o1, borrowed=True).nnz
+    check(lib().cbh_arena_create(ctx.h, max(1, int(cap_frac * nnz1)), 8, ctypes.byref(ar)), ctx.h)
+    p2 = pruned(ar)
+    o2 = ctypes.c_void_p()
+    check(lib().cbh_arena_concat(ctx.h, k, p2, ar, ctypes.byref(o2)), ctx.h)
+    check(lib().cbh_arena_destroy(ctx.h, ar), ctx.h)
+    assert all(p2[i] is None for i in range(k))
+    C1, C2 = cb.SpDCCols(ctx, o1), cb.SpDCCols(ctx, o2)
+    h1, h2 = C1.to_host(), C2.to_host()
+    assert h1.nnz == h2.nnz > 0
+    for a, b in ((h1.jc, h2.jc), (h1.cp, h2.cp), (h1.ir, h2.ir), (h1.num, h2.num)):
+        assert np.array_equal(a, b)
+    for S in (C1, C2, P, dA, dB):
+        S.free()
