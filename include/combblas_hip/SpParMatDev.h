@@ -153,9 +153,15 @@ inline ncclComm_t rccl_comm_for(MPI_Comm comm) {
   ncclUniqueId id;
   if (rank == 0) rccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
   MPI_Bcast(&id, (int)sizeof(id), MPI_BYTE, 0, comm);
-  // the context selects this rank's device; its cached blocks go back to HIP first, so that RCCL's
-  // own buffers find the memory (the block cache may hold a large share of the HBM)
-  cbh_ctx_trim(context());
+  // the context selects this rank's device; when little device memory is left, its cached blocks go
+  // back to HIP first, so that RCCL's own buffers find the memory (the block cache may
+  // hold a large share of the HBM). (Trimming unconditionally made every phased call -- a new
+  // ProductGrid, new communicators -- re-map the cache: 3 s per C5 step.)
+  {
+    int64_t fr = 0, tot = 0;
+    cbh_ctx_memory(context(), nullptr, nullptr, &fr, &tot);
+    if (fr < (int64_t(8) << 30)) cbh_ctx_trim(context());
+  }
   auto* c = new ncclComm_t;
   rccl_check(ncclCommInitRank(c, size, id, rank), "ncclCommInitRank");
   MPI_Comm_set_attr(comm, rccl_keyval(), c);
