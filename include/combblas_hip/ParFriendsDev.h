@@ -405,6 +405,7 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
   // A, B, the plans and the largest phase product (its share of the plans' nnz, 1.25x for uneven
   // cuts and the prune's scratch), at most the unpruned nnz
   cbh_arena* arena = nullptr;
+  int64_t* arena_hint = nullptr;
   {
     cbh_ctx* ctx = combblas_hip::context();
     int64_t live = 0, cached = 0, fr = 0, tot = 0;
@@ -413,6 +414,12 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
     const int64_t phase_bytes = (int64_t)(1.25 * (double)SP.nnz / phases) * eb;
     int64_t cap = (fr + cached - phase_bytes - (int64_t(8) << 30)) / eb;
     cap = std::min<int64_t>(cap, SP.nnz);
+    // an MCL iteration prunes to about the previous call's size: an arena sized from it (+15 %)
+    // leaves the phase blocks in the allocator's cache from call to call (an undersized arena only
+    // costs the copying concatenation)
+    static int64_t last_pruned = 0;
+    if (last_pruned > 0) cap = std::min<int64_t>(cap, last_pruned + last_pruned / 20 * 3);
+    arena_hint = &last_pruned;
     if (cap > 0 && sizeof(NUO) == 8 && cbh_arena_create(ctx, cap, (int64_t)sizeof(NUO), &arena) != CBH_OK)
       arena = nullptr;  // (no room: the pieces are allocated one by one and concatenated)
   }
@@ -441,6 +448,11 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
     Cm = combblas_hip::col_concat(toconcatenate);
   }
   combblas_hip::memdiag("concatenated");
+  if (arena_hint) {
+    int64_t nnz = 0;
+    cbh_mat_info(Cm, nullptr, nullptr, &nnz, nullptr, nullptr);
+    *arena_hint = nnz;
+  }
   (void)kselectVersion;
   return SpParMat<IU, NUO, UDERO>(new UDERO(Cm), GridC);
 }
