@@ -126,6 +126,13 @@ class Context:
         """return the built-in allocator's cached blocks and the phase workspace to HIP"""
         check(lib().cbh_ctx_trim(self.h), self.h)
 
+    def memory(self):
+        """{live, cached, device_free, device_total} in bytes: the built-in allocator's live and
+        cached (free, not yet returned to HIP) bytes and the device's free / total memory"""
+        v = [ctypes.c_int64() for _ in range(4)]
+        check(lib().cbh_ctx_memory(self.h, *[ctypes.byref(x) for x in v]), self.h)
+        return dict(zip(("live", "cached", "device_free", "device_total"), (x.value for x in v)))
+
     def take_retries(self):
         """sub-tiles the task kernels retried with half the row range since the last call (resets)"""
         n = ctypes.c_int64()

@@ -7,7 +7,9 @@ products) and require identical digests:
     never reused, so a use after free would change the digest;
   * the torch caching allocator on an explicit side stream while unrelated torch work allocates
     and frees on the default stream;
-  * cbh_ctx_trim between products.
+  * cbh_ctx_trim between products;
+  * the splitting pool for blocks >= 16 MiB (round 4): products whose phase pieces change size
+    reuse the pool's segments (no device memory taken beyond the first product's), digests equal.
 """
 import numpy as np
 import pytest
@@ -102,3 +104,60 @@ def test_trim_between_products(expected):
         ctx.close()
     for nnz, v, d in res:
         assert v == vs and d == dg, res
+
+
+def test_pool_reuses_segments_across_piece_sizes(oracle):
+    """R-MAT scale 16 A^2 (53.6 M outputs, a 644 MB result: pooled blocks) as a whole and as
+    column pieces of 1/3, 1/2 and 1/5 (pieces of different sizes, some held while the next is
+    formed): both whole products equal the oracle's digest, the pieces' nnz add up, every block
+    comes back (live returns to the inputs' bytes), and everything after the first product is
+    served from the pool's segments (device free memory never below what the first left)."""
+    import combblas_amd as cb
+
+    A = _gen(16)
+    vs, dg = H.digest(oracle.spgemm(A, A, "plus_times", threads=8))
+    ctx = cb.Context(0, torch_allocator=False)
+    try:
+        h = cb.HostDcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num)
+        dA = cb.SpDCCols.from_host(ctx, h)
+        dB = cb.SpDCCols.from_host(ctx, h)
+        base = ctx.memory()["live"]
+        n = A.n
+        C = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dA, dB)
+        first = C.checksum()
+        nnz = C.getnnz()
+        C.free()
+        ctx.synchronize()
+        mem = [ctx.memory()]
+        plan = cb.SpGEMMPlan(dA, dB)
+        for parts in (3, 2, 5):
+            cuts = [n * k // parts for k in range(parts + 1)]
+            held, tot = [], 0
+            for k in range(parts):
+                P = plan.multiply(cb.PlusTimesSRing, cuts[k], cuts[k + 1])
+                tot += P.getnnz()
+                held.append(P)
+                if len(held) == 2:  # two pieces alive at a time, freed oldest first
+                    held.pop(0).free()
+            for P in held:
+                P.free()
+            assert tot == nnz, (parts, tot, nnz)
+            ctx.synchronize()
+            mem.append(ctx.memory())
+        plan.close()
+        C = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dA, dB)
+        last = C.checksum()
+        C.free()
+        ctx.synchronize()
+        mem.append(ctx.memory())
+        dA.free()
+        dB.free()
+        end = ctx.memory()
+    finally:
+        ctx.close()
+    assert first == (vs, dg) and last == (vs, dg), (first, last, vs, dg)
+    assert mem[0]["live"] == base and mem[-1]["live"] == base, (base, mem)
+    assert len({m["live"] for m in mem[1:-1]}) == 1, mem  # the plan's arrays only
+    slack = 64 << 20
+    assert all(m["device_free"] >= mem[0]["device_free"] - slack for m in mem[1:]), mem
+    assert end["live"] == 0 and end["cached"] > 0, end
