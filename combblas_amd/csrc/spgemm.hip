@@ -209,6 +209,16 @@ static void shrink_cache(cbh_ctx* ctx, size_t keep) {
   }
   (void)hipGetLastError();
 }
+// the largest single block an allocation can get now: a free pool block as it is, or a new
+// mapping in what is free on the device plus what the cache can hand back whole (size classes and
+// fully free segments; free space inside a segment with live blocks is not returnable)
+static size_t alloc_room(cbh_ctx* ctx, size_t device_free) {
+  size_t back = 0;
+  for (auto& kv : ctx->cache) back += kv.first;
+  for (auto& w : ctx->pool.whole_segments()) back += w.first;
+  const size_t largest = ctx->pool.fr.empty() ? 0 : std::prev(ctx->pool.fr.end())->first;
+  return std::max(largest, device_free + back);
+}
 template <class T>
 static int dalloc(cbh_ctx* ctx, T** p, size_t count) {
   *p = nullptr;
@@ -1196,7 +1206,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
     CBH_HIP(ctx, hipMemGetInfo(&freeb, &totb));
     // within a fraction of the device (not of what is free: later calls find the earlier call's
     // bitmaps in the block cache and the phase workspace resident), densest classes first
-    const double cap_words = std::min(bmp_frac() * (double)totb, 0.9 * (double)(freeb + ctx->cached_bytes)) / 4.0;
+    const double cap_words = std::min(bmp_frac() * (double)totb, 0.9 * (double)alloc_room(ctx, freeb)) / 4.0;
     double words = 0;
     int min_class = kBmpClasses;
     while (min_class > 0 && words + (double)hc[min_class - 1] <= cap_words) words += (double)hc[--min_class];

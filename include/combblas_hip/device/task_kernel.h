@@ -804,7 +804,13 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
       CBH_STAMP(1);
       int cut = s_cut;
       if (dalign && tlo + 32 * (w0 + cut) < thi) {  // snap the window end down to a row-block boundary
-        const int64_t cb = (w0 + cut) / dbw * dbw - w0;
+        // (an absolute one: a column's first task starts at its first row's word, not on a block)
+#ifdef CBH_AB_RELSNAP
+        const int64_t tw0 = 0;
+#else
+        const int64_t tw0 = tlo / 32;
+#endif
+        const int64_t cb = (tw0 + w0 + cut) / dbw * dbw - tw0 - w0;
         if (cb > 0 && cb * 4 >= 3ll * cut) cut = (int)cb;
       }
       const int dtotal = cut < wl ? (int)dp[cut] : wtotal;
