@@ -192,6 +192,13 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: build it with `python -m combblas_amd.build` "
                               "(there is no CPU fallback)")
+        # torch ships its own HIP runtime (torch/lib/libamdhip64.so): it must be the process's one.
+        # Loaded after this library's (/opt/rocm's), torch later finds a device while this
+        # library's hipGetDeviceCount finds none (GPU box: cb.rmat before the first Context)
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             if os.environ.get("CBH_LIB") and not hasattr(L, name):

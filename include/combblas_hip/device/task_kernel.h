@@ -804,12 +804,9 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
       CBH_STAMP(1);
       int cut = s_cut;
       if (dalign && tlo + 32 * (w0 + cut) < thi) {  // snap the window end down to a row-block boundary
-        // (an absolute one: a column's first task starts at its first row's word, not on a block)
-#ifdef CBH_AB_RELSNAP
-        const int64_t tw0 = 0;
-#else
+        // (an absolute one: a column's first task starts at its first row's word, not on a block;
+        // relative snapping missed stop_search's one-load hub path: dense 300 -> 280 ms)
         const int64_t tw0 = tlo / 32;
-#endif
         const int64_t cb = (tw0 + w0 + cut) / dbw * dbw - tw0 - w0;
         if (cb > 0 && cb * 4 >= 3ll * cut) cut = (int)cb;
       }

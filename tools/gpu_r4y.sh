@@ -3,6 +3,8 @@
 # windows in a 8192-slot table's LDS (one group per CU), U 8 / 16
 set -o pipefail
 OUT=gpurun_out/r4y; mkdir -p $OUT; export TMPDIR=/tmp
+echo "== $(date +%T) preflight"
+timeout -k 10 180 python -c "import torch; print('torch sees', torch.cuda.device_count(), 'devices, available', torch.cuda.is_available())" || exit 1
 echo "== $(date +%T) pytest"
 timeout -k 10 700 python -u -m pytest tests/test_allocator_gpu.py tests/test_fallbacks_gpu.py tests/test_devpath3d_gpu.py tests/test_devpath_gpu.py -m gpu -x -v --timeout 180 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
