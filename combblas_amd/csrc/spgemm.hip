@@ -18,7 +18,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
-#include <set>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -29,7 +28,6 @@
 #include "convert.h"
 #include "blocks.h"
 #include "mclgen.h"
-#include "pool.h"
 
 using namespace cbh;
 
@@ -66,8 +64,6 @@ struct cbh_ctx {
   // for allocators outside the context (RCCL communicators, the caller); OOM and cbh_ctx_trim
   // still release the cache
   size_t cache_cap = size_t(128) << 30;
-  // large-block pool (requests >= kPoolMin, pool.h): hipMalloc'd segments split into blocks
-  BlockPool pool;
   bool poison = false;  // CBH_ALLOC_POISON=1: freed blocks are filled with 0xFF and never reused
   std::vector<void*> quarantine;
   std::vector<hipEvent_t> evpool;
@@ -137,41 +133,19 @@ static int fail(cbh_ctx* ctx, int code, const std::string& msg) {
   return code;
 }
 
-// Default device allocator: a per-context cache of hipMalloc'd memory, reused in stream order.
-// Every kernel and copy of a context runs on its one stream, so memory freed by an earlier call
+// Default device allocator: a per-context cache of hipMalloc'd blocks, reused in stream order.
+// Every kernel and copy of a context runs on its one stream, so a block freed by an earlier call
 // can be handed to a later allocation without a sync: the stream finishes the old users first.
 // (hipMallocAsync's default pool, used before, handed overlapping blocks to live allocations on
 // repeated phased products in processes where torch had not initialised HIP first.)
-// Two tiers:
-//  * requests below kPoolMin: size classes (512 B below 1 MiB, else 2 MiB); a cached block is
-//    reused for a request of at least half its size;
-//  * requests from kPoolMin up (round 4): a splitting pool. A request takes the best-fitting free
-//    block of any segment and splits off the rest; a freed block coalesces with free neighbours
-//    of its segment; new segments are hipMalloc'd at the request's size. A near-capacity phased
-//    driver whose pieces change size from phase to phase (C5's MemEfficientSpGEMM: unpruned
-//    pieces of 15-60 GB, a 180 GB output arena) then reuses its memory instead of re-mapping
-//    tens of GB per phase (hipMalloc + hipFree of a fresh block cost ~20 ms per GB).
-// `cached_bytes` counts both tiers' free bytes. Over cache_cap, on OOM and on cbh_ctx_trim the
-// cache shrinks: fully free segments and size-class blocks, largest first.
-// Debug mode CBH_ALLOC_POISON=1 (read at cbh_ctx_create): the pool is bypassed, a freed block is
-// overwritten with 0xFF on the stream and quarantined until the context is destroyed, so a use
-// after free reads NaN / -1 row ids instead of a later allocation's data
-// (tests/test_allocator_gpu.py).
-static constexpr size_t kPoolMin = size_t(16) << 20;
-static constexpr size_t kPoolQuantum = size_t(2) << 20;
+// Sizes are rounded to 512 B (< 1 MiB) or 2 MiB; a cached block is reused for a request of at
+// least half its size. On OOM the cache is released (after a stream sync) and the request retried;
+// it is also released when it grows past cache_cap, and on cbh_ctx_trim.
+// Debug mode CBH_ALLOC_POISON=1 (read at cbh_ctx_create): a freed block is overwritten with 0xFF
+// on the stream and quarantined until the context is destroyed, so a use after free reads NaN /
+// -1 row ids instead of a later allocation's data (tests/test_allocator_gpu.py).
 static size_t alloc_class(size_t bytes) {
   return bytes < (size_t(1) << 20) ? (bytes + 511) & ~size_t(511) : (bytes + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
-}
-// hipFree of every fully free pool segment, largest first, while the cache holds more than `keep`
-static size_t pool_shrink(cbh_ctx* ctx, size_t keep) {
-  size_t n = 0;
-  for (auto& w : ctx->pool.whole_segments()) {
-    if (ctx->cached_bytes <= keep) break;
-    ctx->cached_bytes -= ctx->pool.drop_segment(w.second);
-    (void)hipFree(w.second);
-    ++n;
-  }
-  return n;
 }
 static void release_cache(cbh_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
@@ -185,22 +159,21 @@ static void release_cache(cbh_ctx* ctx) {
       last = e;
     }
   }
-  const size_t nseg = pool_shrink(ctx, 0);
-  if (diag && (!ctx->cache.empty() || nseg))
-    std::fprintf(stderr, "[cbh memdiag] release_cache: %zu blocks, %zu segments, %d hipFree errors (%s)\n",
-                 ctx->cache.size(), nseg, nerr, hipGetErrorString(last));
+  if (diag && !ctx->cache.empty())
+    std::fprintf(stderr, "[cbh memdiag] release_cache: %zu blocks, %.2f GB, %d hipFree errors (%s)\n", ctx->cache.size(),
+                 ctx->cached_bytes / 1e9, nerr, hipGetErrorString(last));
   (void)hipGetLastError();
-  for (auto& kv : ctx->cache) ctx->cached_bytes -= kv.first;
   ctx->cache.clear();
+  ctx->cached_bytes = 0;
   for (void* q : ctx->quarantine) (void)hipFree(q);
   ctx->quarantine.clear();
 }
-// frees cached memory, largest first (fully free segments, then size-class blocks), until the
-// cache holds at most `keep` bytes (a near-capacity product re-maps only what it must)
+// frees cached blocks, largest first, until the cache holds at most `keep` bytes (round 4: a
+// near-capacity product re-maps only what it must; releasing the whole cache made the C5 C++
+// driver re-map ~150 GB per step, 30 ms per GB)
 static void shrink_cache(cbh_ctx* ctx, size_t keep) {
-  if (ctx->cached_bytes <= keep) return;
+  if (ctx->cached_bytes <= keep || ctx->cache.empty()) return;
   (void)hipStreamSynchronize(ctx->stream);
-  pool_shrink(ctx, keep);
   while (ctx->cached_bytes > keep && !ctx->cache.empty()) {
     auto it = std::prev(ctx->cache.end());
     (void)hipFree(it->second);
@@ -208,16 +181,6 @@ static void shrink_cache(cbh_ctx* ctx, size_t keep) {
     ctx->cache.erase(it);
   }
   (void)hipGetLastError();
-}
-// the largest single block an allocation can get now: a free pool block as it is, or a new
-// mapping in what is free on the device plus what the cache can hand back whole (size classes and
-// fully free segments; free space inside a segment with live blocks is not returnable)
-static size_t alloc_room(cbh_ctx* ctx, size_t device_free) {
-  size_t back = 0;
-  for (auto& kv : ctx->cache) back += kv.first;
-  for (auto& w : ctx->pool.whole_segments()) back += w.first;
-  const size_t largest = ctx->pool.fr.empty() ? 0 : std::prev(ctx->pool.fr.end())->first;
-  return std::max(largest, device_free + back);
 }
 template <class T>
 static int dalloc(cbh_ctx* ctx, T** p, size_t count) {
@@ -229,29 +192,19 @@ static int dalloc(cbh_ctx* ctx, T** p, size_t count) {
     if (!*p) return fail(ctx, CBH_E_OOM, "allocator callback failed for " + std::to_string(bytes) + " bytes");
     return CBH_OK;
   }
-  const bool pooled = bytes >= kPoolMin && !ctx->poison;
-  const size_t cls = pooled ? (bytes + kPoolQuantum - 1) & ~(kPoolQuantum - 1) : alloc_class(bytes);
-  if (pooled) {
-    if (char* q = ctx->pool.take(cls)) {
-      ctx->cached_bytes -= cls;
-      ctx->live[q] = cls;
-      *p = reinterpret_cast<T*>(q);
-      return CBH_OK;
-    }
-  } else {
-    auto it = ctx->cache.lower_bound(cls);
-    if (it != ctx->cache.end() && it->first / 2 <= cls) {
-      void* q = it->second;
-      ctx->live[q] = it->first;
-      ctx->cached_bytes -= it->first;
-      ctx->cache.erase(it);
-      *p = reinterpret_cast<T*>(q);
-      return CBH_OK;
-    }
+  const size_t cls = alloc_class(bytes);
+  auto it = ctx->cache.lower_bound(cls);
+  if (it != ctx->cache.end() && it->first / 2 <= cls) {
+    void* q = it->second;
+    ctx->live[q] = it->first;
+    ctx->cached_bytes -= it->first;
+    ctx->cache.erase(it);
+    *p = reinterpret_cast<T*>(q);
+    return CBH_OK;
   }
   void* q = nullptr;
   hipError_t e = hipMalloc(&q, cls);
-  if (e != hipSuccess && ctx->cached_bytes > 0) {  // give back cached memory, largest first, until it fits
+  if (e != hipSuccess && !ctx->cache.empty()) {  // give back cached blocks, largest first, until it fits
     (void)hipGetLastError();
     size_t fr = 0, tot = 0;
     (void)hipMemGetInfo(&fr, &tot);
@@ -259,7 +212,7 @@ static int dalloc(cbh_ctx* ctx, T** p, size_t count) {
     const size_t need = cls + margin > fr ? cls + margin - fr : 0;
     shrink_cache(ctx, ctx->cached_bytes > need ? ctx->cached_bytes - need : 0);
     e = hipMalloc(&q, cls);
-    if (e != hipSuccess && ctx->cached_bytes > 0) {
+    if (e != hipSuccess && !ctx->cache.empty()) {
       (void)hipGetLastError();
       release_cache(ctx);
       e = hipMalloc(&q, cls);
@@ -273,10 +226,8 @@ static int dalloc(cbh_ctx* ctx, T** p, size_t count) {
     for (auto& kv : ctx->live) live += kv.second;
     return fail(ctx, CBH_E_OOM, "hipMalloc(" + std::to_string(cls) + "): " + hipGetErrorString(e) + " (device free " +
                                     std::to_string(fr) + " of " + std::to_string(tot) + ", context live " +
-                                    std::to_string(live) + ", cached " + std::to_string(ctx->cached_bytes) +
-                                    ", workspace " + std::to_string(ctx->ws_bytes) + ")");
+                                    std::to_string(live) + ", workspace " + std::to_string(ctx->ws_bytes) + ")");
   }
-  if (pooled) ctx->pool.add_live_segment(reinterpret_cast<char*>(q), cls);
   ctx->live[q] = cls;
   *p = reinterpret_cast<T*>(q);
   return CBH_OK;
@@ -289,20 +240,15 @@ static void dfree(cbh_ctx* ctx, void* p) {
   }
   auto it = ctx->live.find(p);
   if (it == ctx->live.end()) return;  // not ours (wrapped device arrays are never freed here)
-  const size_t size = it->second;
-  ctx->live.erase(it);
   if (ctx->poison) {
-    (void)hipMemsetAsync(p, 0xFF, size, ctx->stream);
+    (void)hipMemsetAsync(p, 0xFF, it->second, ctx->stream);
     ctx->quarantine.push_back(p);
+    ctx->live.erase(it);
     return;
   }
-  if (ctx->pool.owns(p)) {
-    ctx->pool.put(reinterpret_cast<char*>(p), size);
-    ctx->cached_bytes += size;
-  } else {
-    ctx->cache.emplace(size, p);
-    ctx->cached_bytes += size;
-  }
+  ctx->cache.emplace(it->second, p);
+  ctx->cached_bytes += it->second;
+  ctx->live.erase(it);
   if (ctx->cached_bytes > ctx->cache_cap) shrink_cache(ctx, ctx->cache_cap);
 }
 
@@ -1206,7 +1152,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
     CBH_HIP(ctx, hipMemGetInfo(&freeb, &totb));
     // within a fraction of the device (not of what is free: later calls find the earlier call's
     // bitmaps in the block cache and the phase workspace resident), densest classes first
-    const double cap_words = std::min(bmp_frac() * (double)totb, 0.9 * (double)alloc_room(ctx, freeb)) / 4.0;
+    const double cap_words = std::min(bmp_frac() * (double)totb, 0.9 * (double)(freeb + ctx->cached_bytes)) / 4.0;
     double words = 0;
     int min_class = kBmpClasses;
     while (min_class > 0 && words + (double)hc[min_class - 1] <= cap_words) words += (double)hc[--min_class];
@@ -1487,9 +1433,7 @@ int cbh_ctx_destroy(cbh_ctx* ctx) {
   for (auto& e : ctx->pin_ev)
     if (e) (void)hipEventDestroy(e);
   release_cache(ctx);
-  for (auto& kv : ctx->live)  // matrices not freed by the caller
-    if (!ctx->pool.owns(kv.first)) (void)hipFree(kv.first);
-  for (auto& kv : ctx->pool.segs) (void)hipFree(kv.first);  // segments still holding live blocks
+  for (auto& kv : ctx->live) (void)hipFree(kv.first);  // matrices not freed by the caller
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return CBH_OK;
