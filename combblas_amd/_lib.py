@@ -60,6 +60,7 @@ SIGNATURES = {
     "cbh_ctx_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
     "cbh_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "cbh_ctx_trim": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbh_ctx_release": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "cbh_ctx_take_retries": (ctypes.c_int, [ctypes.c_void_p, c_int64_p]),
     "cbh_ctx_memory": (ctypes.c_int, [ctypes.c_void_p, c_int64_p, c_int64_p, c_int64_p, c_int64_p]),
     "cbh_hash_config": (ctypes.c_int, [c_int64_p, c_int64_p, c_int64_p]),

@@ -168,14 +168,16 @@ static void release_cache(cbh_ctx* ctx) {
   for (void* q : ctx->quarantine) (void)hipFree(q);
   ctx->quarantine.clear();
 }
-// frees cached blocks, largest first, until the cache holds at most `keep` bytes (round 4: a
-// near-capacity product re-maps only what it must; releasing the whole cache made the C5 C++
-// driver re-map ~150 GB per step, 30 ms per GB)
+// frees cached blocks until the cache holds at most `keep` bytes: each time the smallest block
+// that alone covers what is still to go, else the largest (a near-capacity product re-maps only
+// what it must, and a cache just over its cap keeps its big blocks: C5's C++ driver then reuses
+// its 190 GB output arena from the second call on instead of re-mapping it)
 static void shrink_cache(cbh_ctx* ctx, size_t keep) {
   if (ctx->cached_bytes <= keep || ctx->cache.empty()) return;
   (void)hipStreamSynchronize(ctx->stream);
   while (ctx->cached_bytes > keep && !ctx->cache.empty()) {
-    auto it = std::prev(ctx->cache.end());
+    auto it = ctx->cache.lower_bound(ctx->cached_bytes - keep);
+    if (it == ctx->cache.end()) it = std::prev(ctx->cache.end());
     (void)hipFree(it->second);
     ctx->cached_bytes -= it->first;
     ctx->cache.erase(it);
@@ -1401,11 +1403,12 @@ int cbh_ctx_create(int device, cbh_ctx** out) {
   if (const char* v = std::getenv("CBH_ALLOC_POISON")) c->poison = std::atoi(v) != 0;
   {
     size_t freeb = 0, totb = 0;
-    // 0.85 of the device: a phased near-capacity driver (C5's C++ MemEfficientSpGEMM) reuses its
-    // 200 GB output arena and phase blocks from step to step (0.5 re-mapped ~130 GB per step, 3 s);
-    // other allocators get memory back through the OOM path (largest cached blocks first) and the
-    // RCCL setup (trims when less than 8 GB is free)
-    if (hipMemGetInfo(&freeb, &totb) == hipSuccess && totb > 0) c->cache_cap = totb / 20 * 17;
+    // 0.9 of the device: a phased near-capacity driver (C5's C++ MemEfficientSpGEMM) reuses its
+    // 190 GB output arena and phase blocks from step to step (0.5 re-mapped ~130 GB per step, 3 s;
+    // 0.85 still re-mapped ~60 GB: 8.3 s per step against 2.8 s at 0.9); other
+    // allocators get memory back through the OOM path (largest cached blocks first) and the RCCL
+    // setup (releases what it needs when less than 8 GB is free)
+    if (hipMemGetInfo(&freeb, &totb) == hipSuccess && totb > 0) c->cache_cap = totb / 10 * 9;
   }
   if (const char* v = std::getenv("CBH_CACHE_CAP_GB")) c->cache_cap = size_t(std::atof(v) * double(size_t(1) << 30));
   for (auto& e : c->ev)
@@ -1471,6 +1474,13 @@ int cbh_ctx_trim(cbh_ctx* ctx) {
     ctx->ws = nullptr;
     ctx->ws_bytes = 0;
   }
+  CBH_HIP(ctx, hipGetLastError());
+  return CBH_OK;
+}
+
+int cbh_ctx_release(cbh_ctx* ctx, int64_t bytes) {
+  if (!ctx || bytes < 0) return CBH_E_ARG;
+  shrink_cache(ctx, ctx->cached_bytes > (size_t)bytes ? ctx->cached_bytes - (size_t)bytes : 0);
   CBH_HIP(ctx, hipGetLastError());
   return CBH_OK;
 }

@@ -126,6 +126,10 @@ class Context:
         """return the built-in allocator's cached blocks and the phase workspace to HIP"""
         check(lib().cbh_ctx_trim(self.h), self.h)
 
+    def release(self, nbytes):
+        """return at least nbytes of the built-in allocator's cached blocks to HIP, largest first"""
+        check(lib().cbh_ctx_release(self.h, int(nbytes)), self.h)
+
     def memory(self):
         """{live, cached, device_free, device_total} in bytes: the built-in allocator's live and
         cached (free, not yet returned to HIP) bytes and the device's free / total memory"""

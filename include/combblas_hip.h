@@ -93,6 +93,9 @@ int cbh_ctx_synchronize(cbh_ctx* ctx);
 /* Synchronize and return the context's cached device blocks and phase workspace to HIP (the
  * default allocator keeps freed blocks for reuse in stream order).                            */
 int cbh_ctx_trim(cbh_ctx* ctx);
+/* Synchronize and return at least `bytes` of the context's cached device blocks to HIP, largest
+ * first (all of them if fewer are cached); live blocks and the phase workspace stay. */
+int cbh_ctx_release(cbh_ctx* ctx, int64_t bytes);
 const char* cbh_last_error(cbh_ctx* ctx);
 /* Sub-tiles the task kernels retried with half the row range (table overflow, commit queue) since
  * the last call; resets the counter (diagnostics and tests). */

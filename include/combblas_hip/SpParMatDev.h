@@ -153,14 +153,16 @@ inline ncclComm_t rccl_comm_for(MPI_Comm comm) {
   ncclUniqueId id;
   if (rank == 0) rccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
   MPI_Bcast(&id, (int)sizeof(id), MPI_BYTE, 0, comm);
-  // the context selects this rank's device; when little device memory is left, its cached blocks go
-  // back to HIP first, so that RCCL's own buffers find the memory (the block cache may
-  // hold a large share of the HBM). (Trimming unconditionally made every phased call -- a new
-  // ProductGrid, new communicators -- re-map the cache: 3 s per C5 step.)
+  // the context selects this rank's device; when less than 8 GB of device memory is free, cached
+  // blocks go back to HIP (largest first, as many as make 8 GB free), so that RCCL's own buffers
+  // find the memory (the block cache may hold a large share of the HBM). (Trimming the
+  // whole cache made every phased call -- a new ProductGrid, new communicators -- re-map it:
+  // 3 s per C5 step.)
   {
     int64_t fr = 0, tot = 0;
+    const int64_t want = int64_t(8) << 30;
     cbh_ctx_memory(context(), nullptr, nullptr, &fr, &tot);
-    if (fr < (int64_t(8) << 30)) cbh_ctx_trim(context());
+    if (fr < want) cbh_ctx_release(context(), want - fr);
   }
   auto* c = new ncclComm_t;
   rccl_check(ncclCommInitRank(c, size, id, rank), "ncclCommInitRank");

@@ -109,7 +109,8 @@ def test_cache_accounting_across_piece_sizes(oracle):
     """R-MAT scale 16 A^2 (53.6 M outputs, a 644 MB result) as a whole and as column pieces of
     1/3, 1/2 and 1/5 (pieces of different sizes, some held while the next is formed), twice: both
     whole products equal the oracle's digest, the pieces' nnz add up, every block comes back to
-    the cache (live returns to the inputs' bytes), and cbh_ctx_trim hands the cache to HIP."""
+    the cache (live returns to the inputs' bytes), cbh_ctx_release hands back at least what
+    it is asked for and cbh_ctx_trim the rest."""
     import combblas_amd as cb
 
     A = _gen(16)
@@ -151,11 +152,15 @@ def test_cache_accounting_across_piece_sizes(oracle):
         dA.free()
         dB.free()
         end = ctx.memory()
+        half = end["cached"] // 2
+        ctx.release(half)  # at least half of the cache goes back, the rest stays cached
+        part = ctx.memory()
         ctx.trim()
         trimmed = ctx.memory()
     finally:
         ctx.close()
     assert first == (vs, dg) and last == (vs, dg), (first, last, vs, dg)
+    assert part["cached"] <= end["cached"] - half and part["device_free"] > end["device_free"], (end, part)
     assert trimmed["cached"] == 0 and trimmed["device_free"] > end["device_free"], (end, trimmed)
     assert mem[0]["live"] == base and mem[-1]["live"] == base, (base, mem)
     assert len({m["live"] for m in mem[1:-1]}) == 1, mem  # the plan's arrays only
