@@ -58,11 +58,10 @@ struct cbh_ctx {
   std::multimap<size_t, void*> cache;
   std::unordered_map<void*, size_t> live;
   size_t cached_bytes = 0;
-  // CBH_CACHE_CAP_GB; above it the cache is released. Default: half the device's memory -- a
-  // product near HBM capacity (scale-22 A^2: 108 GB of stored bitmaps) otherwise re-maps its
-  // scratch every call (4-5 s per call measured with a 64 GB cap), while the other half stays
-  // for allocators outside the context (RCCL communicators, the caller); OOM and cbh_ctx_trim
-  // still release the cache
+  // CBH_CACHE_CAP_GB; above it cached blocks go back to HIP (shrink_cache). Default, set at
+  // cbh_ctx_create: 0.9 of the device -- a product near HBM capacity (scale-22 A^2: 108 GB of
+  // stored bitmaps; C5's 190 GB output arena) otherwise re-maps its scratch every call; OOM,
+  // the RCCL setup (cbh_ctx_release) and cbh_ctx_trim give memory to other allocators
   size_t cache_cap = size_t(128) << 30;
   bool poison = false;  // CBH_ALLOC_POISON=1: freed blocks are filled with 0xFF and never reused
   std::vector<void*> quarantine;
@@ -139,8 +138,9 @@ static int fail(cbh_ctx* ctx, int code, const std::string& msg) {
 // (hipMallocAsync's default pool, used before, handed overlapping blocks to live allocations on
 // repeated phased products in processes where torch had not initialised HIP first.)
 // Sizes are rounded to 512 B (< 1 MiB) or 2 MiB; a cached block is reused for a request of at
-// least half its size. On OOM the cache is released (after a stream sync) and the request retried;
-// it is also released when it grows past cache_cap, and on cbh_ctx_trim.
+// least half its size. On OOM cached blocks go back to HIP (after a stream sync, as many as the
+// request needs, then all of them) and the request is retried; the cache also sheds blocks when
+// it grows past cache_cap, on cbh_ctx_release and (all) on cbh_ctx_trim.
 // Debug mode CBH_ALLOC_POISON=1 (read at cbh_ctx_create): a freed block is overwritten with 0xFF
 // on the stream and quarantined until the context is destroyed, so a use after free reads NaN /
 // -1 row ids instead of a later allocation's data (tests/test_allocator_gpu.py).
