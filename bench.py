@@ -36,7 +36,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
 # the task kernels of one product (bench kernel kinds -> rocprof names); the roofline line reports
 # the one with the most time per step
 KERNELS = {"num_large": "cbh::task_kernel<cbh::PlusTimesD<double>, 2048, 512, 512, 4, 1, false>",
-           "num_dense": "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 8, 2, false>",
+           # round 5: the dense tasks' kernel (device/dense_kernel.h; CBH_DENSE_V2=0 builds the round-4
+           # "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 8, 2, false>")
+           "num_dense": "cbh::dense_kernel<cbh::PlusTimesD<double>, 1024, 1024, 8, 163776>",
            "sym_large": "cbh::task_kernel<cbh::PlusTimesD<long>, 8192, 512, 512, 16, 0, false>"}
 # every task-kernel class of the f64 PlusTimes product (the application lines pick their dominant one)
 ALL_KERNELS = dict(KERNELS, **{
@@ -427,7 +429,7 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3), "higher_is_better": True,
-            "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "f64",
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: packed Graph500 R-MAT (seed 0xDECAFBAD), bit-identical to the reference generator",
             "config": {"workload": f"rmat{args.scale}_ef{args.edgefactor}_AxA_PlusTimes_f64", "scale": args.scale,
                        "edgefactor": args.edgefactor, "nnzA": nnzA, "flops": int(flops), "nnzC": int(nnzC),

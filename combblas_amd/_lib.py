@@ -67,6 +67,7 @@ SIGNATURES = {
     "cbh_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "cbh_ctx_set_allocator": (ctypes.c_int, [ctypes.c_void_p, ALLOC_FN, FREE_FN, ctypes.c_void_p]),
     "cbh_ctx_set_phase_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    "cbh_ctx_set_bitmap_fraction": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double]),
     "cbh_ctx_set_phase_consumer": (ctypes.c_int, [ctypes.c_void_p, PHASE_FN, ctypes.c_void_p]),
     "cbh_mat_upload": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cbh_dcsc), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_mat_upload_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(cbh_dcsc), ctypes.c_int64,

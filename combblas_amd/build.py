@@ -6,26 +6,41 @@ travels with the repository snapshot to the GPU box and is the library the tests
 from __future__ import annotations
 
 import os
+import re
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcombblas_hip.so")
 SOURCES = ["spgemm.hip", "rmat.cpp"]
-HEADERS = ["apps.h", "blocks.h", "convert.h", "host_util.h", "mclgen.h"] + [os.path.join("..", "..", "include", h) for h in (
-    "combblas_hip.h", "combblas_hip/device/semiring.h", "combblas_hip/device/block_ops.h",
-    "combblas_hip/device/task_kernel.h", "combblas_hip/device/wave_kernel.h",
-    "combblas_hip/device/numeric.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("CBH_OFFLOAD_ARCH", "gfx950")
+
+
+def _deps() -> list:
+    """the sources and every header they reach through #include "..." (quoted includes only)"""
+    seen, todo = set(), [os.path.join(CSRC, f) for f in SOURCES]
+    while todo:
+        f = os.path.normpath(todo.pop())
+        if f in seen or not os.path.exists(f):
+            continue
+        seen.add(f)
+        with open(f, errors="replace") as fh:
+            for line in fh:
+                m = _INC.match(line)
+                if m:
+                    todo.append(os.path.join(os.path.dirname(f), m.group(1)))
+    return sorted(seen)
+
+
+_INC = re.compile(r'\s*#\s*include\s+"([^"]+)"')
 
 
 def _stale(lib: str = LIB) -> bool:
     if not os.path.exists(lib):
         return True
     t = os.path.getmtime(lib)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    return any(os.path.getmtime(d) > t for d in _deps())
 
 
 def build(force: bool = False, verbose: bool = False, stamps: bool = False, variant: str = "",

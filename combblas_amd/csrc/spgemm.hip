@@ -38,6 +38,7 @@ struct cbh_ctx {
   bool own_stream = false;
   std::string err;
   int64_t phase_budget = 0;
+  double bmp_frac = -1.0;  // < 0: bmp_frac() (cbh_ctx_set_bitmap_fraction)
   bool timing = false;
   cbh_kernel_times times{-1, -1, -1, 0};
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -1000,6 +1001,7 @@ struct Plan {  // device arrays describing C = A*B (B's nonzero column slots, ta
   int32_t* gnx0 = nullptr;    // row at each committed cursor (double-buffered like gcur)
   int32_t* gnx1 = nullptr;
   int32_t* ghub = nullptr;    // hub id of each chunked entry's A column
+  int64_t* gbase = nullptr;   // its start (the stop search's column base)
   int64_t* boff = nullptr;    // ntasks + 1: stored-bitmap word offsets (see bmp_count_kernel)
   uint32_t* bmp = nullptr;    // null: no stored bitmaps (dense kernel off)
   int64_t total_flops = 0, total_nnz = 0;
@@ -1035,6 +1037,7 @@ static TaskArgs task_args(const cbh_mat* A, const cbh_mat* B, const Plan& P, cbh
   a.gnx0 = P.gnx0;
   a.gnx1 = P.gnx1;
   a.ghub = P.ghub;
+  a.gbase = P.gbase;
   a.boff = P.bmp ? P.boff : nullptr;
   a.bmp = P.bmp;
   return a;
@@ -1131,6 +1134,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
       CBH_TRY(S.get(&P.gnx0, (size_t)gtot));
       CBH_TRY(S.get(&P.gnx1, (size_t)gtot));
       CBH_TRY(S.get(&P.ghub, (size_t)gtot));
+      CBH_TRY(S.get(&P.gbase, (size_t)gtot));
     } else {
       P.goff = nullptr;
     }
@@ -1154,7 +1158,8 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
     CBH_HIP(ctx, hipMemGetInfo(&freeb, &totb));
     // within a fraction of the device (not of what is free: later calls find the earlier call's
     // bitmaps in the block cache and the phase workspace resident), densest classes first
-    const double cap_words = std::min(bmp_frac() * (double)totb, 0.9 * (double)(freeb + ctx->cached_bytes)) / 4.0;
+    const double frac = ctx->bmp_frac >= 0 ? ctx->bmp_frac : bmp_frac();
+    const double cap_words = std::min(frac * (double)totb, 0.9 * (double)(freeb + ctx->cached_bytes)) / 4.0;
     double words = 0;
     int min_class = kBmpClasses;
     while (min_class > 0 && words + (double)hc[min_class - 1] <= cap_words) words += (double)hc[--min_class];
@@ -1273,11 +1278,20 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
                        names[k], st[k][0], st[k][1], st[k][2], st[k][2] / std::max(1.0, st[k][1]),
                        st[k][1] / st[k][0], 100.0 * st[k][1] / std::max(1.0, st[k][3]));
     }
+#if CBH_DENSE_V2
+    CBH_TRY(timed_launch(ctx, CBH_K_NUM_DENSE, nb_d, [&] {
+      return launch_dense_numeric<SR>(a, bd.large_first, bd.large_count, ctx->stream);
+    }));
+#else
     CBH_TRY((launch_task_diag<SR, TNumLarge, MODE_TDENSE>(ctx, a, bd, "numeric dense")));
+#endif
     CBH_TRY((launch_task_diag<SR, TNumHash, MODE_TNUM>(ctx, a, bl, "numeric hash")));
   }
   if (!diag_enabled()) {
-    CBH_TRY((launch_task<SR, TNumLarge, MODE_TDENSE>(ctx, a, bd.large_first, bd.large_count, CBH_K_NUM_DENSE, nb_d)));
+    if (bd.large_count > 0)
+      CBH_TRY(timed_launch(ctx, CBH_K_NUM_DENSE, nb_d, [&] {
+        return launch_dense_numeric<SR>(a, bd.large_first, bd.large_count, ctx->stream);
+      }));
     CBH_TRY((launch_task<SR, TNumHash, MODE_TNUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
   }
   CBH_TRY((launch_task<SR, TNumMid, MODE_TNUM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_NUM_MID, nb_m)));
@@ -1536,6 +1550,12 @@ int cbh_ctx_set_phase_consumer(cbh_ctx* ctx, cbh_phase_fn fn, void* user) {
 int cbh_ctx_set_phase_budget(cbh_ctx* ctx, int64_t bytes) {
   if (!ctx || bytes < 0) return CBH_E_ARG;
   ctx->phase_budget = bytes;
+  return CBH_OK;
+}
+
+int cbh_ctx_set_bitmap_fraction(cbh_ctx* ctx, double frac) {
+  if (!ctx || frac > 1.0) return CBH_E_ARG;
+  ctx->bmp_frac = frac;
   return CBH_OK;
 }
 
@@ -2153,6 +2173,7 @@ int cbh_plan_numeric(cbh_plan* p, cbh_dtype dtype, int64_t value_bytes, uint32_t
   out->gnx0 = P.gnx0;
   out->gnx1 = P.gnx1;
   out->ghub = P.ghub;
+  out->gbase = P.gbase;
   out->boff = P.bmp ? P.boff : nullptr;
   out->bmp = P.bmp;
   out->err = ctx->d_err;

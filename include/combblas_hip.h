@@ -114,6 +114,11 @@ typedef void (*cbh_free_fn)(void* user, void* ptr, void* stream);
 int cbh_ctx_set_allocator(cbh_ctx* ctx, cbh_alloc_fn alloc, cbh_free_fn release, void* user);
 /* Workspace budget for cbh_spgemm_phased (bytes of output buffer per phase); 0 = auto. */
 int cbh_ctx_set_phase_budget(cbh_ctx* ctx, int64_t bytes);
+/* Share of the device's HBM one plan's stored dense-task bitmaps may take (default CBH_BMP_FRAC,
+ * 0.4); 0 = store none (the dense tasks run the hash kernels). Callers holding several plans at
+ * once (the C++ phase loop's stage plans) split one budget between them. A negative value
+ * restores the default.                                                                          */
+int cbh_ctx_set_bitmap_fraction(cbh_ctx* ctx, double frac);
 
 /* Copy a host DCSC into a new device matrix (SpParHelper::BCastMatrix receive side / upload). */
 int cbh_mat_upload(cbh_ctx* ctx, const cbh_dcsc* host, cbh_dtype dtype, cbh_mat** out);
@@ -247,6 +252,7 @@ typedef struct cbh_numeric_plan {
   int64_t mid_first, mid_count;                              /* mid-size hash tasks (<= 1024 out) */
   const int64_t* boff; uint32_t* bmp;                        /* stored row bitmaps of dense tasks */
   int32_t* ghub;                                             /* hub id of each chunked-task entry */
+  int64_t* gbase;                                            /* its A column's start              */
 } cbh_numeric_plan;
 /* bin every task for the hash kernels: the dense (bitmap-rank) kernel needs a lock-free SR::add
  * and 8-byte accumulators, the layout the plan's dense split is computed for (numeric.h

@@ -48,7 +48,7 @@ void SUMMALayer(combblas_hip::SpDCColsDev<IT, NT>& SplitA, combblas_hip::SpDCCol
     combblas_hip::SpDCColsDev<IT, NT>& Bi = (i == Bself) ? SplitB : Brecv;
     combblas_hip::BCastMatrix(CMG.rowWorld, Ai, Asizes[i], i);
     combblas_hip::BCastMatrix(CMG.colWorld, Bi, Bsizes[i], i);
-    (void)hipStreamSynchronize(reinterpret_cast<hipStream_t>(cbh_ctx_stream(combblas_hip::context())));
+    combblas_hip::hip_check(hipStreamSynchronize(reinterpret_cast<hipStream_t>(cbh_ctx_stream(combblas_hip::context()))), "hipStreamSynchronize");
     comm_bcast += MPI_Wtime() - bcast_beg;
     const double summa_beg = MPI_Wtime();
     cbh_mat* Ci = combblas_hip::local_multiply<PTNN, NT, NT, NT>(Ai.mat(), Bi.mat());
@@ -109,7 +109,7 @@ combblas_hip::SpDCColsDev<IT, NT>* multiply(combblas_hip::SpDCColsDev<IT, NT>& s
   std::vector<combblas_hip::SpDCColsDev<IT, NT>*> unreducedC;
   SUMMALayer(splitA, splitB, unreducedC, CMG, isBT, threaded);
   combblas_hip::SpDCColsDev<IT, NT>* C = ReduceAll_threaded<NT>(unreducedC, CMG);
-  (void)hipStreamSynchronize(reinterpret_cast<hipStream_t>(cbh_ctx_stream(combblas_hip::context())));
+  combblas_hip::hip_check(hipStreamSynchronize(reinterpret_cast<hipStream_t>(cbh_ctx_stream(combblas_hip::context()))), "hipStreamSynchronize");
   return C;
 }
 

@@ -17,7 +17,7 @@ namespace combblas_hip {
 // reference semiring type -> device functor
 template <class SR, class NT1, class NT2, class NTO>
 struct device_semiring {
-  using type = cbh::UserSRD<SR, NT1, NT2, NTO>;
+  using type = cbh::UserSRD<SR, NT1, NT2, NTO, reference_order<SR>::value>;
 };
 template <class T1, class T2, class NT1, class NT2, class NTO>
 struct device_semiring<combblas::PlusTimesSRing<T1, T2>, NT1, NT2, NTO> {
@@ -54,6 +54,26 @@ struct MinPlusPromoteD {
   static __device__ __forceinline__ NTO identity() { return NTO(); }
   static __device__ __forceinline__ NTO finalize(NTO a) { return a; }
 };
+// Select2ndSRing (Semirings.h:143-163): host-only functions restated; reference-order accumulation
+template <class OUT, class NT1, class NT2, class NTO>
+struct Select2ndD {
+  using a_t = NT1;
+  using b_t = NT2;
+  using val_t = NTO;
+  using acc_t = NTO;
+  static constexpr bool kLocked = true;
+  static constexpr bool kOrdered = true;
+  static __device__ __forceinline__ NTO multiply(const NT1&, const NT2& b) {
+    return static_cast<NTO>(static_cast<OUT>(b));
+  }
+  static __device__ __forceinline__ NTO add(const NTO&, const NTO& y) { return y; }
+  static __device__ __forceinline__ NTO identity() { return NTO(); }
+  static __device__ __forceinline__ NTO finalize(const NTO& a) { return a; }
+};
+template <class T1, class T2, class OUT, class NT1, class NT2, class NTO>
+struct device_semiring<combblas::Select2ndSRing<T1, T2, OUT>, NT1, NT2, NTO> {
+  using type = Select2ndD<OUT, NT1, NT2, NTO>;
+};
 template <class T1, class T2, class NT1, class NT2, class NTO>
 struct device_semiring<combblas::SelectMaxSRing<T1, T2>, NT1, NT2, NTO> {
   using type = SelectMaxPromoteD<NT1, NT2, NTO>;
@@ -66,7 +86,8 @@ struct device_semiring<combblas::MinPlusSRing<T1, T2>, NT1, NT2, NTO> {
 // C = A*B on the device for any (SR, NT1, NT2, NTO): library plan + caller-instantiated kernels.
 template <class SR, class NTO, class IT, class NT1, class NT2>
 combblas::SpTuples<IT, NTO>* DeviceLocalSpGEMM(const combblas::SpDCCols<IT, NT1>& A,
-                                               const combblas::SpDCCols<IT, NT2>& B, bool clearA, bool clearB) {
+                                               const combblas::SpDCCols<IT, NT2>& B, bool clearA, bool clearB,
+                                               int branch) {
   using DSR = typename device_semiring<SR, NT1, NT2, NTO>::type;
   static_assert(std::is_trivially_copyable<NTO>::value, "device values must be trivially copyable");
   const IT mdim = A.getnrow(), ndim = B.getncol();
@@ -90,7 +111,12 @@ combblas::SpTuples<IT, NTO>* DeviceLocalSpGEMM(const combblas::SpDCCols<IT, NT1>
     cbh_mat_device_arrays(c.m, &cp, &jc, &ir, &num);
     int64_t nnzC = 0;
     cbh_mat_info(c.m, nullptr, nullptr, &nnzC, nullptr, nullptr);
-    const hipError_t e = cbh::run_numeric_plan<DSR>(np, const_cast<int32_t*>(ir), const_cast<void*>(num), nnzC);
+    hipError_t e;
+    if constexpr (cbh::sr_ordered<DSR>::value)  // the reference's own per-column order
+      e = cbh::run_numeric_plan_ordered<DSR>(np, const_cast<int32_t*>(ir), const_cast<void*>(num), nnzC,
+                                              (int64_t)B.getnnz(), branch);
+    else
+      e = cbh::run_numeric_plan<DSR>(np, const_cast<int32_t*>(ir), const_cast<void*>(num), nnzC);
     if (e != hipSuccess) {
       std::fprintf(stderr, "combblas_hip: numeric launch failed: %s\n", hipGetErrorString(e));
       MPI_Abort(MPI_COMM_WORLD, CBH_E_HIP);
@@ -110,4 +136,4 @@ combblas::SpTuples<IT, NTO>* DeviceLocalSpGEMM(const combblas::SpDCCols<IT, NT1>
 
 #define COMBBLAS_HIP_DEVICE_KERNELS(SR, IT, NT1, NT2, NTO)                                                   \
   template combblas::SpTuples<IT, NTO>* combblas_hip::DeviceLocalSpGEMM<SR, NTO, IT, NT1, NT2>(            \
-      const combblas::SpDCCols<IT, NT1>&, const combblas::SpDCCols<IT, NT2>&, bool, bool);
+      const combblas::SpDCCols<IT, NT1>&, const combblas::SpDCCols<IT, NT2>&, bool, bool, int);

@@ -68,6 +68,32 @@ inline std::vector<int64_t> essentials(const cbh_mat* M) {  // {nnz, m, n, nzc}
   return {nnz, m, n, nzc};
 }
 // SpDCCols::ColSplit(parts) cuts: (i+1) * (n/parts), the last piece takes the remainder
+// phase cuts with an even share of the product's entries (cnt: exact nnz per column): the pieces
+// of a phase loop then have nearly one size, so the context allocator serves every phase from the
+// block the first one left in its cache (ColSplit's even column counts gave C5 pieces of 44 to
+// 58 GB, and each larger one re-mapped its block: 0.5-0.9 s per such phase). C does not depend on
+// the cuts.
+inline std::vector<int64_t> balanced_cuts(const std::vector<int64_t>& cnt, int parts) {
+  const int64_t n = (int64_t)cnt.size();
+  int64_t total = 0;
+  for (int64_t v : cnt) total += v;
+  std::vector<int64_t> c{0};
+  int64_t cum = 0, col = 0;
+  for (int p = 1; p < parts && col < n; ++p) {
+    const int64_t target = (int64_t)((double)total * p / parts);
+    while (col < n && cum < target) cum += cnt[(size_t)col++];  // the first column past the share
+    if (col <= c.back() && col < n) cum += cnt[(size_t)col++];  // every phase keeps >= 1 column
+    if (col >= n) break;
+    c.push_back(col);
+  }
+  c.push_back(n);
+  return c;
+}
+inline bool even_column_cuts() {  // COMBBLAS_HIP_EVEN_CUTS=1: the reference's ColSplit cuts
+  const char* e = std::getenv("COMBBLAS_HIP_EVEN_CUTS");
+  return e && std::atoi(e) != 0;
+}
+
 inline std::vector<int64_t> colsplit_cuts(int64_t n, int parts) {
   std::vector<int64_t> c{0};
   for (int i = 1; i < parts; ++i) c.push_back(i * (n / parts));
@@ -161,14 +187,14 @@ inline cbh_mat* fiber_reduce_scatter(cbh_semiring sr, cbh_mat* P, const std::vec
       for (int k = 0; k < 4; ++k) {
         std::vector<char> hs(a.b[k]), hr(b.b[k]);
         if (a.b[k]) {
-          (void)hipMemcpyAsync(hs.data(), a.p[k], a.b[k], hipMemcpyDeviceToHost, s);
-          (void)hipStreamSynchronize(s);
+          hip_check(hipMemcpyAsync(hs.data(), a.p[k], a.b[k], hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+          hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
         }
         MPI_Sendrecv(hs.data(), (int)a.b[k], MPI_BYTE, to, k, hr.data(), (int)b.b[k], MPI_BYTE, from, k, fiber,
                      MPI_STATUS_IGNORE);
         if (b.b[k]) {
-          (void)hipMemcpyAsync(b.p[k], hr.data(), b.b[k], hipMemcpyHostToDevice, s);
-          (void)hipStreamSynchronize(s);
+          hip_check(hipMemcpyAsync(b.p[k], hr.data(), b.b[k], hipMemcpyHostToDevice, s), "hipMemcpyAsync");
+          hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
         }
       }
     }
@@ -218,6 +244,9 @@ class StagePlans {
     auto Asizes = GetSetSizes(Aloc, GA->GetRowWorld());
     auto Bsizes = GetSetSizes(Bloc, GB->GetColWorld());
     const int Aself = GA->GetRankInProcRow(), Bself = GB->GetRankInProcCol();
+    // every stage's plan stays resident through the phase loop: their stored dense-task bitmaps
+    // share ONE budget (0.4 of the device) instead of taking up to 0.4 each
+    if (stages > 1) cbh_ctx_set_bitmap_fraction(context(), 0.4 / stages);
     for (int i = 0; i < stages; ++i) {
       SpDCColsDev<IU, NU1>* Ai = &Aloc;
       SpDCColsDev<IU, NU2>* Bi = &Bloc;
@@ -246,6 +275,7 @@ class StagePlans {
       plans.push_back(p);
       bjc.push_back(std::move(jc));
     }
+    if (stages > 1) cbh_ctx_set_bitmap_fraction(context(), -1.0);
   }
   ~StagePlans() {
     for (cbh_plan* p : plans)
@@ -279,6 +309,29 @@ class StagePlans {
     int rc = cbh_mat_rebase_cols(context(), out, c0, c1 - c0);
     if (rc != CBH_OK) die(context(), rc, "cbh_mat_rebase_cols");
     return out;
+  }
+  // exact nnz of every local column of C (n columns), summed over the stages' plans and then over
+  // `comm` (the processor column: MCLPruneRecoverySelect's column sums pair its ranks up, so they
+  // must cut their phases identically)
+  std::vector<int64_t> col_nnz(int64_t n, MPI_Comm comm) const {
+    std::vector<int64_t> cnt((size_t)n, 0);
+    for (size_t i = 0; i < plans.size(); ++i) {
+      if (!plans[i] || bjc[i].empty()) continue;
+      const size_t nzc = bjc[i].size();
+      int64_t* d = nullptr;
+      hip_check(hipMalloc(reinterpret_cast<void**>(&d), nzc * sizeof(int64_t)), "hipMalloc");
+      const int rc = cbh_plan_col_nnz(plans[i], d);
+      if (rc != CBH_OK) die(context(), rc, "cbh_plan_col_nnz");
+      std::vector<int64_t> h(nzc);
+      hip_check(hipStreamSynchronize(reinterpret_cast<hipStream_t>(cbh_ctx_stream(context()))), "hipStreamSynchronize");
+      hip_check(hipMemcpy(h.data(), d, nzc * sizeof(int64_t), hipMemcpyDeviceToHost), "hipMemcpy");
+      hip_check(hipFree(d), "hipFree");
+      for (size_t sl = 0; sl < nzc; ++sl) cnt[(size_t)bjc[i][sl]] += h[sl];
+    }
+    int csize = 1;
+    MPI_Comm_size(comm, &csize);
+    if (csize > 1) MPI_Allreduce(MPI_IN_PLACE, cnt.data(), (int)n, MPI_INT64_T, MPI_SUM, comm);
+    return cnt;
   }
   std::shared_ptr<combblas::CommGrid> GridC;
   int stages = 0;
@@ -399,11 +452,23 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
     if (remainingMem > 0) phases = 1 + (int)((asquareMem + kselectmem) / remainingMem);
   }
   const IU C_n = B.seq().getncol();
-  const auto cuts = combblas_hip::colsplit_cuts(C_n, phases);
+  // phase cuts: an even share of the exact entries per phase (balanced_cuts); the reference's even
+  // column counts with COMBBLAS_HIP_EVEN_CUTS=1. Either way C is the same matrix.
+  const std::vector<int64_t> ccnt = SP.col_nnz(C_n, GridC->GetColWorld());
+  const auto cuts = combblas_hip::even_column_cuts() ? combblas_hip::colsplit_cuts(C_n, phases)
+                                                     : combblas_hip::balanced_cuts(ccnt, phases);
+  phases = (int)cuts.size() - 1;
+  int64_t max_phase_nnz = 0;
+  for (int p = 0; p < phases; ++p) {
+    int64_t z = 0;
+    for (int64_t c = cuts[p]; c < cuts[p + 1]; ++c) z += ccnt[(size_t)c];
+    max_phase_nnz = std::max(max_phase_nnz, z);
+  }
   std::vector<cbh_mat*> toconcatenate;
   // the pruned pieces go back to back into one arena whose arrays become C's: the memory beside
-  // A, B, the plans and the largest phase product (its share of the plans' nnz, 1.25x for uneven
-  // cuts and the prune's scratch), at most the unpruned nnz
+  // A, B, the plans and the largest phase product (its exact nnz; twice that when the stage
+  // partials of a multi-stage grid are merged, plus 10 % for the prune's scratch), at most the
+  // unpruned nnz
   cbh_arena* arena = nullptr;
   int64_t* arena_hint = nullptr;
   {
@@ -411,7 +476,7 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
     int64_t live = 0, cached = 0, fr = 0, tot = 0;
     cbh_ctx_memory(ctx, &live, &cached, &fr, &tot);
     const int64_t eb = (int64_t)(sizeof(int32_t) + sizeof(NUO));
-    const int64_t phase_bytes = (int64_t)(1.25 * (double)SP.nnz / phases) * eb;
+    const int64_t phase_bytes = (int64_t)(1.1 * (double)max_phase_nnz * (SP.stages > 1 ? 2 : 1)) * eb;
     int64_t cap = (fr + cached - phase_bytes - (int64_t(8) << 30)) / eb;
     cap = std::min<int64_t>(cap, SP.nnz);
     // an MCL iteration prunes to about the previous call's size: an arena sized from it (+15 %)

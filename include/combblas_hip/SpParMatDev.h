@@ -114,6 +114,16 @@ inline bool use_mpi_transport() {
   return v;
 }
 
+// HIP runtime calls of the device drivers: a failed copy, event or synchronize (where an
+// asynchronous kernel fault surfaces) aborts the job with the HIP code, as rccl_check does for RCCL,
+// so a host-staged exchange can never ship stale host data over MPI
+inline void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    std::fprintf(stderr, "combblas_hip: %s failed: %s (%d)\n", what, hipGetErrorString(e), (int)e);
+    MPI_Abort(MPI_COMM_WORLD, CBH_E_HIP);
+  }
+}
+
 inline void rccl_check(ncclResult_t r, const char* what) {
   if (r != ncclSuccess) {
     std::fprintf(stderr, "combblas_hip: %s failed: %s\n", what, ncclGetErrorString(r));
@@ -129,7 +139,7 @@ inline void rccl_check(ncclResult_t r, const char* what) {
 // so it can never return an ncclComm with the wrong members.
 inline int rccl_comm_delete(MPI_Comm, int, void* attr, void*) {
   auto* c = static_cast<ncclComm_t*>(attr);
-  (void)hipStreamSynchronize(reinterpret_cast<hipStream_t>(cbh_ctx_stream(context())));
+  hip_check(hipStreamSynchronize(reinterpret_cast<hipStream_t>(cbh_ctx_stream(context()))), "hipStreamSynchronize");
   ncclCommDestroy(*c);
   delete c;
   return MPI_SUCCESS;
@@ -215,13 +225,13 @@ void bcast_arrays(MPI_Comm comm, SpDCColsDev<IT, NT>& M, const std::vector<IT>& 
       if (!x.bytes) continue;
       std::vector<char> h(x.bytes);
       if (rank == root) {
-        (void)hipMemcpyAsync(h.data(), x.p, x.bytes, hipMemcpyDeviceToHost, s);
-        (void)hipStreamSynchronize(s);
+        hip_check(hipMemcpyAsync(h.data(), x.p, x.bytes, hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+        hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
       }
       MPI_Bcast(h.data(), (int)x.bytes, MPI_BYTE, root, comm);
       if (rank != root) {
-        (void)hipMemcpyAsync(x.p, h.data(), x.bytes, hipMemcpyHostToDevice, s);
-        (void)hipStreamSynchronize(s);
+        hip_check(hipMemcpyAsync(x.p, h.data(), x.bytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync");
+        hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
       }
     }
     return;
@@ -340,21 +350,21 @@ void summa_overlap(SpDCColsDev<IU, NU1>& Aloc, combblas::CommGrid* GA, SpDCColsD
     (void)rccl_comm_for(cw);
     hipEvent_t ready;
     if (hipEventCreateWithFlags(&ready, hipEventDisableTiming) != hipSuccess) die(context(), CBH_E_HIP, "hipEventCreate");
-    (void)hipEventRecord(ready, ks);  // the receive blocks' memory: ordered after the context stream's work
-    (void)hipStreamWaitEvent(cs, ready, 0);
-    (void)hipEventDestroy(ready);
+    hip_check(hipEventRecord(ready, ks), "hipEventRecord");  // the receive blocks' memory: ordered after the context stream's work
+    hip_check(hipStreamWaitEvent(cs, ready, 0), "hipStreamWaitEvent");
+    hip_check(hipEventDestroy(ready), "hipEventDestroy");
     for (int i = 0; i < stages; ++i) {
       rccl_check(ncclGroupStart(), "ncclGroupStart");
       bcast_arrays(rw, Ai(i), Asizes[i], i, cs, true);
       bcast_arrays(cw, Bi(i), Bsizes[i], i, cs, true);
       rccl_check(ncclGroupEnd(), "ncclGroupEnd");
       if (hipEventCreateWithFlags(&done[i], hipEventDisableTiming) != hipSuccess) die(context(), CBH_E_HIP, "hipEventCreate");
-      (void)hipEventRecord(done[i], cs);
+      hip_check(hipEventRecord(done[i], cs), "hipEventRecord");
     }
   }
   for (int i = 0; i < stages; ++i) {
     if (overlap) {
-      (void)hipStreamWaitEvent(ks, done[i], 0);
+      hip_check(hipStreamWaitEvent(ks, done[i], 0), "hipStreamWaitEvent");
     } else {
       bcast_arrays(GridC->GetRowWorld(), Ai(i), Asizes[i], i, ks);
       bcast_arrays(GridC->GetColWorld(), Bi(i), Bsizes[i], i, ks);
@@ -368,7 +378,7 @@ void summa_overlap(SpDCColsDev<IU, NU1>& Aloc, combblas::CommGrid* GA, SpDCColsD
     if (i != Bself) Br[i].reset();
   }
   for (hipEvent_t e : done)
-    if (e) (void)hipEventDestroy(e);
+    if (e) hip_check(hipEventDestroy(e), "hipEventDestroy");
 }
 
 inline cbh_mat* merge_partials(cbh_semiring sr, std::vector<cbh_mat*>& parts, int64_t m, int64_t n, int dtype,

@@ -1,0 +1,502 @@
+// dense_kernel.h -- the DENSE numeric kernel (bitmap-rank windows) of the hash-SpGEMM's dense
+// tasks [LocalHybridSpGEMM, mtSpGEMM.h:289-441, for output columns whose rows are dense enough],
+// round 5 layout: ONE workgroup of BS threads per CU with the whole LDS, and wave-independent
+// product processing inside a window.
+//
+// What a dense task computes is unchanged from task_kernel<MODE_TDENSE> (task_kernel.h): the task's
+// output rows are the set bits of its row bitmap, stored by the symbolic pass; a WINDOW is a run of
+// bitmap words whose popcount prefix gives every row its output rank, so products accumulate at
+// their ranks (SR::lds_acc) and the commit writes values coalesced and rows off the bitmap.
+//
+// Why a new kernel: the round-4 dense kernel was bound by fetched bytes (383 GB per scale-22 phase
+// for 158 GB algorithmic, 87 % of the achievable fabric rate), and half of those bytes were paid per
+// ACTIVE ENTRY VISIT -- every window revisits every B entry whose A segment has products in it,
+// fetching the partial row / value lines at both ends of the segment and a hub-table line. The
+// visits per product fall with the window's width, and the window is bounded by LDS. So:
+//  * one 1024-thread workgroup per CU owns all 160 KB of LDS: about twice the rows per window of
+//    two 80 KB workgroups (the same 16 waves per CU);
+//  * that alone measured flat in round 3 because every phase of a window was block-synchronous
+//    (one latency chain per workgroup): here only the window's setup, the segment scan and the
+//    commit are block-wide; the products of a window are cut into one contiguous range per wave
+//    and every wave walks its range on its own (owner entry by a per-wave start map and a DPP
+//    max-scan, no owner-map barriers), so the waves' gathers overlap each other's latency.
+//
+// Per window, per chunk of <= EL entries (LDS-resident state when the task has <= EL entries,
+// HBM cursor state otherwise):
+//   phase 1 (thread per entry): segment [cursor, stop) inside the window (stop_search), the entry
+//           advanced; block scan of (length, active flag) -> the ACTIVE entries compacted to
+//           (start offset, gather base, B value) -- every compacted entry has >= 1 product, so at
+//           most 64 of them start inside any 64-product batch;
+//   phase 2 (wave-independent): wave w takes products [w*P/NW, (w+1)*P/NW); per step of up to
+//           64*U products the 64 entries after the current one write their start slot into the
+//           wave's byte map (one LDS load, one store each), a DPP max-scan per 64-product batch
+//           gives every lane its entry, and all U batches gather before any update (the multiply
+//           by B's value waits for the accumulate: a multiply right after its load made the
+//           compiler drain vmcnt per batch).
+#pragma once
+#include "wave_kernel.h"  // task_kernel.h, wave_lds_sync
+
+namespace cbh {
+
+// registers per thread that prefetch the next window's first words (the rest load at its start)
+#ifndef CBH_DENSE2_PREFETCH
+#define CBH_DENSE2_PREFETCH 8
+#endif
+
+template <class SR, int BS, int EL, int U, int LDSB>
+struct DenseCfg {
+  using acc_t = typename SR::acc_t;
+  using b_t = typename sr_b_type<SR>::type;
+  static constexpr int NW = BS / 64;
+  static constexpr size_t al(size_t x) { return (x + 15) & ~size_t(15); }
+  // entry state (LDS-resident tasks): cursor, row at the cursor, end - cursor, cursor - column
+  // start, hub id, B value
+  static constexpr size_t o_cur = 0;
+  static constexpr size_t o_nx = al(o_cur + sizeof(int64_t) * EL);
+  static constexpr size_t o_rem = al(o_nx + sizeof(int32_t) * EL);
+  static constexpr size_t o_coff = al(o_rem + sizeof(int32_t) * EL);
+  static constexpr size_t o_hub = al(o_coff + sizeof(int32_t) * EL);
+  static constexpr size_t o_scale = al(o_hub + sizeof(int32_t) * EL);
+  // compacted active entries of the current chunk: start offset (+ the total at [nact]), gather
+  // base (cursor - start offset), B value
+  static constexpr size_t o_cstart = al(o_scale + sizeof(b_t) * EL);
+  static constexpr size_t o_cbase = al(o_cstart + sizeof(int32_t) * (EL + 1));
+  static constexpr size_t o_cscale = al(o_cbase + sizeof(int64_t) * EL);
+  static constexpr size_t o_own = al(o_cscale + sizeof(b_t) * EL);  // NW x 512-byte owner maps
+  static constexpr size_t o_red = al(o_own + 512 * NW);
+  static constexpr size_t o_win = al(o_red + sizeof(int32_t) * (4 * NW + 8));
+  // the window: values from the bottom, the window's words and int16 prefixes (6 B per word) from
+  // the top (as task_kernel's dense windows)
+  static constexpr size_t TB = (LDSB - o_win) & ~size_t(15);
+  static constexpr size_t bytes = o_win + TB;
+  static constexpr int NWB = (int)((TB - 64) / 6) / 8 * 8;  // widest window (all words, no values)
+  static_assert(NWB <= 32767, "int16 window prefixes");
+  static_assert(bytes <= 163840, "one workgroup's LDS");
+  static_assert(EL == BS, "one entry per thread per chunk");
+  static_assert(U >= 1 && U <= 8, "a lane's owner counts are the 8 bytes of one word");
+};
+
+// exclusive block scan of two ints per thread (thread order); totals in ta / tb. Uses red[0, 2*NW).
+template <int BS>
+__device__ __forceinline__ void block_excl_sum2(int& a, int& b, int* red, int& ta, int& tb) {
+  constexpr int NW = BS / 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int sa = wave_incl_sum(a), sb = wave_incl_sum(b);
+  __syncthreads();  // red may still be read by a previous user
+  if (lane == 63) {
+    red[wid] = sa;
+    red[NW + wid] = sb;
+  }
+  __syncthreads();
+  int pa = 0, pb = 0, xa = 0, xb = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const int ra = red[w], rb = red[NW + w];
+    pa += (w < wid) ? ra : 0;
+    pb += (w < wid) ? rb : 0;
+    xa += ra;
+    xb += rb;
+  }
+  a = pa + sa - a;
+  b = pb + sb - b;
+  ta = xa;
+  tb = xb;
+}
+
+template <class SR, int BS, int EL, int U, int LDSB>
+__global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves per CU
+  using C = DenseCfg<SR, BS, EL, U, LDSB>;
+  using val_t = typename SR::val_t;
+  using acc_t = typename SR::acc_t;
+  using a_t = typename sr_a_type<SR>::type;
+  using b_t = typename C::b_t;
+  constexpr int NW = C::NW;
+  static_assert(!sr_locked<SR>::value, "the dense kernel accumulates with SR::lds_acc");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int64_t* scur = reinterpret_cast<int64_t*>(smem + C::o_cur);
+  int32_t* snx = reinterpret_cast<int32_t*>(smem + C::o_nx);
+  int32_t* srem = reinterpret_cast<int32_t*>(smem + C::o_rem);
+  int32_t* scoff = reinterpret_cast<int32_t*>(smem + C::o_coff);
+  int32_t* shub = reinterpret_cast<int32_t*>(smem + C::o_hub);
+  b_t* sscale = reinterpret_cast<b_t*>(smem + C::o_scale);
+  int32_t* cstart = reinterpret_cast<int32_t*>(smem + C::o_cstart);
+  int64_t* cbase = reinterpret_cast<int64_t*>(smem + C::o_cbase);
+  b_t* cscale = reinterpret_cast<b_t*>(smem + C::o_cscale);
+  int32_t* red = reinterpret_cast<int32_t*>(smem + C::o_red);
+  unsigned char* win = smem + C::o_win;
+  acc_t* vals = reinterpret_cast<acc_t*>(win);
+  __shared__ int32_t s_cut;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int32_t* own = reinterpret_cast<int32_t*>(smem + C::o_own + 512 * wid);
+  const int32_t* __restrict__ rowsA = a.Air;
+  const a_t* __restrict__ valsA = reinterpret_cast<const a_t*>(a.Anum);
+  if ((int64_t)blockIdx.x >= a.norder) return;
+  const int32_t task = a.order[blockIdx.x];
+  if (task < 0 || task >= a.ntasks) {
+    if (tid == 0) guard_fail(a.err, 9, task);
+    return;
+  }
+  const int32_t c = a.tcol[task];
+  const int64_t e0 = a.Bcp[c];
+  const int64_t ne = a.Bcp[c + 1] - e0;
+  const int64_t work = a.twork[task];
+  const int32_t tlo = a.tlo[task], thi = a.thi[task];
+  const uint8_t full = a.tfull[task];
+  if (work <= 0 || thi <= tlo) return;
+  const int64_t span = (int64_t)thi - tlo;
+  const bool chunked = ne > EL;
+  const int nchunks = (int)((ne + EL - 1) / EL);
+  const int64_t go = chunked ? a.goff[task] : 0;
+  int bad = 0;
+  auto hub_tab = [&](int32_t h) -> const int2* {
+    return reinterpret_cast<const int2*>(a.htab) + (int64_t)h * (a.nblk + 2) + 1;
+  };
+
+  // An entry's state at its first visit: the cursor at the first row >= lo of its A column clamped
+  // to the task's rows (the block table of a hub column gives both ends at row-block boundaries)
+  struct Ent {
+    int64_t cur;
+    int32_t nx, rem, coff, hub;
+    b_t scale;
+  };
+  auto first_visit = [&](int64_t i, int32_t lo, bool lo_is_start) -> Ent {
+    Ent e;
+    const int64_t p = e0 + i;
+    const int32_t k = a.Bir[p];
+    e.scale = reinterpret_cast<const b_t*>(a.Bnum)[p];
+    e.cur = 0;
+    e.nx = kNoRow;
+    e.rem = e.coff = 0;
+    e.hub = -1;
+    if (k < 0 || k >= a.ncolA) {
+      bad |= 1 << 1;
+      return e;
+    }
+    int64_t base = a.Acp[k], end = a.Acp[k + 1];
+    if (base < 0 || end < base || end > a.nnzA) {
+      bad |= 1 << 2;
+      return e;
+    }
+    const int32_t h = (base < end && a.RB > 0) ? a.hidx[k] : -1;
+    const int2* blk = h >= 0 ? hub_tab(h) : nullptr;
+    int64_t cend = end;
+    if (!(full & 2) && base < end) {
+      if (blk && thi % a.RB == 0) cend = base + blk[thi / a.RB].x;
+      else cend = lb_rows64(rowsA, base, end, thi);
+    }
+    int64_t pos = base;
+    int32_t known = kUnknownRow;
+    if (!lo_is_start && base < cend) {
+      if (blk && lo % a.RB == 0) {
+        const int2 t = blk[lo / a.RB];
+        pos = base + t.x;
+        known = t.y;
+      } else {
+        pos = lb_rows64(rowsA, base, cend, lo);
+      }
+      if (pos > cend) pos = cend;
+    }
+    e.cur = pos;
+    e.nx = pos < cend ? known : kNoRow;
+    e.rem = (int32_t)(cend - pos);
+    e.coff = (int32_t)(pos - base);
+    e.hub = h;
+    if (chunked) {
+      a.gend[go + i] = cend;
+      a.gbase[go + i] = base;
+      a.ghub[go + i] = h;
+    }
+    return e;
+  };
+  if (!chunked) {
+    if (tid < ne) {
+      const Ent e = first_visit(tid, tlo, (full & 1) != 0);
+      scur[tid] = e.cur;
+      snx[tid] = e.nx;
+      srem[tid] = e.rem;
+      scoff[tid] = e.coff;
+      shub[tid] = e.hub;
+      sscale[tid] = e.scale;
+    }
+  }
+
+  int64_t out_pos = a.toff[task] - a.cbase;
+  const int64_t out_end = a.toff[task + 1] - a.cbase;
+  const int64_t bw0 = a.boff[task];
+  const int64_t nwt = a.boff[task + 1] - bw0;
+  if (a.bmp == nullptr || nwt != (span + 31) / 32) {
+    if (tid == 0) guard_fail(a.err, 10, c, task, nwt, span);
+    return;
+  }
+  const uint32_t* __restrict__ tb = a.bmp + bw0;
+  constexpr int64_t TB = (int64_t)C::TB;
+  int64_t wdes = TB * nwt / ((int64_t)sizeof(acc_t) * work + 6 * nwt);  // words whose outputs fill the rest
+  wdes = wdes < 64 ? 64 : (wdes > C::NWB ? C::NWB : wdes);
+  const bool dalign = kAlignSubtiles && a.RB > 0 && (a.RB & 31) == 0 && (tlo & 31) == 0;
+  const int64_t dbw = dalign ? a.RB / 32 : 1;  // words per row block
+  bool inited = !chunked;
+  constexpr int KW0 = (C::NWB + BS - 1) / BS;
+  constexpr int KW = KW0 < CBH_DENSE2_PREFETCH ? KW0 : CBH_DENSE2_PREFETCH;
+  uint32_t pre[KW > 0 ? KW : 1];
+  int64_t pre_w0 = -1;
+  int64_t w0 = 0;
+  __syncthreads();
+  while (w0 < nwt) {
+    const int wl = (int)((nwt - w0) < wdes ? (nwt - w0) : wdes);
+    const int dbase = (int)((TB - 6 * wl) & ~int64_t(15));
+    uint32_t* dw = reinterpret_cast<uint32_t*>(win + dbase);
+    int16_t* dp = reinterpret_cast<int16_t*>(win + dbase + 4 * wl);
+    const int capv = dbase / (int)sizeof(acc_t);
+    const int kw = (wl + BS - 1) / BS;
+    {
+      int x = tid;
+      if (pre_w0 == w0) {
+#pragma unroll
+        for (int j = 0; j < KW; ++j)
+          if (tid + j * BS < wl) dw[tid + j * BS] = pre[j];
+        x += KW * BS;
+      }
+      for (; x < wl; x += BS) dw[x] = tb[w0 + x];
+    }
+    if (tid == 0) s_cut = wl;
+    __syncthreads();
+    int tsum = 0;
+    for (int k = 0; k < kw; ++k) {
+      const int x = tid * kw + k;
+      tsum += x < wl ? __popc(dw[x]) : 0;
+    }
+    int wtotal = 0;
+    int ex = block_excl_sum<BS>(tsum, red, wtotal);
+    for (int k = 0; k < kw; ++k) {
+      const int x = tid * kw + k;
+      if (x < wl) {
+        const int pc = __popc(dw[x]);
+        dp[x] = (int16_t)(ex < 32767 ? ex : 32767);
+        if (ex <= capv && ex + pc > capv) s_cut = x;
+        ex += pc;
+      }
+    }
+    __syncthreads();
+    int cut = __builtin_amdgcn_readfirstlane(s_cut);  // (block-uniform values kept in SGPRs)
+    if (dalign && tlo + 32 * (w0 + cut) < thi) {  // window ends snap down to absolute row blocks
+      const int64_t tw0 = tlo / 32;
+      const int64_t cb = (tw0 + w0 + cut) / dbw * dbw - tw0 - w0;
+      if (cb > 0 && cb * 4 >= 3ll * cut) cut = (int)cb;
+    }
+    const int dtotal = __builtin_amdgcn_readfirstlane(cut < wl ? (int)dp[cut] : wtotal);
+    // the next window's words, loaded before this window's commit (not before its products: KW
+    // registers live across the product phase spilled)
+    auto prefetch_next = [&]() {
+      const int64_t w0n = w0 + cut;
+      if (KW > 0 && w0n < nwt) {
+        const int wln = (int)((nwt - w0n) < wdes ? (nwt - w0n) : wdes);
+#pragma unroll
+        for (int j = 0; j < KW; ++j) pre[j] = (tid + j * BS < wln) ? tb[w0n + tid + j * BS] : 0u;
+        pre_w0 = w0n;
+      }
+    };
+    const int32_t lo = (int32_t)(tlo + 32 * w0);
+    const int64_t hcut = tlo + 32 * (w0 + cut);
+    const int32_t hi = (int32_t)(hcut < thi ? hcut : thi);
+    const bool hi_is_end = hi == thi;
+    const uint32_t tw = (uint32_t)(hi - lo);
+    if (dtotal > 0) {
+      for (int x = tid; x < dtotal; x += BS) vals[x] = SR::identity();
+      for (int ch = 0; ch < nchunks; ++ch) {
+        // ---- phase 1: this chunk's entries (thread per entry)
+        const int64_t i = (int64_t)ch * EL + tid;
+        int len = 0;
+        int64_t cur0 = 0;
+        b_t scale{};
+        if (i < ne) {
+          Ent e;
+          if (!chunked) {
+            e.cur = scur[tid];
+            e.nx = snx[tid];
+          } else if (!inited) {
+            e = first_visit(i, lo, lo == tlo && (full & 1));
+          } else {
+            e.cur = a.gcur0[go + i];
+            e.nx = a.gnx0[go + i];
+          }
+          cur0 = e.cur;
+          if (e.nx < hi) {
+            if (!chunked) {
+              e.rem = srem[tid];
+              e.coff = scoff[tid];
+              e.hub = shub[tid];
+              e.scale = sscale[tid];
+            } else if (inited) {
+              e.hub = a.ghub[go + i];
+              e.rem = (int32_t)(a.gend[go + i] - e.cur);
+              e.coff = e.hub >= 0 ? (int32_t)(e.cur - a.gbase[go + i]) : 0;
+              e.scale = reinterpret_cast<const b_t*>(a.Bnum)[e0 + i];
+            }
+            int64_t stop;
+            int32_t nx2;
+            if (hi_is_end) {
+              stop = e.cur + e.rem;
+              nx2 = kNoRow;
+            } else {
+              const int2* blk = e.hub >= 0 ? hub_tab(e.hub) : nullptr;
+              stop = stop_search<8>(rowsA, e.nx == kUnknownRow ? e.cur : e.cur + 1, e.cur + e.rem, hi, blk,
+                                    e.cur - e.coff, a.RB, nx2);
+            }
+            len = (int)(stop - e.cur);
+            scale = e.scale;
+            if (!chunked) {
+              scur[tid] = stop;
+              snx[tid] = nx2;
+              srem[tid] = e.rem - len;
+              scoff[tid] = e.coff + len;
+            } else {
+              a.gcur0[go + i] = stop;
+              a.gnx0[go + i] = nx2;
+            }
+          } else if (chunked && !inited) {  // an idle first visit: its state is committed as is
+            a.gcur0[go + i] = e.cur;
+            a.gnx0[go + i] = e.nx;
+          }
+        }
+        int off = len, aidx = len > 0 ? 1 : 0;
+        int P = 0, nact = 0;
+        block_excl_sum2<BS>(off, aidx, red, P, nact);
+        P = __builtin_amdgcn_readfirstlane(P);
+        nact = __builtin_amdgcn_readfirstlane(nact);
+        if (len > 0) {
+          cstart[aidx] = off;
+          cbase[aidx] = cur0 - off;
+          cscale[aidx] = scale;
+        }
+        if (tid == 0) cstart[nact] = P;
+        __syncthreads();
+        // ---- phase 2: wave w walks products [w*P/NW, (w+1)*P/NW) on its own
+        const int pb = (int)((int64_t)P * wid / NW), pe = (int)((int64_t)P * (wid + 1) / NW);
+        if (pb < pe) {
+          // the compacted entry owning product pb: the last one starting at or before it
+          int elo = 0;
+          {
+            int l0 = 0, h0 = nact;  // cstart[0] = 0 <= pb < P = cstart[nact]
+            while (h0 - l0 > 1) {
+              const int m = (l0 + h0) >> 1;
+              if (cstart[m] <= pb) l0 = m;
+              else h0 = m;
+            }
+            elo = __builtin_amdgcn_readfirstlane(l0);
+          }
+          // per step, up to 64*U products [x0, x0 + len): the 64 compacted entries after elo are
+          // loaded once (lane j: entry elo+1+j, start s_j relative to x0; starts are distinct since
+          // every compacted entry has a product) and scatter j+1 into the wave's byte map at their
+          // start, laid out [lane][u] so that lane l reads the U positions u*64+l as ONE 8-byte
+          // word; per batch u a DPP max-scan plus the carry from batch u-1 then counts the entries
+          // starting at or before the lane's product. The step ends where the 64th entry starts
+          // (entries past it are not loaded), at least 63 products on.
+          uint8_t* ownb = reinterpret_cast<uint8_t*>(own);
+          for (int x0 = pb; x0 < pe;) {
+            const int ae = elo + 1 + lane;
+            const int s = ae <= nact ? cstart[ae] - x0 : (1 << 30);  // >= 1
+            const int s63 = __builtin_amdgcn_readlane(s, 63);
+            int len = pe - x0 < 64 * U ? pe - x0 : 64 * U;
+            if (s63 < len) len = s63;
+            *reinterpret_cast<uint64_t*>(ownb + 8 * lane) = 0ull;
+            wave_lds_sync();
+            if (s < len) ownb[8 * (s & 63) + (s >> 6)] = (uint8_t)(lane + 1);
+            wave_lds_sync();
+            const uint64_t ow = *reinterpret_cast<const uint64_t*>(ownb + 8 * lane);
+            wave_lds_sync();  // ownb is rewritten by the next step
+            int32_t r[U];
+            a_t va[U];
+            int ev[U];
+            int carry = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              r[u] = kNoRow;
+              if (u * 64 >= len) continue;  // wave-uniform
+              const int cnt0 = wave_incl_max((int)((ow >> (8 * u)) & 0xffu), 0);
+              const int cnt = cnt0 > carry ? cnt0 : carry;
+              carry = __builtin_amdgcn_readlane(cnt, 63);
+              const int x = u * 64 + lane;
+              if (x < len) {
+                const int e = elo + cnt;
+                ev[u] = e;
+                const int64_t q = cbase[e] + x0 + x;
+                r[u] = rowsA[q];
+                va[u] = valsA[q];
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              if (r[u] == kNoRow) continue;
+              const uint32_t d = (uint32_t)(r[u] - lo);
+              if (d >= tw) {
+                bad |= 1 << 8;
+                continue;
+              }
+              const uint32_t wv = dw[d >> 5];
+              if (!((wv >> (d & 31)) & 1u)) bad |= 1 << 11;  // a product row the symbolic pass did not mark
+              const int slot = dp[d >> 5] + __popc(wv & ((1u << (d & 31)) - 1u));
+              SR::lds_acc(&vals[slot], SR::multiply(va[u], cscale[ev[u]]));
+            }
+            elo += __popcll(__ballot(s <= len));
+            x0 += len;
+          }
+        }
+        __syncthreads();  // the compacted arrays are rewritten by the next chunk
+      }
+      prefetch_next();
+      // commit: values in row order (rank q = output out_pos + q), rows off the bitmap
+      if (out_pos + dtotal > out_end || out_pos + dtotal > a.ccap) {
+        bad |= 1 << 5;
+      } else {
+        for (int q = tid; q < dtotal; q += BS)
+          reinterpret_cast<val_t*>(a.Cnum)[out_pos + q] = SR::finalize(vals[q]);
+        for (int x = tid; x < cut; x += BS) {
+          uint32_t wv = dw[x];
+          int32_t* cr = a.Cir + out_pos + dp[x];
+          while (wv) {
+            *cr++ = lo + 32 * x + __builtin_ctz(wv);
+            wv &= wv - 1u;
+          }
+        }
+      }
+      out_pos += dtotal;
+      inited = true;
+    } else {
+      prefetch_next();
+    }
+    w0 += cut;
+    __syncthreads();
+  }
+  if (tid == 0 && out_pos != out_end) atomicAdd(&a.err[0], 1);
+  if (bad) guard_fail(a.err, 31 - __clz(bad), c, bad, tlo);
+}
+
+// Launches dense_kernel over order[first, first+count) (grid slices below 2^32 work-items).
+template <class SR, int BS, int EL, int U, int LDSB>
+hipError_t launch_dense(const TaskArgs& args, int64_t first, int64_t count, hipStream_t stream) {
+  if (count <= 0) return hipSuccess;
+  using C = DenseCfg<SR, BS, EL, U, LDSB>;
+  auto kern = dense_kernel<SR, BS, EL, U, LDSB>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)C::bytes);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int64_t kMaxGrid = ((1ll << 32) - 1) / BS;
+  for (int64_t off = 0; off < count; off += kMaxGrid) {
+    const int64_t n = count - off < kMaxGrid ? count - off : kMaxGrid;
+    TaskArgs b = args;
+    b.order = args.order + first + off;
+    b.norder = n;
+    hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(BS), C::bytes, stream, b);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace cbh

@@ -9,6 +9,8 @@
 #include <algorithm>
 
 #include "../../combblas_hip.h"
+#include "dense_kernel.h"
+#include "order_kernel.h"
 #include "task_kernel.h"
 #include "wave_kernel.h"
 
@@ -172,6 +174,7 @@ inline TaskArgs numeric_args(const cbh_numeric_plan& p, int64_t cbase, int32_t* 
   a.gnx0 = p.gnx0;
   a.gnx1 = p.gnx1;
   a.ghub = p.ghub;
+  a.gbase = p.gbase;
   a.boff = p.boff;
   a.bmp = p.bmp;
   return a;
@@ -187,6 +190,32 @@ constexpr bool dense_capable() {
 template <class SR>
 constexpr uint32_t plan_flags() {
   return dense_capable<SR>() ? 0u : CBH_PLAN_NO_DENSE;
+}
+
+// The dense (bitmap-rank) tasks: dense_kernel.h (round 5: one 1024-thread workgroup per CU with
+// the whole LDS, wave-independent products); CBH_DENSE_V2=0 builds the round-4 task_kernel form.
+#ifndef CBH_DENSE_V2
+#define CBH_DENSE_V2 1
+#endif
+#ifndef CBH_DENSE2_BS
+#define CBH_DENSE2_BS 1024
+#endif
+#ifndef CBH_DENSE2_U
+#define CBH_DENSE2_U 8
+#endif
+#ifndef CBH_DENSE2_LDS
+#define CBH_DENSE2_LDS 163776  // 160 KiB less the kernel's static LDS (s_cut)
+#endif
+struct TDense2 {
+  static constexpr int BS = CBH_DENSE2_BS, EL = CBH_DENSE2_BS, U = CBH_DENSE2_U, LDSB = CBH_DENSE2_LDS;
+};
+template <class SR>
+hipError_t launch_dense_numeric(const TaskArgs& a, int64_t first, int64_t count, hipStream_t s) {
+#if CBH_DENSE_V2
+  return launch_dense<SR, TDense2::BS, TDense2::EL, TDense2::U, TDense2::LDSB>(a, first, count, s);
+#else
+  return launch_tasks<SR, TNumLarge, MODE_TDENSE>(a, first, count, s);
+#endif
 }
 
 // Numeric tasks of the small bin: one per wave (wave_kernel.h); wide user value types keep the
@@ -208,7 +237,7 @@ hipError_t run_numeric_plan(const cbh_numeric_plan& p, int32_t* Cir, void* Cnum,
   hipStream_t s = reinterpret_cast<hipStream_t>(p.stream);
   hipError_t e = hipSuccess;
   if constexpr (dense_capable<SR>()) {
-    e = launch_tasks<SR, TNumLarge, MODE_TDENSE>(a, p.dense_first, p.dense_count, s);
+    e = launch_dense_numeric<SR>(a, p.dense_first, p.dense_count, s);
     if (e != hipSuccess) return e;
   } else if (p.dense_count > 0) {
     return hipErrorInvalidValue;  // planned without CBH_PLAN_NO_DENSE

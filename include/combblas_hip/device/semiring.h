@@ -150,13 +150,14 @@ struct PlusTimesPromoteD {
 // A user semiring with the reference's static-functor contract (Semirings.h:143-255; e.g.
 // ReleaseTests/KTipsTest.cpp:12-20, Applications/SegTestApp/SegTest.cpp:35-61) whose add and
 // multiply are callable on the device (__host__ __device__). Accumulated under the slot lock.
-template <class USR, class NT1, class NT2, class NTO>
+template <class USR, class NT1, class NT2, class NTO, bool ORD = false>
 struct UserSRD {
   using a_t = NT1;
   using b_t = NT2;
   using val_t = NTO;
   using acc_t = NTO;
   static constexpr bool kLocked = true;
+  static constexpr bool kOrdered = ORD;  // reference-order accumulation (order_kernel.h)
   static_assert(std::is_trivially_copyable<NTO>::value, "device values must be trivially copyable");
   static __device__ __forceinline__ NTO multiply(const NT1& a, const NT2& b) { return USR::multiply(a, b); }
   static __device__ __forceinline__ NTO add(const NTO& x, const NTO& y) { return USR::add(x, y); }

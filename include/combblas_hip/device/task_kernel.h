@@ -121,6 +121,8 @@ struct TaskArgs {
   int32_t* gnx0;
   int32_t* gnx1;
   int32_t* ghub;  // hub id of each chunked entry's A column (-1: none), written at its first visit
+  int64_t* gbase;  // start of each chunked hub entry's A column, written at its first visit: the
+                   // stop search reads it from here (coalesced) instead of the hub table's row
   // stored row bitmaps of the dense candidates (bmp_count_kernel): task t owns words
   // [boff[t], boff[t+1]) of bmp, bit x of word w = row tlo[t] + 32 w + x. The large symbolic kernel
   // writes them while it counts; the dense numeric kernel reads them instead of a marking pass.
@@ -165,11 +167,20 @@ __device__ __forceinline__ int64_t gallop64(const int32_t* __restrict__ rows, in
 // of a galloping search of ~2 log2(segment) dependent loads; short columns gallop. Also returns
 // the row at the stop (kNoRow past hi), the next sub-tile's cursor row. Sub-tiles and dense
 // windows end on row-block boundaries where they can (kAlignSubtiles), and there a hub's stop is
-// the table entry itself: one load instead of the preload, the table and a bisection.
+// the table entry itself: one load instead of the preload, the table and a bisection. The column
+// start (`base`) comes from the entry state, not from the hub table's row (round 5: one random
+// 128-B line less per active hub visit, A^2 153.3 -> 155.5 GFLOP/s). Round 5 also tried the
+// preload FIRST at aligned stops (CBH_STOP_TABLE_FIRST=0: its rows are the line the gather reads
+// anyway, and half the dense kernel's active segments end inside it): 147.3 GFLOP/s, dense 275 ->
+// 299 ms -- the extra dependent round trip of the long segments costs more than the table lines.
+#ifndef CBH_STOP_TABLE_FIRST
+#define CBH_STOP_TABLE_FIRST 1
+#endif
 template <int W>
 __device__ __forceinline__ int64_t stop_search(const int32_t* __restrict__ rows, int64_t lo, int64_t hi, int32_t key,
                                                const int2* __restrict__ blk, int64_t base, int32_t RB,
                                                int32_t& row_at) {
+#if CBH_STOP_TABLE_FIRST
   if (blk != nullptr && key % RB == 0) {  // a row-block boundary (aligned sub-tiles): one table load
     const int2 e = blk[key / RB];
     const int64_t s0 = base + e.x;
@@ -177,6 +188,7 @@ __device__ __forceinline__ int64_t stop_search(const int32_t* __restrict__ rows,
     row_at = stop >= hi ? kNoRow : (stop == s0 ? e.y : rows[stop]);
     return stop;
   }
+#endif
   int32_t v[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) v[w] = (lo + w < hi) ? rows[lo + w] : kNoRow;
@@ -193,6 +205,13 @@ __device__ __forceinline__ int64_t stop_search(const int32_t* __restrict__ rows,
   }
   lo += W;
   int64_t stop;
+  if (blk != nullptr && key % RB == 0) {  // a row-block boundary (aligned sub-tiles): one table load
+    const int2 e = blk[key / RB];
+    const int64_t s0 = base + e.x;
+    stop = s0 < lo ? lo : (s0 > hi ? hi : s0);
+    row_at = stop >= hi ? kNoRow : (stop == s0 ? e.y : rows[stop]);
+    return stop;
+  }
   if (blk != nullptr) {
     const int32_t b = key / RB;
     const int64_t s0 = base + blk[b].x, s1 = base + blk[b + 1].x;
@@ -408,6 +427,9 @@ struct TaskCfg {
   static constexpr size_t o_dbits = al(o_dvals + sizeof(acc_t) * CAPD);
   static constexpr int NWB = NUM ? (int)((o_pos - o_dbits) / 6) / 8 * 8 : 0;
   static_assert(!DENSE || o_dbits + 6 * NWB <= o_pos, "dense bitmap and prefix fit the tables");
+  // o_end: two int32 arrays, the entry's remaining length in the task (end - cursor) and the cursor's
+  // offset in its A column (cursor - column start, so the stop search needs no hub-table load for
+  // the start); columns have < 2^31 rows
   static constexpr size_t o_end = al(o_pos + sizeof(int64_t) * EMAX);
   static constexpr size_t o_scale = al(o_end + sizeof(int64_t) * EMAX);
   static constexpr size_t o_next = al(o_scale + (NUM ? sizeof(b_t) * EMAX : 0));
@@ -453,7 +475,8 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
   // epos: cursor (absolute index into A); between the segment scan and the end of the sub-tile
   // it holds cursor - exclusive offset (the gather base of the entry's products)
   int64_t* epos = reinterpret_cast<int64_t*>(smem + C::o_pos);
-  int64_t* eend = reinterpret_cast<int64_t*>(smem + C::o_end);    // end of the A column in the task
+  int32_t* erem = reinterpret_cast<int32_t*>(smem + C::o_end);    // end of the A column in the task - cursor
+  int32_t* ecoff = erem + EMAX;                                    // cursor - start of the A column
   b_t* escale = reinterpret_cast<b_t*>(smem + C::o_scale);        // B value
   int32_t* enext = reinterpret_cast<int32_t*>(smem + C::o_next);  // row at the cursor (kNoRow: done)
   int32_t* enext2 = reinterpret_cast<int32_t*>(smem + C::o_next2);  // row at the sub-tile's stop
@@ -538,13 +561,10 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
   // violated bounds guards are recorded in a register and reported once at the end: a guard_fail
   // (global atomics with return values) inside a hot loop makes the compiler drain vmcnt there
   int bad = 0;  // bit k: guard site k violated
-  // hub h's block pairs and its column start (TaskArgs::htab); entries keep h in ecol, so a
-  // sub-tile's stop search loads the pair and the start side by side
+  // hub h's block pairs (TaskArgs::htab); entries keep h in ecol and their column start as the
+  // cursor's column offset (ecoff), so a sub-tile's stop search loads only the pair it needs
   auto hub_tab = [&](int32_t h) -> const int2* {
     return reinterpret_cast<const int2*>(a.htab) + (int64_t)h * (a.nblk + 2) + 1;
-  };
-  auto hub_base = [&](int32_t h) -> int64_t {
-    return reinterpret_cast<const int64_t*>(a.htab)[(int64_t)h * (a.nblk + 2)];
   };
   // entry state of entries [first, first+cnt): cursor at the first row >= lo
   const int64_t go = chunked ? a.goff[task] : 0;
@@ -562,7 +582,8 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
         int64_t pos = base;
         if (!lo_is_start && base < cend) pos = lb_rows64(rowsA, base, cend, lo);
         epos[i] = pos;
-        eend[i] = cend;
+        erem[i] = (int32_t)(cend - pos);
+        ecoff[i] = 0;
         enext[i] = pos < cend ? rowsA[pos] : kNoRow;
       }
       return;
@@ -574,11 +595,13 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
         const int64_t g = go + first + i;
         const int32_t nx = (par ? a.gnx1 : a.gnx0)[g];
         const int32_t h = a.ghub[g];
-        epos[i] = (par ? a.gcur1 : a.gcur0)[g];
+        const int64_t cur = (par ? a.gcur1 : a.gcur0)[g];
+        epos[i] = cur;
         enext[i] = nx;
         ecol[i] = h;
         if (nx >= hi) continue;  // idle in this sub-tile: segments() reads only the cursor and its row
-        eend[i] = a.gend[g];
+        erem[i] = (int32_t)(a.gend[g] - cur);
+        ecoff[i] = h >= 0 ? (int32_t)(cur - a.gbase[g]) : 0;
         if constexpr (NUM) escale[i] = reinterpret_cast<const b_t*>(a.Bnum)[p];
         continue;
       }
@@ -587,7 +610,8 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
       if (k < 0 || k >= a.ncolA) {
         bad |= 1 << 1;
         ecol[i] = -1;
-        epos[i] = eend[i] = 0;
+        epos[i] = 0;
+        erem[i] = ecoff[i] = 0;
         enext[i] = kNoRow;
         if (chunked) {
           a.gend[go + first + i] = 0;
@@ -626,11 +650,13 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
         if (pos > cend) pos = cend;
       }
       epos[i] = pos;
-      eend[i] = cend;
+      erem[i] = (int32_t)(cend - pos);
+      ecoff[i] = (int32_t)(pos - base);
       const int32_t nx = pos < cend ? known : kNoRow;
       enext[i] = nx;
       if (chunked) {  // the first sub-tile's cursors are committed state too
         a.gend[go + first + i] = cend;
+        a.gbase[go + first + i] = base;
         (par ? a.gcur1 : a.gcur0)[go + first + i] = pos;
         (par ? a.gnx1 : a.gnx0)[go + first + i] = nx;
         a.ghub[go + first + i] = h;
@@ -653,14 +679,14 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
 #ifdef CBH_STAMPS
         dg_active++;
 #endif
-        const int64_t end = eend[i];
+        const int64_t end = p + erem[i];
         if (hi_is_end) {
           stop = end;
           nx2 = kNoRow;
         } else {
           const int32_t h = MERGE ? -1 : ecol[i];
           const int2* blk = h >= 0 ? hub_tab(h) : nullptr;
-          stop = stop_search<8>(rowsA, nx == kUnknownRow ? p : p + 1, end, hi, blk, h >= 0 ? hub_base(h) : 0, a.RB, nx2);
+          stop = stop_search<8>(rowsA, nx == kUnknownRow ? p : p + 1, end, hi, blk, p - ecoff[i], a.RB, nx2);
         }
       }
       eoff[i] = (int32_t)(stop - p);
@@ -881,7 +907,10 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
           inited = true;
         } else {
           for (int i = tid; i < (int)ne; i += BS) {
+            const int sg = eoff[i + 1] - eoff[i];
             epos[i] += eoff[i + 1];
+            erem[i] -= sg;
+            ecoff[i] += sg;
             enext[i] = enext2[i];
           }
         }
@@ -1057,7 +1086,10 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
     par ^= chunked ? 1 : 0;  // the cursors written during this sub-tile are now the committed ones
     if (!chunked)  // advance the cursors past the committed sub-tile
       for (int i = tid; i < (int)ne; i += BS) {
+        const int sg = eoff[i + 1] - eoff[i];
         epos[i] += eoff[i + 1];
+        erem[i] -= sg;
+        ecoff[i] += sg;
         enext[i] = enext2[i];
       }
     CBH_STAMP(9);

@@ -183,17 +183,32 @@ def _free_port():
     return p
 
 
+def _trace(rank, msg):
+    """CBH_TRACE_DIR: each rank appends its progress (flushed) to rank<r>.log there"""
+    d = os.environ.get("CBH_TRACE_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"rank{rank}.log"), "a") as f:
+            f.write(f"{time.time():.3f} {msg}\n")
+
+
 def _worker(rank, world, port, fn, args, outdir, coll_timeout=200):
     import pickle
 
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    # gloo's default device resolves the host name, a DNS query that can block for the resolver's
+    # timeouts on a box without name service; on the loopback interface it needs no lookup
+    if "GLOO_SOCKET_IFNAME" not in os.environ and os.path.exists("/sys/class/net/lo"):
+        os.environ["GLOO_SOCKET_IFNAME"] = "lo"
+    _trace(rank, "spawned")
     res = None
     try:
         # a collective times out (and the rank reports where) before the world's deadline, instead
         # of waiting gloo's default 30 minutes
         dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=coll_timeout))
+        _trace(rank, "process group")
         res = ("ok", fn(rank, world, *args))
         dist.barrier()
         dist.destroy_process_group()

@@ -14,6 +14,8 @@
 //     MinMaxSR    -- test-defined semiring over a two-field struct, int64 inputs (NT != NTO, as
 //                    SegTest.cpp:165-171's KmerIntersect<int64_t, CommonKmers>)
 //     PlusTimesSRing<double,int64_t> -- promotion NT1 != NT2 -> T_promote = double
+//     Select2ndSRing<int64,int64,int64> -- non-commutative add (reference order, order_kernel.h)
+//     PTOrdDev    -- f64 PlusTimes marked reference_order: non-dyadic sums bit-exact
 //   dropin_harness <scale>      -> prints "DROPIN <case> OK nnz=..." lines, exit 0 on success
 #include <mpi.h>
 
@@ -70,6 +72,9 @@ COMBBLAS_HIP_INSTANTIATE(SMLL, int64_t, int64_t)
 COMBBLAS_HIP_INSTANTIATE_DEVICE(KTipsDev, int64_t, bool, bool, bool)
 COMBBLAS_HIP_INSTANTIATE_DEVICE(MinMaxDev, int64_t, int64_t, int64_t, MinMax)
 COMBBLAS_HIP_INSTANTIATE_DEVICE(PTDI, int64_t, double, int64_t, double)
+typedef Select2ndSRing<int64_t, int64_t, int64_t> S2LL;
+COMBBLAS_HIP_INSTANTIATE_DEVICE(S2LL, int64_t, int64_t, int64_t, int64_t)
+COMBBLAS_HIP_INSTANTIATE_DEVICE(PTOrdDev, int64_t, double, double, double)
 
 template <class NT>
 static bool same(const SpDCCols<int64_t, NT>& x, const SpDCCols<int64_t, NT>& y) {
@@ -86,8 +91,8 @@ static bool same(const SpDCCols<int64_t, NT>& x, const SpDCCols<int64_t, NT>& y)
 }
 
 // value = f(row, col, value) on the local block (1 rank: local ids are global), as TC.cpp:72-87 edits L
-template <class F>
-static void set_values(SpParMat<int64_t, int64_t, SpDCCols<int64_t, int64_t>>& M, F f) {
+template <class NT, class F>
+static void set_values(SpParMat<int64_t, NT, SpDCCols<int64_t, NT>>& M, F f) {
   for (auto colit = M.seq().begcol(); colit != M.seq().endcol(); ++colit)
     for (auto nzit = M.seq().begnz(colit); nzit != M.seq().endnz(colit); ++nzit)
       nzit.value() = f(nzit.rowid(), colit.colid(), nzit.value());
@@ -202,6 +207,14 @@ int main(int argc, char** argv) {
     set_values(Bv, [](int64_t r, int64_t c, int64_t x) { return x * ((r * 104729 + c * 17) % 19 - 9); });
     bad += run_case<MinMax, MinMaxDev, MinMaxCpu>("PSpGEMM<user struct MinMax, int64 -> struct>", Av, Bv);
     bad += run_case<double, PTDI, CpuPlusTimesDI>("PSpGEMM<PlusTimes<double,int64> promotion>", Ad, Bi);
+    // non-commutative add: Select2nd keeps the first product of the hash branch, the last popped of
+    // the heap branch (mtSpGEMM.h:341, :408)
+    bad += run_case<int64_t, S2LL, Select2ndCpu>("PSpGEMM<Select2nd<int64> reference order>", Av, Bv);
+    // non-dyadic f64 sums in the reference's order
+    SpParMat<int64_t, double, SpDCCols<int64_t, double>> Af(G), Bf(G);
+    set_values(Af, [](int64_t r, int64_t c, double x) { return x * (0.1 + 1e-3 * ((r * 7919 + c * 31) % 97)); });
+    set_values(Bf, [](int64_t r, int64_t c, double x) { return x * (0.3 - 1e-3 * ((r * 104729 + c * 17) % 89)); });
+    bad += run_case<double, PTOrdDev, PTOrdCpu>("PSpGEMM<PlusTimes<double> reference order, non-dyadic>", Af, Bf);
   }
   MPI_Finalize();
   return bad ? 1 : 0;

@@ -52,6 +52,39 @@ struct MinMaxDev {
     return r;
   }
 };
+// f64 PlusTimes computed in the REFERENCE'S accumulation order on the device (reference_order,
+// HipSpGEMMDevice.h -> device/order_kernel.h): with non-dyadic values the sums must still equal the
+// stock path's bit for bit
+struct PTOrdDev {
+  static double id() { return 0.0; }
+  static bool returnedSAID() { return false; }
+  static MPI_Op mpi_op() { return MPI_SUM; }
+  CBH_HD static double add(const double& a, const double& b) { return a + b; }
+  CBH_HD static double multiply(const double& a, const double& b) { return a * b; }
+  static void axpy(double a, const double& x, double& y) { y += a * x; }
+};
+struct PTOrdCpu {
+  static double id() { return 0.0; }
+  static bool returnedSAID() { return false; }
+  static MPI_Op mpi_op() { return MPI_SUM; }
+  static double add(const double& a, const double& b) { return a + b; }
+  static double multiply(const double& a, const double& b) { return a * b; }
+  static void axpy(double a, const double& x, double& y) { y += a * x; }
+};
+// Select2ndSRing<int64,int64,int64> (Semirings.h:143-163) on the stock path: add(x, y) = y
+struct Select2ndCpu {
+  static int64_t id() { return 0; }
+  static bool returnedSAID() { return false; }
+  static MPI_Op mpi_op() { return MPI_MAX; }
+  static int64_t add(const int64_t&, const int64_t& b) { return b; }
+  static int64_t multiply(const int64_t&, const int64_t& b) { return b; }
+  static void axpy(int64_t a, const int64_t& x, int64_t& y) { y = multiply(a, x); }
+};
+namespace combblas_hip {
+template <>
+struct reference_order<PTOrdDev> : std::true_type {};
+}  // namespace combblas_hip
+
 struct MinMaxCpu {
   static MinMax id() { return MinMax(); }
   static bool returnedSAID() { return false; }

@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 HARNESS = os.path.join(H.REPO, "oracle", "_ref", "dropin_harness")
 
 
-@pytest.mark.parametrize("scale", [8, 12])
+@pytest.mark.parametrize("scale", [8, 12, 16])  # 16: config C1 (MultTest plumbing, R-MAT scale 16)
 def test_reference_driver_uses_hip_kernels(scale):
     assert os.path.exists(HARNESS), "oracle/_ref/dropin_harness missing: run __graft_entry__.build() with the reference"
     env = dict(os.environ, LD_LIBRARY_PATH="/usr/lib/x86_64-linux-gnu:/opt/conda/lib", OMP_NUM_THREADS="8")
@@ -21,4 +21,5 @@ def test_reference_driver_uses_hip_kernels(scale):
     out = r.stdout + r.stderr
     assert r.returncode == 0, out
     lines = [l for l in out.splitlines() if l.startswith("DROPIN")]
-    assert len(lines) == 5 and all(" OK " in l for l in lines), out
+    # 5 arrival-order cases + Select2nd (non-commutative add) and non-dyadic f64 in reference order
+    assert len(lines) == 7 and all(" OK " in l for l in lines), out

@@ -130,3 +130,25 @@ def test_c4_tc_scale22_dot_vs_expand(ctx):
     assert checked == 200 and bad == 0
     for X in (Cd, L, L2):
         X.free()
+
+
+def test_c4_tc_scale24_dot(ctx):
+    """C4 at its configured size (R-MAT scale 24): the dot form's triangle count and whole-result
+    digest against the recorded values (tests/golden/fullsize.json "tc24": a regression pin -- the
+    reference cannot run this size) and 200 mask columns recomputed on the host (parity)."""
+    from combblas_amd.apps import MaskedSpGEMM, TCLower
+    from combblas_amd.semirings import PlusTimesSRing
+
+    sys.path.insert(0, H.REPO)
+    from bench_tc import host_check
+
+    g = json.load(open(os.path.join(H.REPO, "tests", "golden", "fullsize.json")))["tc24"]
+    L, L2 = TCLower(ctx, 24, 16), TCLower(ctx, 24, 16)
+    Cd = MaskedSpGEMM(PlusTimesSRing, L, L2, L, method="dot")
+    tri = int(Cd.tensors()[3].sum().item())
+    _, dg = Cd.checksum()
+    assert (Cd.nnz, tri, str(dg)) == (g["nnzC"], g["triangles"], g["digest"])
+    checked, bad = host_check(L, Cd, 200)
+    assert checked == 200 and bad == 0
+    for X in (Cd, L, L2):
+        X.free()
