@@ -39,7 +39,7 @@ class cbh_kernel_stat(ctypes.Structure):
 
 K_SYM_LARGE, K_SYM_SMALL, K_NUM_LARGE, K_NUM_SMALL, K_MERGE_SYM, K_MERGE_NUM = range(6)
 K_NAMES = ["sym_large", "sym_small", "num_large", "num_small", "merge_sym", "merge_num", "num_dense", "sym_mid",
-           "num_mid"]
+           "num_mid", "sym_bmp"]
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
 FREE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p)

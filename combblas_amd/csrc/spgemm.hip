@@ -880,6 +880,27 @@ __global__ void dense_split_kernel(const int64_t* __restrict__ tcnt, const int32
   wd[t] = d ? w : 0;
   wh[t] = d ? 0 : (w > 0 && w <= smallcap && flops && flops[t] > wavemax ? smallcap + 1 : w);
 }
+// symbolic tasks split between the one-workgroup-per-CU bitmap kernel (dense_kernel.h, SYM) and
+// the task kernels: wb / wh = the task's flops in the kernel it goes to, 0 in the other. A large
+// task (flops > midcap) runs the bitmap kernel when it stores its bitmap (a dense candidate) or when
+// its row bitmap needs no more sub-tiles (of nws_rows rows) than the task kernel's key hash (of
+// hashcap keys) would; the small and mid tasks keep their kernels.
+__global__ void sym_split_kernel(const int64_t* __restrict__ twork, const int32_t* __restrict__ tlo,
+                                 const int32_t* __restrict__ thi, const int64_t* __restrict__ boff, int64_t n,
+                                 int64_t midcap, int64_t hashcap, int64_t nws_rows, int64_t* __restrict__ wb,
+                                 int64_t* __restrict__ wh) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int64_t w = twork[t], span = (int64_t)thi[t] - tlo[t];
+  bool b = false;
+  if (w > midcap && span > 0) {
+    const bool store = boff != nullptr && boff[t + 1] > boff[t];
+    b = store || (span + nws_rows - 1) / nws_rows <= (w + hashcap - 1) / hashcap;
+  }
+  wb[t] = b ? w : 0;
+  wh[t] = b ? 0 : w;
+}
+
 // share of the free HBM the phase workspace of cbh_spgemm_phased takes (CBH_PHASE_FRAC)
 static double phase_frac() {
   static double v = [] {
@@ -1178,8 +1199,26 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
     }
   }
   CBH_HIP(ctx, hipMemsetAsync(P.tcnt, 0, sizeof(int64_t) * (nt + 1), ctx->stream));
-  BinLists bl;
+  BinLists bl, bb;
+#if CBH_SYM_V2
+  {  // the large bitmap tasks to the one-workgroup-per-CU kernel, the rest to the task kernels
+    using CS = DenseCfg<PlusTimesD<int64_t>, TSym2::BS, TSym2::EL, TSym2::U, TSym2::LDSB, true>;
+    constexpr int64_t kHashKeys = (int64_t)kSymWords * kSymFill8 / 8;  // TSymLarge's key-hash capacity
+    int64_t *wb, *wh;
+    CBH_TRY(S.get(&wb, nt));
+    CBH_TRY(S.get(&wh, nt));
+    hipLaunchKernelGGL(sym_split_kernel, dim3(blocks_for(P.ntasks, 256)), dim3(256), 0, ctx->stream, P.twork, P.tlo,
+                       P.thi, P.bmp ? P.boff : nullptr, P.ntasks, (int64_t)kSymMidCap, kHashKeys, 32ll * CS::NWS, wb,
+                       wh);
+    CBH_HIP(ctx, hipGetLastError());
+    CBH_TRY(make_bins(ctx, S, wh, P.ntasks, 0, P.order, &bl, BinCaps{kSymWaveCap, kSymMidCap}, P.tunits, P.trk));
+    const int64_t nh = bl.small_count + bl.mid_count + bl.large_count;
+    CBH_TRY(make_bins(ctx, S, wb, P.ntasks, 0, P.order + nh, &bb, BinCaps{kSymWaveCap, kSymMidCap}, P.tunits, P.trk));
+    bb.large_first += nh;  // (wb holds large tasks only)
+  }
+#else
   CBH_TRY(make_bins(ctx, S, P.twork, P.ntasks, 0, P.order, &bl, BinCaps{kSymWaveCap, kSymMidCap}, P.tunits, P.trk));
+#endif
   TaskArgs a = task_args(A, B, P, ctx);
   a.twork = P.twork;
   a.cnt = P.tcnt;
@@ -1188,6 +1227,12 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   const double sb_l = 4.0 * bl.units[2] + 16.0 * bl.large_count;
   const double sb_s = 4.0 * bl.units[0] + 16.0 * bl.small_count;
   const double sb_m = 4.0 * bl.units[1] + 16.0 * bl.mid_count;
+  const double sb_b = 4.0 * bb.units[2] + 16.0 * bb.large_count;
+  if (bb.large_count > 0)
+    CBH_TRY(timed_launch(ctx, CBH_K_SYM_BMP, sb_b, [&] {
+      return launch_dense<Dummy, TSym2::BS, TSym2::EL, TSym2::U, TSym2::LDSB, true>(a, bb.large_first, bb.large_count,
+                                                                                    ctx->stream);
+    }));
   if (diag_enabled()) CBH_TRY((launch_task_diag<Dummy, TSymLarge, MODE_TSYM>(ctx, a, bl, "symbolic")));
   else CBH_TRY((launch_task<Dummy, TSymLarge, MODE_TSYM>(ctx, a, bl.large_first, bl.large_count, CBH_K_SYM_LARGE, sb_l)));
   CBH_TRY((launch_task<Dummy, TSymMid, MODE_TSYM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_SYM_MID, sb_m)));

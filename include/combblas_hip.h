@@ -215,10 +215,11 @@ int cbh_ctx_enable_timing(cbh_ctx* ctx, int enable);
 #define CBH_K_NUM_SMALL 3 /* task_kernel<SR,512,128,256,4,MODE_TNUM>     numeric, <= 256 outputs */
 #define CBH_K_MERGE_SYM 4
 #define CBH_K_MERGE_NUM 5
-#define CBH_K_NUM_DENSE 6 /* task_kernel<SR,4096,512,512,8,MODE_TDENSE>  numeric bitmap-rank    */
+#define CBH_K_NUM_DENSE 6 /* dense_kernel<SR,1024,1024,8,163776,false>  numeric bitmap-rank    */
 #define CBH_K_SYM_MID 7   /* task_kernel<...,4096,256,256,4,MODE_TSYM>   symbolic, 256 < work <= 2048 */
 #define CBH_K_NUM_MID 8   /* task_kernel<SR,2048,256,256,4,MODE_TNUM>    numeric, 256 < outputs <= 1024 */
-#define CBH_K_NKINDS 9
+#define CBH_K_SYM_BMP 9   /* dense_kernel<...,1024,1024,8,163776,true>  symbolic bitmap tasks (one WG per CU) */
+#define CBH_K_NKINDS 10
 typedef struct cbh_kernel_stat {
   double ms;
   int64_t launches;

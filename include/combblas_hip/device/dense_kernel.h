@@ -43,14 +43,15 @@ namespace cbh {
 #define CBH_DENSE2_PREFETCH 8
 #endif
 
-template <class SR, int BS, int EL, int U, int LDSB>
+template <class SR, int BS, int EL, int U, int LDSB, bool SYM = false>
 struct DenseCfg {
   using acc_t = typename SR::acc_t;
   using b_t = typename sr_b_type<SR>::type;
+  static constexpr bool NUM = !SYM;
   static constexpr int NW = BS / 64;
   static constexpr size_t al(size_t x) { return (x + 15) & ~size_t(15); }
   // entry state (LDS-resident tasks): cursor, row at the cursor, end - cursor, cursor - column
-  // start, hub id, B value
+  // start, hub id, B value (numeric only)
   static constexpr size_t o_cur = 0;
   static constexpr size_t o_nx = al(o_cur + sizeof(int64_t) * EL);
   static constexpr size_t o_rem = al(o_nx + sizeof(int32_t) * EL);
@@ -58,18 +59,19 @@ struct DenseCfg {
   static constexpr size_t o_hub = al(o_coff + sizeof(int32_t) * EL);
   static constexpr size_t o_scale = al(o_hub + sizeof(int32_t) * EL);
   // compacted active entries of the current chunk: start offset (+ the total at [nact]), gather
-  // base (cursor - start offset), B value
-  static constexpr size_t o_cstart = al(o_scale + sizeof(b_t) * EL);
+  // base (cursor - start offset), B value (numeric only)
+  static constexpr size_t o_cstart = al(o_scale + (NUM ? sizeof(b_t) * EL : 0));
   static constexpr size_t o_cbase = al(o_cstart + sizeof(int32_t) * (EL + 1));
   static constexpr size_t o_cscale = al(o_cbase + sizeof(int64_t) * EL);
-  static constexpr size_t o_own = al(o_cscale + sizeof(b_t) * EL);  // NW x 512-byte owner maps
+  static constexpr size_t o_own = al(o_cscale + (NUM ? sizeof(b_t) * EL : 0));  // NW x 512-byte owner maps
   static constexpr size_t o_red = al(o_own + 512 * NW);
   static constexpr size_t o_win = al(o_red + sizeof(int32_t) * (4 * NW + 8));
-  // the window: values from the bottom, the window's words and int16 prefixes (6 B per word) from
-  // the top (as task_kernel's dense windows)
+  // numeric: the window -- values from the bottom, the window's words and int16 prefixes (6 B per
+  // word) from the top (as task_kernel's dense windows); symbolic: the sub-tile's row bitmap
   static constexpr size_t TB = (LDSB - o_win) & ~size_t(15);
   static constexpr size_t bytes = o_win + TB;
   static constexpr int NWB = (int)((TB - 64) / 6) / 8 * 8;  // widest window (all words, no values)
+  static constexpr int NWS = (int)(TB / 4) / 64 * 64;      // symbolic bitmap words (32 rows each)
   static_assert(NWB <= 32767, "int16 window prefixes");
   static_assert(bytes <= 163840, "one workgroup's LDS");
   static_assert(EL == BS, "one entry per thread per chunk");
@@ -103,14 +105,19 @@ __device__ __forceinline__ void block_excl_sum2(int& a, int& b, int* red, int& t
   tb = xb;
 }
 
-template <class SR, int BS, int EL, int U, int LDSB>
+// SYM = false: the numeric dense tasks (windows of the stored bitmap, values by rank);
+// SYM = true: the symbolic pass's bitmap tasks (sub-tiles of NWS words, rows marked with atomicOr,
+// distinct rows counted and, for a dense candidate, its bitmap stored) -- estimateNNZ_Hash
+// (mtSpGEMM.h:806-933) for the tasks whose row bitmap is cheaper than a key hash.
+template <class SR, int BS, int EL, int U, int LDSB, bool SYM = false>
 __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves per CU
-  using C = DenseCfg<SR, BS, EL, U, LDSB>;
+  using C = DenseCfg<SR, BS, EL, U, LDSB, SYM>;
   using val_t = typename SR::val_t;
   using acc_t = typename SR::acc_t;
   using a_t = typename sr_a_type<SR>::type;
   using b_t = typename C::b_t;
   constexpr int NW = C::NW;
+  constexpr bool NUM = C::NUM;
   static_assert(!sr_locked<SR>::value, "the dense kernel accumulates with SR::lds_acc");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -129,7 +136,7 @@ __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves
   __shared__ int32_t s_cut;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  int32_t* own = reinterpret_cast<int32_t*>(smem + C::o_own + 512 * wid);
+  uint8_t* ownb = smem + C::o_own + 512 * wid;
   const int32_t* __restrict__ rowsA = a.Air;
   const a_t* __restrict__ valsA = reinterpret_cast<const a_t*>(a.Anum);
   if ((int64_t)blockIdx.x >= a.norder) return;
@@ -144,7 +151,10 @@ __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves
   const int64_t work = a.twork[task];
   const int32_t tlo = a.tlo[task], thi = a.thi[task];
   const uint8_t full = a.tfull[task];
-  if (work <= 0 || thi <= tlo) return;
+  if (work <= 0 || thi <= tlo) {
+    if (!NUM && tid == 0) a.cnt[task] = 0;
+    return;
+  }
   const int64_t span = (int64_t)thi - tlo;
   const bool chunked = ne > EL;
   const int nchunks = (int)((ne + EL - 1) / EL);
@@ -165,7 +175,7 @@ __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves
     Ent e;
     const int64_t p = e0 + i;
     const int32_t k = a.Bir[p];
-    e.scale = reinterpret_cast<const b_t*>(a.Bnum)[p];
+    if constexpr (NUM) e.scale = reinterpret_cast<const b_t*>(a.Bnum)[p];
     e.cur = 0;
     e.nx = kNoRow;
     e.rem = e.coff = 0;
@@ -218,267 +228,323 @@ __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves
       srem[tid] = e.rem;
       scoff[tid] = e.coff;
       shub[tid] = e.hub;
-      sscale[tid] = e.scale;
+      if constexpr (NUM) sscale[tid] = e.scale;
     }
   }
+  bool inited = !chunked;  // chunked: the HBM entry state is written by the first processed range
 
-  int64_t out_pos = a.toff[task] - a.cbase;
-  const int64_t out_end = a.toff[task + 1] - a.cbase;
-  const int64_t bw0 = a.boff[task];
-  const int64_t nwt = a.boff[task + 1] - bw0;
-  if (a.bmp == nullptr || nwt != (span + 31) / 32) {
-    if (tid == 0) guard_fail(a.err, 10, c, task, nwt, span);
-    return;
-  }
-  const uint32_t* __restrict__ tb = a.bmp + bw0;
-  constexpr int64_t TB = (int64_t)C::TB;
-  int64_t wdes = TB * nwt / ((int64_t)sizeof(acc_t) * work + 6 * nwt);  // words whose outputs fill the rest
-  wdes = wdes < 64 ? 64 : (wdes > C::NWB ? C::NWB : wdes);
-  const bool dalign = kAlignSubtiles && a.RB > 0 && (a.RB & 31) == 0 && (tlo & 31) == 0;
-  const int64_t dbw = dalign ? a.RB / 32 : 1;  // words per row block
-  bool inited = !chunked;
-  constexpr int KW0 = (C::NWB + BS - 1) / BS;
-  constexpr int KW = KW0 < CBH_DENSE2_PREFETCH ? KW0 : CBH_DENSE2_PREFETCH;
-  uint32_t pre[KW > 0 ? KW : 1];
-  int64_t pre_w0 = -1;
-  int64_t w0 = 0;
-  __syncthreads();
-  while (w0 < nwt) {
-    const int wl = (int)((nwt - w0) < wdes ? (nwt - w0) : wdes);
-    const int dbase = (int)((TB - 6 * wl) & ~int64_t(15));
-    uint32_t* dw = reinterpret_cast<uint32_t*>(win + dbase);
-    int16_t* dp = reinterpret_cast<int16_t*>(win + dbase + 4 * wl);
-    const int capv = dbase / (int)sizeof(acc_t);
-    const int kw = (wl + BS - 1) / BS;
-    {
-      int x = tid;
-      if (pre_w0 == w0) {
-#pragma unroll
-        for (int j = 0; j < KW; ++j)
-          if (tid + j * BS < wl) dw[tid + j * BS] = pre[j];
-        x += KW * BS;
-      }
-      for (; x < wl; x += BS) dw[x] = tb[w0 + x];
-    }
-    if (tid == 0) s_cut = wl;
-    __syncthreads();
-    int tsum = 0;
-    for (int k = 0; k < kw; ++k) {
-      const int x = tid * kw + k;
-      tsum += x < wl ? __popc(dw[x]) : 0;
-    }
-    int wtotal = 0;
-    int ex = block_excl_sum<BS>(tsum, red, wtotal);
-    for (int k = 0; k < kw; ++k) {
-      const int x = tid * kw + k;
-      if (x < wl) {
-        const int pc = __popc(dw[x]);
-        dp[x] = (int16_t)(ex < 32767 ? ex : 32767);
-        if (ex <= capv && ex + pc > capv) s_cut = x;
-        ex += pc;
-      }
-    }
-    __syncthreads();
-    int cut = __builtin_amdgcn_readfirstlane(s_cut);  // (block-uniform values kept in SGPRs)
-    if (dalign && tlo + 32 * (w0 + cut) < thi) {  // window ends snap down to absolute row blocks
-      const int64_t tw0 = tlo / 32;
-      const int64_t cb = (tw0 + w0 + cut) / dbw * dbw - tw0 - w0;
-      if (cb > 0 && cb * 4 >= 3ll * cut) cut = (int)cb;
-    }
-    const int dtotal = __builtin_amdgcn_readfirstlane(cut < wl ? (int)dp[cut] : wtotal);
-    // the next window's words, loaded before this window's commit (not before its products: KW
-    // registers live across the product phase spilled)
-    auto prefetch_next = [&]() {
-      const int64_t w0n = w0 + cut;
-      if (KW > 0 && w0n < nwt) {
-        const int wln = (int)((nwt - w0n) < wdes ? (nwt - w0n) : wdes);
-#pragma unroll
-        for (int j = 0; j < KW; ++j) pre[j] = (tid + j * BS < wln) ? tb[w0n + tid + j * BS] : 0u;
-        pre_w0 = w0n;
-      }
-    };
-    const int32_t lo = (int32_t)(tlo + 32 * w0);
-    const int64_t hcut = tlo + 32 * (w0 + cut);
-    const int32_t hi = (int32_t)(hcut < thi ? hcut : thi);
+  // Every product of the row range [lo, hi) (all chunks of the task's entries): phase 1 moves each
+  // entry's cursor past the range and compacts the active entries, phase 2 (wave-independent)
+  // gathers the products and calls place(row, A value, compacted entry) for each.
+  auto run_chunks = [&](int32_t lo, int32_t hi, auto&& place) {
     const bool hi_is_end = hi == thi;
-    const uint32_t tw = (uint32_t)(hi - lo);
-    if (dtotal > 0) {
-      for (int x = tid; x < dtotal; x += BS) vals[x] = SR::identity();
-      for (int ch = 0; ch < nchunks; ++ch) {
-        // ---- phase 1: this chunk's entries (thread per entry)
-        const int64_t i = (int64_t)ch * EL + tid;
-        int len = 0;
-        int64_t cur0 = 0;
-        b_t scale{};
-        if (i < ne) {
-          Ent e;
+    for (int ch = 0; ch < nchunks; ++ch) {
+      // ---- phase 1: this chunk's entries (thread per entry)
+      const int64_t i = (int64_t)ch * EL + tid;
+      int len = 0;
+      int64_t cur0 = 0;
+      b_t scale{};
+      if (i < ne) {
+        Ent e;
+        if (!chunked) {
+          e.cur = scur[tid];
+          e.nx = snx[tid];
+        } else if (!inited) {
+          e = first_visit(i, lo, lo == tlo && (full & 1));
+        } else {
+          e.cur = a.gcur0[go + i];
+          e.nx = a.gnx0[go + i];
+        }
+        cur0 = e.cur;
+        if (e.nx < hi) {
           if (!chunked) {
-            e.cur = scur[tid];
-            e.nx = snx[tid];
-          } else if (!inited) {
-            e = first_visit(i, lo, lo == tlo && (full & 1));
+            e.rem = srem[tid];
+            e.coff = scoff[tid];
+            e.hub = shub[tid];
+            if constexpr (NUM) e.scale = sscale[tid];
+          } else if (inited) {
+            e.hub = a.ghub[go + i];
+            e.rem = (int32_t)(a.gend[go + i] - e.cur);
+            e.coff = e.hub >= 0 ? (int32_t)(e.cur - a.gbase[go + i]) : 0;
+            if constexpr (NUM) e.scale = reinterpret_cast<const b_t*>(a.Bnum)[e0 + i];
+          }
+          int64_t stop;
+          int32_t nx2;
+          if (hi_is_end) {
+            stop = e.cur + e.rem;
+            nx2 = kNoRow;
           } else {
-            e.cur = a.gcur0[go + i];
-            e.nx = a.gnx0[go + i];
+            const int2* blk = e.hub >= 0 ? hub_tab(e.hub) : nullptr;
+            stop = stop_search<8>(rowsA, e.nx == kUnknownRow ? e.cur : e.cur + 1, e.cur + e.rem, hi, blk,
+                                  e.cur - e.coff, a.RB, nx2);
           }
-          cur0 = e.cur;
-          if (e.nx < hi) {
-            if (!chunked) {
-              e.rem = srem[tid];
-              e.coff = scoff[tid];
-              e.hub = shub[tid];
-              e.scale = sscale[tid];
-            } else if (inited) {
-              e.hub = a.ghub[go + i];
-              e.rem = (int32_t)(a.gend[go + i] - e.cur);
-              e.coff = e.hub >= 0 ? (int32_t)(e.cur - a.gbase[go + i]) : 0;
-              e.scale = reinterpret_cast<const b_t*>(a.Bnum)[e0 + i];
-            }
-            int64_t stop;
-            int32_t nx2;
-            if (hi_is_end) {
-              stop = e.cur + e.rem;
-              nx2 = kNoRow;
-            } else {
-              const int2* blk = e.hub >= 0 ? hub_tab(e.hub) : nullptr;
-              stop = stop_search<8>(rowsA, e.nx == kUnknownRow ? e.cur : e.cur + 1, e.cur + e.rem, hi, blk,
-                                    e.cur - e.coff, a.RB, nx2);
-            }
-            len = (int)(stop - e.cur);
-            scale = e.scale;
-            if (!chunked) {
-              scur[tid] = stop;
-              snx[tid] = nx2;
-              srem[tid] = e.rem - len;
-              scoff[tid] = e.coff + len;
-            } else {
-              a.gcur0[go + i] = stop;
-              a.gnx0[go + i] = nx2;
-            }
-          } else if (chunked && !inited) {  // an idle first visit: its state is committed as is
-            a.gcur0[go + i] = e.cur;
-            a.gnx0[go + i] = e.nx;
+          len = (int)(stop - e.cur);
+          if constexpr (NUM) scale = e.scale;
+          if (!chunked) {
+            scur[tid] = stop;
+            snx[tid] = nx2;
+            srem[tid] = e.rem - len;
+            scoff[tid] = e.coff + len;
+          } else {
+            a.gcur0[go + i] = stop;
+            a.gnx0[go + i] = nx2;
           }
-        }
-        int off = len, aidx = len > 0 ? 1 : 0;
-        int P = 0, nact = 0;
-        block_excl_sum2<BS>(off, aidx, red, P, nact);
-        P = __builtin_amdgcn_readfirstlane(P);
-        nact = __builtin_amdgcn_readfirstlane(nact);
-        if (len > 0) {
-          cstart[aidx] = off;
-          cbase[aidx] = cur0 - off;
-          cscale[aidx] = scale;
-        }
-        if (tid == 0) cstart[nact] = P;
-        __syncthreads();
-        // ---- phase 2: wave w walks products [w*P/NW, (w+1)*P/NW) on its own
-        const int pb = (int)((int64_t)P * wid / NW), pe = (int)((int64_t)P * (wid + 1) / NW);
-        if (pb < pe) {
-          // the compacted entry owning product pb: the last one starting at or before it
-          int elo = 0;
-          {
-            int l0 = 0, h0 = nact;  // cstart[0] = 0 <= pb < P = cstart[nact]
-            while (h0 - l0 > 1) {
-              const int m = (l0 + h0) >> 1;
-              if (cstart[m] <= pb) l0 = m;
-              else h0 = m;
-            }
-            elo = __builtin_amdgcn_readfirstlane(l0);
-          }
-          // per step, up to 64*U products [x0, x0 + len): the 64 compacted entries after elo are
-          // loaded once (lane j: entry elo+1+j, start s_j relative to x0; starts are distinct since
-          // every compacted entry has a product) and scatter j+1 into the wave's byte map at their
-          // start, laid out [lane][u] so that lane l reads the U positions u*64+l as ONE 8-byte
-          // word; per batch u a DPP max-scan plus the carry from batch u-1 then counts the entries
-          // starting at or before the lane's product. The step ends where the 64th entry starts
-          // (entries past it are not loaded), at least 63 products on.
-          uint8_t* ownb = reinterpret_cast<uint8_t*>(own);
-          for (int x0 = pb; x0 < pe;) {
-            const int ae = elo + 1 + lane;
-            const int s = ae <= nact ? cstart[ae] - x0 : (1 << 30);  // >= 1
-            const int s63 = __builtin_amdgcn_readlane(s, 63);
-            int len = pe - x0 < 64 * U ? pe - x0 : 64 * U;
-            if (s63 < len) len = s63;
-            *reinterpret_cast<uint64_t*>(ownb + 8 * lane) = 0ull;
-            wave_lds_sync();
-            if (s < len) ownb[8 * (s & 63) + (s >> 6)] = (uint8_t)(lane + 1);
-            wave_lds_sync();
-            const uint64_t ow = *reinterpret_cast<const uint64_t*>(ownb + 8 * lane);
-            wave_lds_sync();  // ownb is rewritten by the next step
-            int32_t r[U];
-            a_t va[U];
-            int ev[U];
-            int carry = 0;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-              r[u] = kNoRow;
-              if (u * 64 >= len) continue;  // wave-uniform
-              const int cnt0 = wave_incl_max((int)((ow >> (8 * u)) & 0xffu), 0);
-              const int cnt = cnt0 > carry ? cnt0 : carry;
-              carry = __builtin_amdgcn_readlane(cnt, 63);
-              const int x = u * 64 + lane;
-              if (x < len) {
-                const int e = elo + cnt;
-                ev[u] = e;
-                const int64_t q = cbase[e] + x0 + x;
-                r[u] = rowsA[q];
-                va[u] = valsA[q];
-              }
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-              if (r[u] == kNoRow) continue;
-              const uint32_t d = (uint32_t)(r[u] - lo);
-              if (d >= tw) {
-                bad |= 1 << 8;
-                continue;
-              }
-              const uint32_t wv = dw[d >> 5];
-              if (!((wv >> (d & 31)) & 1u)) bad |= 1 << 11;  // a product row the symbolic pass did not mark
-              const int slot = dp[d >> 5] + __popc(wv & ((1u << (d & 31)) - 1u));
-              SR::lds_acc(&vals[slot], SR::multiply(va[u], cscale[ev[u]]));
-            }
-            elo += __popcll(__ballot(s <= len));
-            x0 += len;
-          }
-        }
-        __syncthreads();  // the compacted arrays are rewritten by the next chunk
-      }
-      prefetch_next();
-      // commit: values in row order (rank q = output out_pos + q), rows off the bitmap
-      if (out_pos + dtotal > out_end || out_pos + dtotal > a.ccap) {
-        bad |= 1 << 5;
-      } else {
-        for (int q = tid; q < dtotal; q += BS)
-          reinterpret_cast<val_t*>(a.Cnum)[out_pos + q] = SR::finalize(vals[q]);
-        for (int x = tid; x < cut; x += BS) {
-          uint32_t wv = dw[x];
-          int32_t* cr = a.Cir + out_pos + dp[x];
-          while (wv) {
-            *cr++ = lo + 32 * x + __builtin_ctz(wv);
-            wv &= wv - 1u;
-          }
+        } else if (chunked && !inited) {  // an idle first visit: its state is committed as is
+          a.gcur0[go + i] = e.cur;
+          a.gnx0[go + i] = e.nx;
         }
       }
-      out_pos += dtotal;
-      inited = true;
-    } else {
-      prefetch_next();
+      int off = len, aidx = len > 0 ? 1 : 0;
+      int P = 0, nact = 0;
+      block_excl_sum2<BS>(off, aidx, red, P, nact);
+      P = __builtin_amdgcn_readfirstlane(P);
+      nact = __builtin_amdgcn_readfirstlane(nact);
+      if (len > 0) {
+        cstart[aidx] = off;
+        cbase[aidx] = cur0 - off;
+        if constexpr (NUM) cscale[aidx] = scale;
+      }
+      if (tid == 0) cstart[nact] = P;
+      __syncthreads();
+      // ---- phase 2: wave w walks products [w*P/NW, (w+1)*P/NW) on its own
+      const int pb = (int)((int64_t)P * wid / NW), pe = (int)((int64_t)P * (wid + 1) / NW);
+      if (pb < pe) {
+        // the compacted entry owning product pb: the last one starting at or before it
+        int elo = 0;
+        {
+          int l0 = 0, h0 = nact;  // cstart[0] = 0 <= pb < P = cstart[nact]
+          while (h0 - l0 > 1) {
+            const int m = (l0 + h0) >> 1;
+            if (cstart[m] <= pb) l0 = m;
+            else h0 = m;
+          }
+          elo = __builtin_amdgcn_readfirstlane(l0);
+        }
+        // per step, up to 64*U products [x0, x0 + len): the 64 compacted entries after elo are
+        // loaded once (lane j: entry elo+1+j, start s_j relative to x0; starts are distinct since
+        // every compacted entry has a product) and scatter j+1 into the wave's byte map at their
+        // start, laid out [lane][u] so that lane l reads the U positions u*64+l as ONE 8-byte
+        // word; per batch u a DPP max-scan plus the carry from batch u-1 then counts the entries
+        // starting at or before the lane's product. The step ends where the 64th entry starts
+        // (entries past it are not loaded), at least 63 products on.
+        for (int x0 = pb; x0 < pe;) {
+          const int ae = elo + 1 + lane;
+          const int s = ae <= nact ? cstart[ae] - x0 : (1 << 30);  // >= 1
+          const int s63 = __builtin_amdgcn_readlane(s, 63);
+          int len = pe - x0 < 64 * U ? pe - x0 : 64 * U;
+          if (s63 < len) len = s63;
+          *reinterpret_cast<uint64_t*>(ownb + 8 * lane) = 0ull;
+          wave_lds_sync();
+          if (s < len) ownb[8 * (s & 63) + (s >> 6)] = (uint8_t)(lane + 1);
+          wave_lds_sync();
+          const uint64_t ow = *reinterpret_cast<const uint64_t*>(ownb + 8 * lane);
+          wave_lds_sync();  // ownb is rewritten by the next step
+          int32_t r[U];
+          a_t va[U];
+          int ev[U];
+          int carry = 0;
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            r[u] = kNoRow;
+            if (u * 64 >= len) continue;  // wave-uniform
+            const int cnt0 = wave_incl_max((int)((ow >> (8 * u)) & 0xffu), 0);
+            const int cnt = cnt0 > carry ? cnt0 : carry;
+            carry = __builtin_amdgcn_readlane(cnt, 63);
+            const int x = u * 64 + lane;
+            if (x < len) {
+              const int e = elo + cnt;
+              ev[u] = e;
+              const int64_t q = cbase[e] + x0 + x;
+              r[u] = rowsA[q];
+              if constexpr (NUM) va[u] = valsA[q];
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (r[u] != kNoRow) place(r[u], va[u], ev[u]);
+          elo += __popcll(__ballot(s <= len));
+          x0 += len;
+        }
+      }
+      __syncthreads();  // the compacted arrays are rewritten by the next chunk
     }
-    w0 += cut;
+    inited = true;
+  };
+
+  if constexpr (SYM) {
+    // ---------------- symbolic: sub-tiles of up to NWS bitmap words; with a row-block table they
+    // are dealt whole row blocks (hub stops are one table load), as task_kernel's sub-tiles
+    const bool store = a.bmp != nullptr && a.boff[task + 1] > a.boff[task];
+    uint32_t* words = reinterpret_cast<uint32_t*>(win);
+    constexpr int64_t SW = 32ll * C::NWS;  // rows per sub-tile at most
+    const int64_t R = (span + SW - 1) / SW;
+    const bool align = a.RB > 0 && (a.RB & 31) == 0 && (tlo & 31) == 0 && R >= 2;
+    int64_t wblk = 0, wrow = ((span + R - 1) / R + 31) & ~int64_t(31);
+    if (align) {
+      const int64_t nbt = ((int64_t)thi + a.RB - 1) / a.RB - tlo / a.RB;
+      const int64_t bmax = SW / a.RB;
+      const int64_t Ra = (nbt + bmax - 1) / bmax;
+      wblk = (nbt + Ra - 1) / Ra;
+    }
+    if (store && a.boff[task + 1] - a.boff[task] != (span + 31) / 32) {
+      if (tid == 0) guard_fail(a.err, 10, c, task, a.boff[task + 1] - a.boff[task], span);
+      return;
+    }
+    int my_count = 0;
+    int32_t lo = tlo;
+    while (lo < thi) {
+      int64_t he = align ? ((int64_t)lo / a.RB + wblk) * a.RB : (int64_t)lo + wrow;
+      const int32_t hi = (int32_t)(he < thi ? he : thi);
+      const uint32_t tw = (uint32_t)(hi - lo);
+      const int nwd = (int)((tw + 31) >> 5);
+      for (int x = tid; x < nwd; x += BS) words[x] = 0u;
+      // (phase 1's block scan orders the clearing before any product is marked)
+      run_chunks(lo, hi, [&](int32_t r, const a_t&, int) {
+        const uint32_t d = (uint32_t)(r - lo);
+        if (d >= tw) bad |= 1 << 8;
+        else atomicOr(&words[d >> 5], 1u << (d & 31));
+      });
+      uint32_t* sb = store ? a.bmp + a.boff[task] + ((lo - tlo) >> 5) : nullptr;
+      for (int x = tid; x < nwd; x += BS) {
+        const uint32_t wv = words[x];
+        my_count += __popc(wv);
+        if (store) sb[x] = wv;
+      }
+      __syncthreads();  // the words are cleared for the next sub-tile
+      lo = hi;
+    }
+    const int total = block_sum_int<NW>(my_count, red);
+    if (tid == 0) a.cnt[task] = total;
+    if (bad) guard_fail(a.err, 31 - __clz(bad), c, bad, tlo);
+    return;
+  } else {
+    // ---------------- numeric dense: windows of the stored row bitmap
+    int64_t out_pos = a.toff[task] - a.cbase;
+    const int64_t out_end = a.toff[task + 1] - a.cbase;
+    const int64_t bw0 = a.boff[task];
+    const int64_t nwt = a.boff[task + 1] - bw0;
+    if (a.bmp == nullptr || nwt != (span + 31) / 32) {
+      if (tid == 0) guard_fail(a.err, 10, c, task, nwt, span);
+      return;
+    }
+    const uint32_t* __restrict__ tb = a.bmp + bw0;
+    constexpr int64_t TB = (int64_t)C::TB;
+    int64_t wdes = TB * nwt / ((int64_t)sizeof(acc_t) * work + 6 * nwt);  // words whose outputs fill the rest
+    wdes = wdes < 64 ? 64 : (wdes > C::NWB ? C::NWB : wdes);
+    const bool dalign = kAlignSubtiles && a.RB > 0 && (a.RB & 31) == 0 && (tlo & 31) == 0;
+    const int64_t dbw = dalign ? a.RB / 32 : 1;  // words per row block
+    constexpr int KW0 = (C::NWB + BS - 1) / BS;
+    constexpr int KW = KW0 < CBH_DENSE2_PREFETCH ? KW0 : CBH_DENSE2_PREFETCH;
+    uint32_t pre[KW > 0 ? KW : 1];
+    int64_t pre_w0 = -1;
+    int64_t w0 = 0;
     __syncthreads();
+    while (w0 < nwt) {
+      const int wl = (int)((nwt - w0) < wdes ? (nwt - w0) : wdes);
+      const int dbase = (int)((TB - 6 * wl) & ~int64_t(15));
+      uint32_t* dw = reinterpret_cast<uint32_t*>(win + dbase);
+      int16_t* dp = reinterpret_cast<int16_t*>(win + dbase + 4 * wl);
+      const int capv = dbase / (int)sizeof(acc_t);
+      const int kw = (wl + BS - 1) / BS;
+      {
+        int x = tid;
+        if (pre_w0 == w0) {
+#pragma unroll
+          for (int j = 0; j < KW; ++j)
+            if (tid + j * BS < wl) dw[tid + j * BS] = pre[j];
+          x += KW * BS;
+        }
+        for (; x < wl; x += BS) dw[x] = tb[w0 + x];
+      }
+      if (tid == 0) s_cut = wl;
+      __syncthreads();
+      int tsum = 0;
+      for (int k = 0; k < kw; ++k) {
+        const int x = tid * kw + k;
+        tsum += x < wl ? __popc(dw[x]) : 0;
+      }
+      int wtotal = 0;
+      int ex = block_excl_sum<BS>(tsum, red, wtotal);
+      for (int k = 0; k < kw; ++k) {
+        const int x = tid * kw + k;
+        if (x < wl) {
+          const int pc = __popc(dw[x]);
+          dp[x] = (int16_t)(ex < 32767 ? ex : 32767);
+          if (ex <= capv && ex + pc > capv) s_cut = x;
+          ex += pc;
+        }
+      }
+      __syncthreads();
+      int cut = __builtin_amdgcn_readfirstlane(s_cut);  // (block-uniform values kept in SGPRs)
+      if (dalign && tlo + 32 * (w0 + cut) < thi) {  // window ends snap down to absolute row blocks
+        const int64_t tw0 = tlo / 32;
+        const int64_t cb = (tw0 + w0 + cut) / dbw * dbw - tw0 - w0;
+        if (cb > 0 && cb * 4 >= 3ll * cut) cut = (int)cb;
+      }
+      const int dtotal = __builtin_amdgcn_readfirstlane(cut < wl ? (int)dp[cut] : wtotal);
+      // the next window's words, loaded before this window's commit (not before its products: KW
+      // registers live across the product phase spilled)
+      auto prefetch_next = [&]() {
+        const int64_t w0n = w0 + cut;
+        if (KW > 0 && w0n < nwt) {
+          const int wln = (int)((nwt - w0n) < wdes ? (nwt - w0n) : wdes);
+#pragma unroll
+          for (int j = 0; j < KW; ++j) pre[j] = (tid + j * BS < wln) ? tb[w0n + tid + j * BS] : 0u;
+          pre_w0 = w0n;
+        }
+      };
+      const int32_t lo = (int32_t)(tlo + 32 * w0);
+      const int64_t hcut = tlo + 32 * (w0 + cut);
+      const int32_t hi = (int32_t)(hcut < thi ? hcut : thi);
+      const uint32_t tw = (uint32_t)(hi - lo);
+      if (dtotal > 0) {
+        for (int x = tid; x < dtotal; x += BS) vals[x] = SR::identity();
+        // (phase 1's block scan orders the initialisation before any accumulation)
+        run_chunks(lo, hi, [&](int32_t r, const a_t& av, int e) {
+          const uint32_t d = (uint32_t)(r - lo);
+          if (d >= tw) {
+            bad |= 1 << 8;
+            return;
+          }
+          const uint32_t wv = dw[d >> 5];
+          if (!((wv >> (d & 31)) & 1u)) bad |= 1 << 11;  // a product row the symbolic pass did not mark
+          const int slot = dp[d >> 5] + __popc(wv & ((1u << (d & 31)) - 1u));
+          SR::lds_acc(&vals[slot], SR::multiply(av, cscale[e]));
+        });
+        prefetch_next();
+        // commit: values in row order (rank q = output out_pos + q), rows off the bitmap
+        if (out_pos + dtotal > out_end || out_pos + dtotal > a.ccap) {
+          bad |= 1 << 5;
+        } else {
+          for (int q = tid; q < dtotal; q += BS)
+            reinterpret_cast<val_t*>(a.Cnum)[out_pos + q] = SR::finalize(vals[q]);
+          for (int x = tid; x < cut; x += BS) {
+            uint32_t wv = dw[x];
+            int32_t* cr = a.Cir + out_pos + dp[x];
+            while (wv) {
+              *cr++ = lo + 32 * x + __builtin_ctz(wv);
+              wv &= wv - 1u;
+            }
+          }
+        }
+        out_pos += dtotal;
+      } else {
+        prefetch_next();
+      }
+      w0 += cut;
+      __syncthreads();
+    }
+    if (tid == 0 && out_pos != out_end) atomicAdd(&a.err[0], 1);
+    if (bad) guard_fail(a.err, 31 - __clz(bad), c, bad, tlo);
   }
-  if (tid == 0 && out_pos != out_end) atomicAdd(&a.err[0], 1);
-  if (bad) guard_fail(a.err, 31 - __clz(bad), c, bad, tlo);
 }
 
 // Launches dense_kernel over order[first, first+count) (grid slices below 2^32 work-items).
-template <class SR, int BS, int EL, int U, int LDSB>
+template <class SR, int BS, int EL, int U, int LDSB, bool SYM = false>
 hipError_t launch_dense(const TaskArgs& args, int64_t first, int64_t count, hipStream_t stream) {
   if (count <= 0) return hipSuccess;
-  using C = DenseCfg<SR, BS, EL, U, LDSB>;
-  auto kern = dense_kernel<SR, BS, EL, U, LDSB>;
+  using C = DenseCfg<SR, BS, EL, U, LDSB, SYM>;
+  auto kern = dense_kernel<SR, BS, EL, U, LDSB, SYM>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -218,6 +218,16 @@ hipError_t launch_dense_numeric(const TaskArgs& a, int64_t first, int64_t count,
 #endif
 }
 
+// The symbolic pass's large bitmap tasks: the same one-workgroup-per-CU kernel (dense_kernel.h,
+// SYM = true: sub-tiles of ~940 K rows instead of task_kernel's 389 K); CBH_SYM_V2=0 keeps them on
+// task_kernel<MODE_TSYM>.
+#ifndef CBH_SYM_V2
+#define CBH_SYM_V2 1
+#endif
+struct TSym2 {
+  static constexpr int BS = 1024, EL = 1024, U = 8, LDSB = 163776;
+};
+
 // Numeric tasks of the small bin: one per wave (wave_kernel.h); wide user value types keep the
 // workgroup kernel CFG.
 template <class SR, class CFG>

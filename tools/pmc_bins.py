@@ -23,8 +23,8 @@ MODES = {0: "sym", 1: "num", 2: "dense"}
 
 
 def bin_of(name):
-    if "dense_kernel<" in name:  # device/dense_kernel.h (round 5)
-        return "num_dense"
+    if "dense_kernel<" in name:  # device/dense_kernel.h (round 5): numeric dense / symbolic bitmap
+        return "sym_bmp" if "true>" in name else "num_dense"
     m = PAT.search(name)
     if not m:
         return None
