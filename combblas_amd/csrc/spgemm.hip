@@ -1202,7 +1202,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   BinLists bl, bb;
 #if CBH_SYM_V2
   {  // the large bitmap tasks to the one-workgroup-per-CU kernel, the rest to the task kernels
-    using CS = DenseCfg<PlusTimesD<int64_t>, TSym2::BS, TSym2::EL, TSym2::U, TSym2::LDSB, true>;
+    using CS = DenseCfg<PlusTimesD<int64_t>, TSym2::BS, TSym2::EL, TSym2::U, TSym2::LDSB, KSYMB>;
     constexpr int64_t kHashKeys = (int64_t)kSymWords * kSymFill8 / 8;  // TSymLarge's key-hash capacity
     int64_t *wb, *wh;
     CBH_TRY(S.get(&wb, nt));
@@ -1230,8 +1230,8 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
   const double sb_b = 4.0 * bb.units[2] + 16.0 * bb.large_count;
   if (bb.large_count > 0)
     CBH_TRY(timed_launch(ctx, CBH_K_SYM_BMP, sb_b, [&] {
-      return launch_dense<Dummy, TSym2::BS, TSym2::EL, TSym2::U, TSym2::LDSB, true>(a, bb.large_first, bb.large_count,
-                                                                                    ctx->stream);
+      return launch_dense<Dummy, TSym2::BS, TSym2::EL, TSym2::U, TSym2::LDSB, KSYMB>(a, bb.large_first, bb.large_count,
+                                                                                     ctx->stream);
     }));
   if (diag_enabled()) CBH_TRY((launch_task_diag<Dummy, TSymLarge, MODE_TSYM>(ctx, a, bl, "symbolic")));
   else CBH_TRY((launch_task<Dummy, TSymLarge, MODE_TSYM>(ctx, a, bl.large_first, bl.large_count, CBH_K_SYM_LARGE, sb_l)));
@@ -1337,7 +1337,15 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
       CBH_TRY(timed_launch(ctx, CBH_K_NUM_DENSE, nb_d, [&] {
         return launch_dense_numeric<SR>(a, bd.large_first, bd.large_count, ctx->stream);
       }));
+#if CBH_HASH_V2
+    if (bl.large_count > 0)
+      CBH_TRY(timed_launch(ctx, CBH_K_NUM_LARGE, nb_l, [&] {
+        return launch_dense<SR, THash2::BS, THash2::EL, THash2::U, THash2::LDSB, KHASH>(a, bl.large_first,
+                                                                                        bl.large_count, ctx->stream);
+      }));
+#else
     CBH_TRY((launch_task<SR, TNumHash, MODE_TNUM>(ctx, a, bl.large_first, bl.large_count, CBH_K_NUM_LARGE, nb_l)));
+#endif
   }
   CBH_TRY((launch_task<SR, TNumMid, MODE_TNUM>(ctx, a, bl.mid_first, bl.mid_count, CBH_K_NUM_MID, nb_m)));
   if (bl.small_count > 0)  // one task per wave (wave_kernel.h)
@@ -1547,9 +1555,16 @@ int cbh_ctx_release(cbh_ctx* ctx, int64_t bytes) {
 const char* cbh_last_error(cbh_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 int cbh_hash_config(int64_t* table_slots, int64_t* threads, int64_t* per_thread) {
+#if CBH_HASH_V2
+  using CH = DenseCfg<PlusTimesD<double>, THash2::BS, THash2::EL, THash2::U, THash2::LDSB, KHASH>;
+  if (table_slots) *table_slots = CH::TH;
+  if (threads) *threads = THash2::BS;
+  if (per_thread) *per_thread = THash2::U;
+#else
   if (table_slots) *table_slots = TNumHash::T;
   if (threads) *threads = TNumHash::BS;
   if (per_thread) *per_thread = TNumHash::U;
+#endif
   return CBH_OK;
 }
 
@@ -3064,7 +3079,11 @@ int cbh_mat_col_concat(cbh_ctx* ctx, int k, const cbh_mat* const* parts, cbh_mat
 // cbh_mat_col_concat that releases the parts as it goes, one array kind at a time (pointers, then
 // rows, then values): the peak is the parts plus the largest output array, not twice the matrix
 // (a C5 step's pruned pieces are 148 GB; a copying concatenation would need 296 GB beside A and B)
-int cbh_mat_col_concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** out) {
+// The consuming concatenation. arena: the pruned pieces' arena when they borrow its rows and values
+// but could not take them over (cbh_arena_concat's fallback): its rows / values are released as soon
+// as they are copied, like an owned part's. On a failure after C's allocation both C and every part
+// are released (the parts are half consumed by then), and the error is returned.
+static int concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** out, cbh_arena* arena) {
   if (!ctx || !out || k < 1 || !parts) return fail(ctx, CBH_E_ARG, "bad concat arguments");
   *out = nullptr;
   int64_t m = 0, n = 0, nnz = 0, nzc = 0;
@@ -3092,12 +3111,9 @@ int cbh_mat_col_concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** o
         parts[i]->*member = nullptr;
       }
   };
-  int rc = dalloc(ctx, &C->cp, nzc + 1);
-  if (rc == CBH_OK) rc = dalloc(ctx, &C->jc, nzc);
-  if (rc != CBH_OK) {
-    cbh_mat_free(ctx, C);
-    return rc;
-  }
+  const int rc = [&]() -> int {  // (CBH_HIP / CBH_TRY return from here)
+  CBH_TRY(dalloc(ctx, &C->cp, nzc + 1));
+  CBH_TRY(dalloc(ctx, &C->jc, nzc));
   int64_t coff = 0, eoff = 0, zoff = 0;
   for (int i = 0; i < k; ++i) {
     const cbh_mat* P = parts[i];
@@ -3120,10 +3136,7 @@ int cbh_mat_col_concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** o
     std::fprintf(stderr, "[cbh memdiag] concat: %d parts, device free %.2f GB, rows need %.2f GB\n", k, fr / 1e9,
                  nnz * 4 / 1e9);
   }
-  if ((rc = dalloc(ctx, &C->ir, nnz)) != CBH_OK) {
-    cbh_mat_free(ctx, C);
-    return rc;
-  }
+  CBH_TRY(dalloc(ctx, &C->ir, nnz));
   eoff = 0;
   for (int i = 0; i < k; ++i) {
     if (parts[i]->nnz > 0)
@@ -3132,16 +3145,17 @@ int cbh_mat_col_concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** o
     eoff += parts[i]->nnz;
   }
   release(&cbh_mat::ir, true);
+  if (arena) {  // (stream-ordered: the copies above run first)
+    dfree(ctx, arena->ir);
+    arena->ir = nullptr;
+  }
   if (std::getenv("CBH_MEMDIAG")) {
     size_t fr = 0, tot = 0;
     (void)hipMemGetInfo(&fr, &tot);
     std::fprintf(stderr, "[cbh memdiag] concat: rows copied and released, device free %.2f GB, values need %.2f GB\n",
                  fr / 1e9, nnz * vb / 1e9);
   }
-  if ((rc = dalloc(ctx, reinterpret_cast<char**>(&C->num), nnz * vb)) != CBH_OK) {
-    cbh_mat_free(ctx, C);
-    return rc;
-  }
+  CBH_TRY(dalloc(ctx, reinterpret_cast<char**>(&C->num), nnz * vb));
   eoff = 0;
   for (int i = 0; i < k; ++i) {
     if (parts[i]->nnz > 0)
@@ -3150,15 +3164,30 @@ int cbh_mat_col_concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** o
     eoff += parts[i]->nnz;
   }
   release(&cbh_mat::num, true);
+  if (arena) {
+    dfree(ctx, arena->num);
+    arena->num = nullptr;
+    arena->cap = arena->used = 0;
+  }
   CBH_HIP(ctx, hipMemcpyAsync(C->cp + nzc, &nnz, sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // nnz is a host local
   CBH_HIP(ctx, hipGetLastError());
+  return CBH_OK;
+  }();
   for (int i = 0; i < k; ++i) {
     cbh_mat_free(ctx, parts[i]);
     parts[i] = nullptr;
   }
+  if (rc != CBH_OK) {
+    cbh_mat_free(ctx, C);
+    return rc;
+  }
   *out = C;
   return CBH_OK;
+}
+
+int cbh_mat_col_concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** out) {
+  return concat_consume(ctx, k, parts, out, nullptr);
 }
 
 int cbh_arena_create(cbh_ctx* ctx, int64_t capacity, int64_t value_bytes, cbh_arena** out) {
@@ -3200,7 +3229,7 @@ int cbh_arena_concat(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_arena* a, cbh_mat
       contiguous = false;
     off += P->nnz;
   }
-  if (!contiguous || off != a->used) return cbh_mat_col_concat_consume(ctx, k, parts, out);
+  if (!contiguous || off != a->used) return concat_consume(ctx, k, parts, out, a);
   for (int i = 0; i < k; ++i) {
     m = std::max(m, parts[i]->m);
     n += parts[i]->n;

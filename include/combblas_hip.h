@@ -104,8 +104,9 @@ int cbh_ctx_take_retries(cbh_ctx* ctx, int64_t* subtile_retries);
  * device's free / total memory (hipMemGetInfo); any pointer may be NULL. */
 int cbh_ctx_memory(cbh_ctx* ctx, int64_t* live_bytes, int64_t* cached_bytes, int64_t* device_free,
                    int64_t* device_total);
-/* The large numeric hash kernel's configuration: table slots T (plus 64 guard slots), threads per
- * workgroup and products per thread per window (the commit queue holds threads * per_thread). */
+/* The large numeric hash kernel's configuration: home slots T of its order-preserving table (plus
+ * 64 guard slots; a sub-tile plans T/2 outputs), threads per workgroup, products per thread per
+ * gather step. */
 int cbh_hash_config(int64_t* table_slots, int64_t* threads, int64_t* per_thread);
 /* Route every device allocation of this context through caller callbacks (e.g. the torch
  * caching allocator), stream-ordered on `stream`. NULL alloc restores the built-in block cache.        */
@@ -365,7 +366,10 @@ int cbh_mat_col_slice(cbh_ctx* ctx, const cbh_mat* M, int64_t c0, int64_t c1, cb
 int cbh_mat_col_concat(cbh_ctx* ctx, int k, const cbh_mat* const* parts, cbh_mat** out);
 /* The same, releasing the parts as they are consumed (one array kind at a time: pointers, rows,
  * values), so the peak is the parts plus the largest output array instead of twice the matrix;
- * on success every parts[i] is freed and set to NULL. ColConcatenate also empties its inputs. */
+ * every parts[i] is freed and set to NULL -- on success, and also on a failure past the argument
+ * checks (the parts are half consumed by then; no result is produced). ColConcatenate also
+ * empties its inputs. cbh_arena_concat's copying fallback (pieces not tiling the arena) releases
+ * the arena's rows and values as soon as they are copied.                                      */
 int cbh_mat_col_concat_consume(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_mat** out);
 /* Rows [r0, r1) of the block as an (r1 - r0) x n block, row ids rebased, empty columns dropped
  * (Mult_AnXBn_DoubleBuff's row halves of B). */

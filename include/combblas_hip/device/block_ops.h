@@ -39,6 +39,12 @@ __device__ __forceinline__ void guard_fail(int* err, int site, int64_t v0 = 0, i
   }
 }
 
+// The wave scans below use GFX9-only DPP controls (row_bcast:15/31, wave_shr:1); the library is
+// built for gfx950 only (build.py), and any other device target stops here rather than miscompiling.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "block_ops.h: the DPP wave scans are GFX9 (gfx950) code"
+#endif
+
 // Inclusive scans across a wavefront: DPP row shifts 1/2/4/8 and the GFX9 row broadcasts 15/31
 // (the sequence LLVM's atomic optimizer emits for gfx9) -- VALU moves instead of six ds_bpermute
 // round trips through LDS (round 4: A^2 144.3 -> 150.1 GFLOP/s, every task kernel faster).

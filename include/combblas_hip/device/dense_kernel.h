@@ -43,11 +43,16 @@ namespace cbh {
 #define CBH_DENSE2_PREFETCH 8
 #endif
 
-template <class SR, int BS, int EL, int U, int LDSB, bool SYM = false>
+// kernel kinds of dense_kernel: numeric dense windows, symbolic bitmap sub-tiles, numeric hash
+// sub-tiles (the order-preserving LDS hash of task_kernel.h with a table of ~7 K slots)
+enum : int { KDENSE = 0, KSYMB = 1, KHASH = 2 };
+
+template <class SR, int BS, int EL, int U, int LDSB, int KIND = KDENSE>
 struct DenseCfg {
   using acc_t = typename SR::acc_t;
   using b_t = typename sr_b_type<SR>::type;
-  static constexpr bool NUM = !SYM;
+  static constexpr bool NUM = KIND != KSYMB;
+  static constexpr bool ROLL = KIND == KHASH;  // sub-tiles may overflow and be retried: cursors commit after
   static constexpr int NW = BS / 64;
   static constexpr size_t al(size_t x) { return (x + 15) & ~size_t(15); }
   // entry state (LDS-resident tasks): cursor, row at the cursor, end - cursor, cursor - column
@@ -58,9 +63,12 @@ struct DenseCfg {
   static constexpr size_t o_coff = al(o_rem + sizeof(int32_t) * EL);
   static constexpr size_t o_hub = al(o_coff + sizeof(int32_t) * EL);
   static constexpr size_t o_scale = al(o_hub + sizeof(int32_t) * EL);
+  // hash: the cursors after the current sub-tile, committed only when it did not overflow
+  static constexpr size_t o_pcur = al(o_scale + (NUM ? sizeof(b_t) * EL : 0));
+  static constexpr size_t o_pnx = al(o_pcur + (ROLL ? sizeof(int64_t) * EL : 0));
   // compacted active entries of the current chunk: start offset (+ the total at [nact]), gather
   // base (cursor - start offset), B value (numeric only)
-  static constexpr size_t o_cstart = al(o_scale + (NUM ? sizeof(b_t) * EL : 0));
+  static constexpr size_t o_cstart = al(o_pnx + (ROLL ? sizeof(int32_t) * EL : 0));
   static constexpr size_t o_cbase = al(o_cstart + sizeof(int32_t) * (EL + 1));
   static constexpr size_t o_cscale = al(o_cbase + sizeof(int64_t) * EL);
   static constexpr size_t o_own = al(o_cscale + (NUM ? sizeof(b_t) * EL : 0));  // NW x 512-byte owner maps
@@ -72,6 +80,15 @@ struct DenseCfg {
   static constexpr size_t bytes = o_win + TB;
   static constexpr int NWB = (int)((TB - 64) / 6) / 8 * 8;  // widest window (all words, no values)
   static constexpr int NWS = (int)(TB / 4) / 64 * 64;      // symbolic bitmap words (32 rows each)
+  // hash: TH home slots + kGuard (forward probing never wraps), keys then values; the commit queue
+  // (int16 slot ids) reuses the compacted arrays
+  static constexpr int TH0 = ((int)((TB - 32) / (sizeof(int32_t) + sizeof(acc_t))) - kGuard) / 64 * 64;
+  static constexpr int THQ = ((int)((o_own - o_cstart) / 2) - kGuard) / 64 * 64;  // the queue's bound
+  static constexpr int TH = TH0 < THQ ? TH0 : THQ;
+  static constexpr int TA = TH + kGuard;
+  static constexpr size_t o_hvals = al(sizeof(int32_t) * TA);  // (relative to o_win)
+  static_assert(KIND != KHASH || (o_hvals + sizeof(acc_t) * TA <= TB && 2 * TA <= o_own - o_cstart && TA < 32768),
+                "hash table and commit queue fit");
   static_assert(NWB <= 32767, "int16 window prefixes");
   static_assert(bytes <= 163840, "one workgroup's LDS");
   static_assert(EL == BS, "one entry per thread per chunk");
@@ -105,19 +122,25 @@ __device__ __forceinline__ void block_excl_sum2(int& a, int& b, int* red, int& t
   tb = xb;
 }
 
-// SYM = false: the numeric dense tasks (windows of the stored bitmap, values by rank);
-// SYM = true: the symbolic pass's bitmap tasks (sub-tiles of NWS words, rows marked with atomicOr,
+// KDENSE: the numeric dense tasks (windows of the stored bitmap, values by rank);
+// KSYMB: the symbolic pass's bitmap tasks (sub-tiles of NWS words, rows marked with atomicOr,
 // distinct rows counted and, for a dense candidate, its bitmap stored) -- estimateNNZ_Hash
-// (mtSpGEMM.h:806-933) for the tasks whose row bitmap is cheaper than a key hash.
-template <class SR, int BS, int EL, int U, int LDSB, bool SYM = false>
+// (mtSpGEMM.h:806-933) for the tasks whose row bitmap is cheaper than a key hash;
+// KHASH: the numeric hash tasks (LocalHybridSpGEMM's hash branch, mtSpGEMM.h:362-437): sub-tiles of
+// up to TH/2 outputs in task_kernel's order-preserving LDS hash (slot (row-lo)*TH/(hi-lo), forward
+// probing, rank commit without a sort); a sub-tile that overflows its probes is
+// retried with half the rows, so its entries' cursors commit only after it succeeded.
+template <class SR, int BS, int EL, int U, int LDSB, int KIND = KDENSE>
 __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves per CU
-  using C = DenseCfg<SR, BS, EL, U, LDSB, SYM>;
+  constexpr bool SYM = KIND == KSYMB;
+  using C = DenseCfg<SR, BS, EL, U, LDSB, KIND>;
   using val_t = typename SR::val_t;
   using acc_t = typename SR::acc_t;
   using a_t = typename sr_a_type<SR>::type;
   using b_t = typename C::b_t;
   constexpr int NW = C::NW;
   constexpr bool NUM = C::NUM;
+  constexpr bool ROLL = C::ROLL;
   static_assert(!sr_locked<SR>::value, "the dense kernel accumulates with SR::lds_acc");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -127,6 +150,8 @@ __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves
   int32_t* scoff = reinterpret_cast<int32_t*>(smem + C::o_coff);
   int32_t* shub = reinterpret_cast<int32_t*>(smem + C::o_hub);
   b_t* sscale = reinterpret_cast<b_t*>(smem + C::o_scale);
+  int64_t* pcur = reinterpret_cast<int64_t*>(smem + C::o_pcur);
+  int32_t* pnx = reinterpret_cast<int32_t*>(smem + C::o_pnx);
   int32_t* cstart = reinterpret_cast<int32_t*>(smem + C::o_cstart);
   int64_t* cbase = reinterpret_cast<int64_t*>(smem + C::o_cbase);
   b_t* cscale = reinterpret_cast<b_t*>(smem + C::o_cscale);
@@ -134,6 +159,7 @@ __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves
   unsigned char* win = smem + C::o_win;
   acc_t* vals = reinterpret_cast<acc_t*>(win);
   __shared__ int32_t s_cut;
+  __shared__ int32_t s_ovf;  // hash: the current sub-tile overflowed (read after barriers)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   uint8_t* ownb = smem + C::o_own + 512 * wid;
@@ -232,6 +258,7 @@ __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves
     }
   }
   bool inited = !chunked;  // chunked: the HBM entry state is written by the first processed range
+  int par = 0;  // hash, chunked: which HBM cursor buffer holds the committed cursors (gcur0 / gcur1)
 
   // Every product of the row range [lo, hi) (all chunks of the task's entries): phase 1 moves each
   // entry's cursor past the range and compacts the active entries, phase 2 (wave-independent)
@@ -252,10 +279,12 @@ __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves
         } else if (!inited) {
           e = first_visit(i, lo, lo == tlo && (full & 1));
         } else {
-          e.cur = a.gcur0[go + i];
-          e.nx = a.gnx0[go + i];
+          e.cur = (par ? a.gcur1 : a.gcur0)[go + i];
+          e.nx = (par ? a.gnx1 : a.gnx0)[go + i];
         }
         cur0 = e.cur;
+        int64_t ncur = e.cur;  // the cursor past the range, and its row
+        int32_t nnx = e.nx;
         if (e.nx < hi) {
           if (!chunked) {
             e.rem = srem[tid];
@@ -280,18 +309,26 @@ __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves
           }
           len = (int)(stop - e.cur);
           if constexpr (NUM) scale = e.scale;
-          if (!chunked) {
+          ncur = stop;
+          nnx = nx2;
+          if (!ROLL && !chunked) {
             scur[tid] = stop;
             snx[tid] = nx2;
             srem[tid] = e.rem - len;
             scoff[tid] = e.coff + len;
-          } else {
-            a.gcur0[go + i] = stop;
-            a.gnx0[go + i] = nx2;
           }
-        } else if (chunked && !inited) {  // an idle first visit: its state is committed as is
-          a.gcur0[go + i] = e.cur;
-          a.gnx0[go + i] = e.nx;
+        }
+        if constexpr (ROLL) {  // pending until the sub-tile commits (hash_commit_cursors)
+          if (!chunked) {
+            pcur[tid] = ncur;
+            pnx[tid] = nnx;
+          } else {
+            (par ? a.gcur0 : a.gcur1)[go + i] = ncur;
+            (par ? a.gnx0 : a.gnx1)[go + i] = nnx;
+          }
+        } else if (chunked && (ncur != e.cur || !inited)) {  // (an idle entry's state is unchanged)
+          a.gcur0[go + i] = ncur;
+          a.gnx0[go + i] = nnx;
         }
       }
       int off = len, aidx = len > 0 ? 1 : 0;
@@ -328,6 +365,7 @@ __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves
         // starting at or before the lane's product. The step ends where the 64th entry starts
         // (entries past it are not loaded), at least 63 products on.
         for (int x0 = pb; x0 < pe;) {
+          if (ROLL && __hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
           const int ae = elo + 1 + lane;
           const int s = ae <= nact ? cstart[ae] - x0 : (1 << 30);  // >= 1
           const int s63 = __builtin_amdgcn_readlane(s, 63);
@@ -368,10 +406,143 @@ __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves
       }
       __syncthreads();  // the compacted arrays are rewritten by the next chunk
     }
-    inited = true;
   };
 
-  if constexpr (SYM) {
+  if constexpr (KIND == KHASH) {
+    // ---------------- numeric hash: sub-tiles of up to TH/2 planned outputs (task_kernel's plan)
+    int32_t* keys = reinterpret_cast<int32_t*>(win);
+    acc_t* hv = reinterpret_cast<acc_t*>(win + C::o_hvals);
+    int16_t* Q = reinterpret_cast<int16_t*>(smem + C::o_cstart);  // commit queue (after the products)
+    constexpr int TH = C::TH, TA = C::TA;
+    int64_t out_pos = a.toff[task] - a.cbase;
+    const int64_t out_end = a.toff[task + 1] - a.cbase;
+    constexpr int64_t cap = (int64_t)TH * kFill8 / 8;  // outputs per sub-tile
+    int64_t R = (work + cap - 1) / cap;
+    if (R > span) R = span;
+    if (R < 1) R = 1;
+    int64_t wnom = (span + R - 1) / R;
+    const bool align = kAlignSubtiles && R >= 2 && a.RB > 0 && wnom >= 4ll * a.RB;
+    int64_t wblk = 0;
+    if (align) {
+      const int64_t nbt = ((int64_t)thi + a.RB - 1) / a.RB - tlo / a.RB;
+      wblk = (nbt + R - 1) / R;
+      wnom = wblk * a.RB;
+    }
+    constexpr int SPW = ((TA + NW - 1) / NW + 63) / 64 * 64;  // slots per wave in the commit
+    constexpr int NBW = SPW / 64;
+    int32_t lo = tlo;
+    int64_t w = wnom;
+    while (lo < thi) {
+      int64_t he = (int64_t)lo + w;
+      if (align) {
+        if (w == wnom) {
+          he = ((int64_t)lo / a.RB + wblk) * a.RB;
+        } else {  // a retried (halved) sub-tile: its end snaps down to a block boundary
+          const int64_t hb = he / a.RB * a.RB;
+          if (hb > lo) he = hb;
+        }
+      }
+      const int32_t hi = (int32_t)(he < thi ? he : thi);
+      const uint32_t tw = (uint32_t)(hi - lo);
+      const uint64_t scl = ((uint64_t)TH << 32) / (uint64_t)tw;  // order-preserving slot map
+      for (int x = tid; x < TA; x += BS) {
+        keys[x] = kEmpty;
+        hv[x] = SR::identity();
+      }
+      if (tid == 0) s_ovf = 0;
+      // (phase 1's block scan orders the clearing before any insertion)
+      run_chunks(lo, hi, [&](int32_t r, const a_t& av, int e) {
+        const uint32_t d = (uint32_t)(r - lo);
+        if (d >= tw) {
+          bad |= 1 << 8;
+          return;
+        }
+        uint32_t sl = (uint32_t)(((uint64_t)d * scl) >> 32);
+        bool ok = false;
+        for (int probe = 0; probe < kPmax && sl < (uint32_t)TA; ++probe, ++sl) {
+          const int32_t k = atomicCAS(&keys[sl], kEmpty, r);
+          if (k == kEmpty || k == r) {
+            SR::lds_acc(&hv[sl], SR::multiply(av, cscale[e]));
+            ok = true;
+            break;
+          }
+        }
+        if (!ok) __hip_atomic_store(&s_ovf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      });
+      if (__builtin_amdgcn_readfirstlane(s_ovf)) {  // retry with half the rows (pending cursors dropped)
+        if (tid == 0) atomicAdd(&a.err[16], 1);   // retry counter (cbh_ctx_take_retries)
+        if (tw == 1) {
+          if (tid == 0) atomicOr(&a.err[1], 1);
+          return;
+        }
+        w = (tw + 1) / 2;
+        __syncthreads();
+        continue;
+      }
+      // the sub-tile is final: its entries' cursors commit
+      if (!chunked) {
+        if (tid < ne) {
+          const int sg = (int)(pcur[tid] - scur[tid]);
+          scur[tid] = pcur[tid];
+          snx[tid] = pnx[tid];
+          srem[tid] -= sg;
+          scoff[tid] += sg;
+        }
+      } else {
+        par ^= 1;
+      }
+      inited = true;
+      // rank commit (task_kernel.h): occupied slots per wave -> the queue in slot
+      // order -> every wave commits a queue range cut at run starts
+      int qbase = 0, qtot = 0;
+      uint64_t occm[NBW];
+      {
+        const int sb = wid * SPW < TA ? wid * SPW : TA;
+        const int se = sb + SPW < TA ? sb + SPW : TA;
+        int wc = 0;
+#pragma unroll
+        for (int b = 0; b < NBW; ++b) {
+          const int sl = sb + 64 * b + lane;
+          occm[b] = __ballot(sl < se && keys[sl] != kEmpty);
+          wc += __popcll(occm[b]);
+        }
+        if (lane == 0) red[NW + wid] = wc;
+        __syncthreads();
+#pragma unroll
+        for (int x = 0; x < NW; ++x) {
+          const int rr = red[NW + x];
+          qbase += (x < wid) ? rr : 0;
+          qtot += rr;
+        }
+        const uint64_t lt = (1ull << lane) - 1ull;
+        int qo = qbase;
+#pragma unroll
+        for (int b = 0; b < NBW; ++b) {
+          const uint64_t mask = occm[b];
+          if ((mask >> lane) & 1ull) Q[qo + __popcll(mask & lt)] = (int16_t)(sb + 64 * b + lane);
+          qo += __popcll(mask);
+        }
+      }
+      __syncthreads();
+      {
+        const int per = (qtot + NW - 1) / NW;
+        const int qs = queue_run_start(Q, qtot, wid * per);
+        const int qe = wid == NW - 1 ? qtot : queue_run_start(Q, qtot, (wid + 1) * per);
+        for (int b0 = qs; b0 < qe;) {
+          int used = 0;
+          bad |= rank_commit_batch<SR>(keys, hv, Q, qtot, qe, b0, used, out_pos, out_end, a.ccap, a.Cir,
+                                       reinterpret_cast<val_t*>(a.Cnum));
+          b0 += used;
+        }
+      }
+      out_pos += qtot;
+      lo = hi;
+      w = wnom;
+      __syncthreads();  // the table and the queue are reused by the next sub-tile
+    }
+    if (tid == 0 && out_pos != out_end) atomicAdd(&a.err[0], 1);
+    if (bad) guard_fail(a.err, 31 - __clz(bad), c, bad, tlo);
+  } else if constexpr (SYM) {
     // ---------------- symbolic: sub-tiles of up to NWS bitmap words; with a row-block table they
     // are dealt whole row blocks (hub stops are one table load), as task_kernel's sub-tiles
     const bool store = a.bmp != nullptr && a.boff[task + 1] > a.boff[task];
@@ -404,6 +575,7 @@ __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves
         if (d >= tw) bad |= 1 << 8;
         else atomicOr(&words[d >> 5], 1u << (d & 31));
       });
+      inited = true;
       uint32_t* sb = store ? a.bmp + a.boff[task] + ((lo - tlo) >> 5) : nullptr;
       for (int x = tid; x < nwd; x += BS) {
         const uint32_t wv = words[x];
@@ -511,6 +683,7 @@ __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves
           const int slot = dp[d >> 5] + __popc(wv & ((1u << (d & 31)) - 1u));
           SR::lds_acc(&vals[slot], SR::multiply(av, cscale[e]));
         });
+        inited = true;
         prefetch_next();
         // commit: values in row order (rank q = output out_pos + q), rows off the bitmap
         if (out_pos + dtotal > out_end || out_pos + dtotal > a.ccap) {
@@ -540,11 +713,11 @@ __global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves
 }
 
 // Launches dense_kernel over order[first, first+count) (grid slices below 2^32 work-items).
-template <class SR, int BS, int EL, int U, int LDSB, bool SYM = false>
+template <class SR, int BS, int EL, int U, int LDSB, int KIND = KDENSE>
 hipError_t launch_dense(const TaskArgs& args, int64_t first, int64_t count, hipStream_t stream) {
   if (count <= 0) return hipSuccess;
-  using C = DenseCfg<SR, BS, EL, U, LDSB, SYM>;
-  auto kern = dense_kernel<SR, BS, EL, U, LDSB, SYM>;
+  using C = DenseCfg<SR, BS, EL, U, LDSB, KIND>;
+  auto kern = dense_kernel<SR, BS, EL, U, LDSB, KIND>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,

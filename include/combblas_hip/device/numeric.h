@@ -212,7 +212,7 @@ struct TDense2 {
 template <class SR>
 hipError_t launch_dense_numeric(const TaskArgs& a, int64_t first, int64_t count, hipStream_t s) {
 #if CBH_DENSE_V2
-  return launch_dense<SR, TDense2::BS, TDense2::EL, TDense2::U, TDense2::LDSB>(a, first, count, s);
+  return launch_dense<SR, TDense2::BS, TDense2::EL, TDense2::U, TDense2::LDSB, KDENSE>(a, first, count, s);
 #else
   return launch_tasks<SR, TNumLarge, MODE_TDENSE>(a, first, count, s);
 #endif
@@ -226,6 +226,19 @@ hipError_t launch_dense_numeric(const TaskArgs& a, int64_t first, int64_t count,
 #endif
 struct TSym2 {
   static constexpr int BS = 1024, EL = 1024, U = 8, LDSB = 163776;
+};
+// The numeric hash tasks of the large bin on the same kernel (KHASH: ~7.4 K-slot order-preserving
+// table, sub-tiles of ~3.7 K outputs instead of task_kernel's 1 K; U 4: U 8 spills at the 128-VGPR
+// bound of 16 waves per CU) -- built with CBH_HASH_V2=1 only: correct (the GPU suite and the
+// scale-22 digests pass on it) but slower at scale 22, hash 269.9 -> 343.8 ms (A/B r5f,
+// profiles/r05/hash): the hash tasks are short (~9 K outputs, ~2.4 of its sub-tiles each), and one
+// workgroup per CU leaves their per-task setup and block scans uncovered, which task_kernel's three
+// 53 KB workgroups per CU overlap. TNumHash stays the shipped hash kernel.
+#ifndef CBH_HASH_V2
+#define CBH_HASH_V2 0
+#endif
+struct THash2 {
+  static constexpr int BS = 1024, EL = 1024, U = 4, LDSB = 163776;
 };
 
 // Numeric tasks of the small bin: one per wave (wave_kernel.h); wide user value types keep the

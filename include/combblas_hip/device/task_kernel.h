@@ -50,9 +50,10 @@ constexpr int kSymFill8 = 4;
 constexpr int kCapD4 = 3;
 // a task runs dense when its dense sub-tiles are at most kDRatio4/4 of its hash sub-tiles. Round 4
 // (2048-slot hash table, 262144-flop tasks): 5/6/7/8/10 -> 140.3/142.3/142.7/142.1/141.4 GFLOP/s at
-// scale 22; rounds 2-3 had found 4..12 flat around 5 with the 4096-slot hash table
+// scale 22; rounds 2-3 had found 4..12 flat around 5 with the 4096-slot hash table.
+// Round 5 (dense tasks on dense_kernel.h): 7/9/12 -> 164.4/165.6/165.1 and 164.0/165.2 (7 vs 9).
 #ifndef CBH_DRATIO4  // (A/B hook: build variants only)
-#define CBH_DRATIO4 7
+#define CBH_DRATIO4 9
 #endif
 constexpr int kDRatio4 = CBH_DRATIO4;
 

@@ -1,19 +1,19 @@
-"""GPU regression tests for the two device faults of round 2, each forcing the shipped code path
-that faulted ("What's weak" 2):
+"""GPU regression tests for the device faults of round 2 and the retry path of the hash kernel
+("What's weak" 2):
 
-1. A large numeric HASH sub-tile that inserts without a probe overflow but occupies more slots
-   than the commit queue holds (the queue holds WIN = U*BS entries, the table T + 64 slots). It
-   must be retried with half the row range from the cursors BEFORE the segment scan (fixed in
-   633d2f2; before, the retry read out of range). Construction from the shipped configuration
-   (cbh_hash_config; T 2048, 512 threads, U 4 -> WIN 2048 of 2112 slots): K = WIN + 4 rows
-   128*m (m < K) plus one row at 3*X - 1, X = 128*K -> one task of K + 1 outputs spanning 3X rows,
-   R = ceil((K + 1) / (T / 2)) = 3 hash sub-tiles of X rows (dense_subtiles prices it hash: its
-   788 K rows need 6 bitmap windows of 135 K rows, more than 7/4 of the hash sub-tiles); the
-   first holds the K evenly spaced rows (slot = 128*m*T/X = m*T/K: at most 2 rows per home
-   slot) -> K occupied slots > WIN queue entries, no
-   probe overflow -> retry (the counter cbh_ctx_take_retries must see it).
-   Variants: the column's products from ONE B entry (cursors in LDS) and from 600 B entries
-   (> EMAX = 512: chunked, cursors double-buffered in HBM); f64 and int64 values.
+1. A large numeric HASH sub-tile that overflows must be retried with half its row range from the
+   cursors BEFORE it (round 2 faulted on a retry that read cursors the segment scan had already
+   moved). (a) The probe limit: K = 2000 consecutive rows plus one row at the end of a 10^7-row
+   span -> one task of K + 1 outputs (the large hash bin: > 1024 outputs), and the order-preserving
+   slot map (row - lo) * T / span puts the K rows on one home slot: the probe chain passes
+   kPmax = 64 and the sub-tile is halved until its rows spread. (b) task_kernel's commit queue
+   (WIN = U * BS entries < the T + 64 slots, cbh_hash_config): a sub-tile that inserts without a
+   probe overflow but occupies more slots than the queue holds (K = WIN + 4 rows 128*m plus one row
+   at 3*X - 1, X = 128*K: R = 3 sub-tiles of X rows, the first with K occupied slots, at most 2 rows
+   per home slot). The retry counter (cbh_ctx_take_retries) must see both. Variants: the
+   column's products from ONE B entry (cursors in LDS) and from 600 / 1200 B entries (chunked,
+   cursors double-buffered in HBM); f64 and int64 values. (b) is skipped for a kernel whose queue
+   holds every slot (dense_kernel.h KHASH, built with CBH_HASH_V2=1).
 2. The TC dot-form piece kernels are wave-strided with a capped grid (an AQL dispatch counts
    work-items in 32 bits; scale 22 overflowed the direct grid, fixed in 2b52875). The test-only
    CBH_TEST_GRID_CAP lowers the cap to 1 block (4 waves) so that scale 12/14 runs many strides
@@ -29,6 +29,54 @@ import helpers as H
 
 pytestmark = pytest.mark.gpu
 
+K_CLUSTER = 2000  # > the mid bin's 1024 outputs: the task runs the large hash kernel
+
+
+def _probe_overflow_operands(nentries, dtype, seed):
+    import ctypes
+
+    from combblas_amd._lib import lib
+
+    T, bs, u = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    lib().cbh_hash_config(ctypes.byref(T), ctypes.byref(bs), ctypes.byref(u))
+    assert T.value >= 1024, T.value
+    rng = np.random.default_rng(seed)
+    m = 10_000_000
+    rows = np.concatenate([np.arange(K_CLUSTER, dtype=np.int64), [m - 1]])
+    owner = np.concatenate([np.arange(K_CLUSTER) % nentries, [nentries - 1]])  # A column of each row
+    order = np.lexsort((rows, owner))
+    rows, owner = rows[order], owner[order]
+    vals = rng.integers(1, 9, rows.size).astype(dtype) * (1 if dtype == np.int64 else 0.5)
+    cp = np.searchsorted(owner, np.arange(nentries + 1)).astype(np.int64)
+    A = H.Dcsc(m, nentries, np.arange(nentries, dtype=np.int64), cp, rows.astype(np.int32), vals.astype(dtype))
+    bv = rng.integers(1, 5, nentries).astype(dtype) * (1 if dtype == np.int64 else 0.25)
+    B = H.Dcsc(nentries, 1, np.zeros(1, np.int64), np.array([0, nentries], np.int64),
+               np.arange(nentries, dtype=np.int32), bv.astype(dtype))
+    return A, B
+
+
+@pytest.mark.parametrize("nentries", [1, 1200])
+@pytest.mark.parametrize("dtype", [np.float64, np.int64])
+def test_hash_probe_overflow_retry(ctx, oracle, nentries, dtype):
+    import combblas_amd as cb
+
+    A, B = _probe_overflow_operands(nentries, dtype, 7 + nentries)
+    dA = cb.SpDCCols.from_host(ctx, cb.HostDcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num))
+    dB = cb.SpDCCols.from_host(ctx, cb.HostDcsc(B.m, B.n, B.jc, B.cp, B.ir, B.num))
+    ctx.take_retries()  # reset the device retry counter
+    C = cb.LocalHybridSpGEMM(cb.PlusTimesSRing, dA, dB)
+    retries = ctx.take_retries()
+    h = C.to_host()
+    got = H.Dcsc(h.m, h.n, h.jc, h.cp, h.ir, h.num)
+    exp = oracle.spgemm(A, B, "plus_times", "hybrid")
+    assert exp.nnz == K_CLUSTER + 1
+    H.assert_dcsc_equal(got, exp, msg=f"probe overflow, {nentries} B entries, {np.dtype(dtype).name}")
+    # the retry path fired: the clustered sub-tile was redone with half its rows until they spread
+    assert retries >= 1, "the probe overflow did not trigger a sub-tile retry"
+    for S in (C, dA, dB):
+        S.free()
+
+
 def _queue_rows():
     """K = the commit queue + 4 (see the module docstring), from the library's configuration"""
     import ctypes
@@ -37,6 +85,8 @@ def _queue_rows():
 
     T, bs, u = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     lib().cbh_hash_config(ctypes.byref(T), ctypes.byref(bs), ctypes.byref(u))
+    if bs.value == 1024:  # the KHASH kernel (CBH_HASH_V2=1): its commit queue holds every slot
+        pytest.skip("the shipped hash kernel's commit queue holds every slot")
     K = bs.value * u.value + 4
     assert K <= T.value + 64 and -(-(K + 1) // (T.value // 2)) == 3, (T.value, bs.value, u.value)
     return K

@@ -30,7 +30,7 @@ timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/
 tail -1 "$OUT/smoke.log"
 step "per-bin PMC"
 timeout -k 10 900 bash tools/gpu_bins.sh "$TAG/binsrun" 22 > "$OUT/bins.log" 2>&1 || { tail -20 "$OUT/bins.log"; exit 1; }
-for k in "1024, 1024, 8, 163776, false>:num_dense" "1024, 1024, 8, 163776, true>:sym_bmp" "2048, 512, 512, 4, 1, false>:num_large" "PlusTimesD<long>, 8192, 512, 512, 16, 0, false>:sym_large"; do
+for k in "1024, 1024, 8, 163776, 0>:num_dense" "1024, 1024, 8, 163776, 1>:sym_bmp" "2048, 512, 512, 4, 1, false>:num_large" "PlusTimesD<long>, 8192, 512, 512, 16, 0, false>:sym_large"; do
   python3 tools/pmc_traffic.py "$OUT/binsrun/bins" "${k%:*}" "profiles/pmc_${k##*:}.json" "tools/gpu_final.sh $TAG (shipped build)" > /dev/null || exit 1
 done
 mkdir -p "$OUT/pmcjson" && cp profiles/pmc_*.json "$OUT/pmcjson/"
