@@ -210,16 +210,16 @@ int cbh_ctx_enable_timing(cbh_ctx* ctx, int enable);
 /* Per-kernel-class totals accumulated while timing is enabled: HIP-event time of every launch,
  * launch count, and the ALGORITHMIC bytes those launches processed (SURVEY.md §8(d):
  * (s_i+s_v)*(nnz(B)+flops+nnz(C)) + column pointers; the symbolic pass counts row ids only).  */
-#define CBH_K_SYM_LARGE 0 /* task_kernel<...,8192,512,512,8,MODE_TSYM>   symbolic, work > 256   */
-#define CBH_K_SYM_SMALL 1 /* task_kernel<...,512,128,256,4,MODE_TSYM>    symbolic, work <= 256  */
-#define CBH_K_NUM_LARGE 2 /* task_kernel<SR,4096,512,512,8,MODE_TNUM>    numeric hash sub-tiles */
-#define CBH_K_NUM_SMALL 3 /* task_kernel<SR,512,128,256,4,MODE_TNUM>     numeric, <= 256 outputs */
+#define CBH_K_SYM_LARGE 0 /* task_kernel<...,8192,512,512,16,MODE_TSYM>    symbolic hash, work > 2048   */
+#define CBH_K_SYM_SMALL 1 /* wave_kernel<...,2048,4,4,0>                  symbolic, one task per wave  */
+#define CBH_K_NUM_LARGE 2 /* task_kernel<SR,2048,512,512,4,MODE_TNUM>     numeric hash sub-tiles       */
+#define CBH_K_NUM_SMALL 3 /* wave_kernel<SR,512,4,4,1>                    numeric, one task per wave   */
 #define CBH_K_MERGE_SYM 4
 #define CBH_K_MERGE_NUM 5
-#define CBH_K_NUM_DENSE 6 /* dense_kernel<SR,1024,1024,8,163776,false>  numeric bitmap-rank    */
-#define CBH_K_SYM_MID 7   /* task_kernel<...,4096,256,256,4,MODE_TSYM>   symbolic, 256 < work <= 2048 */
-#define CBH_K_NUM_MID 8   /* task_kernel<SR,2048,256,256,4,MODE_TNUM>    numeric, 256 < outputs <= 1024 */
-#define CBH_K_SYM_BMP 9   /* dense_kernel<...,1024,1024,8,163776,true>  symbolic bitmap tasks (one WG per CU) */
+#define CBH_K_NUM_DENSE 6 /* dense_kernel<SR,1024,1024,8,163776,KDENSE>   numeric bitmap-rank windows  */
+#define CBH_K_SYM_MID 7   /* task_kernel<...,4096,256,256,4,MODE_TSYM>    symbolic, mid-size tasks     */
+#define CBH_K_NUM_MID 8   /* task_kernel<SR,2048,256,256,4,MODE_TNUM>     numeric, mid-size tasks      */
+#define CBH_K_SYM_BMP 9   /* dense_kernel<...,1024,1024,8,163776,KSYMB>   symbolic bitmap tasks        */
 #define CBH_K_NKINDS 10
 typedef struct cbh_kernel_stat {
   double ms;
