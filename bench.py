@@ -10,10 +10,14 @@ materialised in HBM one after another (MemEfficientSpGEMM's phase loop, ParFrien
 Inputs are resident in HBM before the timed region.
 
 N>1 (launched by torch.distributed.run): the same fixed product on a process grid, as the
-reference distributes it (north_star): 2D SUMMA with RCCL row/column broadcasts of the DCSC
-blocks on a square world (4 GPUs = 2x2), 3D SUMMA otherwise (2 GPUs = 1x1x2, 8 GPUs = 2x2x2:
-per-layer SUMMA + the fiber reduce-scatter as an RCCL alltoall), every phase of C materialised in
-HBM -> "scaling": "strong". Timing: barrier + synchronize around exactly K steps, max over ranks.
+reference distributes it (north_star): 2D SUMMA on a square world (4 GPUs = 2x2), 3D SUMMA otherwise
+(2 GPUs = 1x1x2, 8 GPUs = 2x2x2: per-layer SUMMA + the fiber reduce-scatter), every phase of C
+materialised in HBM -> "scaling": "strong". The host side is the C++ one north_star names
+(--driver auto/cpp): rank 0 runs cxx/_build/bench_summa under mpirun -- the reference's SpParMat /
+SpParMat3D over device blocks, RCCL broadcasts and fiber exchange -- while the torch ranks wait on
+a CPU barrier; --driver python runs combblas_amd's Python drivers over torch.distributed instead
+(auto falls back to them when the C++ run fails cleanly). Timing: barrier + synchronize around
+exactly K steps, max over ranks.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scale 22]
 """
@@ -99,6 +103,8 @@ def parse():
                    help="N>1: cpp = the C++ host path (cxx/bench_summa under mpirun), python = combblas_amd's "
                         "drivers; auto = cpp when it is built, python if it fails to start")
     p.add_argument("--phases", type=int, default=0, help="N>1 cpp driver: column phases (0 = planned)")
+    p.add_argument("--cpp-timeout", type=float, default=1200.0, help="N>1 cpp driver: seconds before it is killed "
+                                                                       "(auto: the python drivers run instead)")
     return p.parse_args()
 
 
@@ -322,12 +328,20 @@ def _cpp_rank0(args, world, cb):
     cmd = [MPIRUN, "-np", str(world), CPP_BENCH, str(args.scale), str(args.steps), str(args.warmup), str(args.phases)]
     log("C++ driver: " + " ".join(cmd))
     t0 = time.perf_counter()
-    r = subprocess.run(cmd, env=env, cwd=HERE, stdout=subprocess.PIPE, text=True)  # stderr streams through
+    # own session: on a time-out the whole mpirun tree (hydra proxies and ranks) is killed
+    pr = subprocess.Popen(cmd, env=env, cwd=HERE, stdout=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        stdout, _ = pr.communicate(timeout=args.cpp_timeout)  # stderr streams through
+        rc = pr.returncode
+    except subprocess.TimeoutExpired:
+        os.killpg(pr.pid, 9)
+        stdout, _ = pr.communicate()
+        return {"error": f"bench_summa exceeded {args.cpp_timeout} s (killed)", "fatal": False}
     wall = time.perf_counter() - t0
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    if r.returncode != 0 or not lines:
-        crashed = r.returncode < 0 or r.returncode in (124, 134, 137, 139)
-        return {"error": f"bench_summa rc={r.returncode}: {r.stdout[-2000:]}", "fatal": crashed}
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    if rc != 0 or not lines:
+        crashed = rc < 0 or rc in (124, 134, 137, 139)
+        return {"error": f"bench_summa rc={rc}: {stdout[-2000:]}", "fatal": crashed}
     d = json.loads(lines[-1])
     step_s = d["ms_per_step"] / 1e3
     known = KNOWN_NNZC.get(args.scale)

@@ -234,9 +234,7 @@ int main(int argc, char** argv) {
         SP.reset(new combblas_hip::StagePlans<int64_t, double, double>(
             *A3d->GetLayerMat()->seqptr(), A3d->GetLayerMat()->getcommgrid().get(), *B3d->GetLayerMat()->seqptr(),
             B3d->GetLayerMat()->getcommgrid().get()));
-      const int64_t z = SP->nnz;
-      SP.reset();
-      phases = plan_phases(z);
+      phases = plan_phases(SP->nnz);  // with the plans (and their stored bitmaps) still resident
     }
     if (myrank == 0) std::fprintf(stderr, "[bench_summa] setup %.1f s, %d phase(s); warm-up\n", setup_s, phases);
     for (int w = 0; w < warmup; ++w) product(false);
