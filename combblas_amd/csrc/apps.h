@@ -10,7 +10,8 @@
 //                                                           [SpParMat::Kselect1, SpParMat.cpp:1413-1700]
 //   prune_col_kernel     keep entries !(v < thresh[col])    [Dcsc::PruneColumn, dcsc.cpp:699-760]
 //   colstat_kept_kernel  count / sum of what PruneColumn(thresh) keeps, per column
-//   kselect_cols_kernel  Kselect1 of whole local columns in one launch (LDS-staged radix select)
+//   kselect_wave/block   Kselect1 of whole local columns: a wave / a workgroup per column (keys in
+//                        registers or streamed); kselect_long_* for the longest, chunked
 //
 // Included once by spgemm.hip (one translation unit).
 #pragma once
@@ -669,77 +670,326 @@ __global__ void kselect_value_kernel(int64_t nact, const uint64_t* __restrict__ 
   if (a < nact) out[a] = fval(prefix[a]);
 }
 
-// Kselect1 of whole local columns in one launch: workgroups stride over the column slots, an
-// active column's keys are staged in LDS once (columns up to kSelStage entries; longer ones are
-// re-read from HBM each pass) and the 8 radix passes run on them -- histogram by LDS atomics, the
-// digit holding descending rank r found by one wave (lane l owns bins 255-4l .. 252-4l, a shuffle
-// prefix and a ballot). out[aidx[col]] = the k-th largest value, the smallest when the column has
-// fewer than k entries (active columns without a slot keep the caller's fill).
-constexpr int kSelStage = 4096;
-__global__ __launch_bounds__(256) void kselect_cols_kernel(const int64_t* __restrict__ jc, const int64_t* __restrict__ cp,
+// Kselect1 of whole local columns (the k-th largest value of every active column, the smallest
+// when the column has fewer than k entries): a radix select over order-preserving keys, one
+// launch per column-length class -- a wave per column up to 64*R entries and a workgroup per
+// column up to 256*RB entries, the keys in registers; a workgroup per longer column that streams
+// the keys and moves the candidates left after the first digit into LDS; kselect_long_* for the
+// longest. The 8-bit digits start at the highest bit in which the column's keys differ (a
+// min/max reduction first: the sign and most exponent bits of MCL's probabilities are common to
+// a column, and a digit over them put every key on one bin); bins are per wave; the digit holding
+// descending rank r is found by one wave (lane l owns bins 255-4l .. 252-4l, a shuffle prefix
+// and a ballot); a bin holding a single key ends the select.
+
+__device__ __forceinline__ void sel_minmax_shfl(uint64_t& lo, uint64_t& hi) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+}
+// the digit pick, in every lane of one wave: c[j] = count of bin 255-4*lane-j
+struct SelPick {
+  int d;
+  int64_t r;
+  int one;
+};
+__device__ __forceinline__ SelPick sel_pick(const uint32_t (&c)[4], int64_t r) {
+  const int lane = threadIdx.x & 63;
+  uint32_t sum = c[0] + c[1] + c[2] + c[3];
+  uint32_t incl = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(incl, o);
+    if (lane >= o) incl += t;
+  }
+  const uint64_t m = __ballot((int64_t)incl > r);
+  const int L = __ffsll((long long)m) - 1;
+  int64_t rr = r - (int64_t)(incl - sum);
+  int d = 255 - 4 * lane, one = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (rr < (int64_t)c[j]) {
+      d = 255 - 4 * lane - j;
+      one = c[j] == 1u;
+      break;
+    }
+    rr -= c[j];
+  }
+  return {__shfl(d, L), __shfl(rr, L), __shfl(one, L)};
+}
+// the first digit's position from the keys' min and max: top = highest differing bit, pre = the
+// common bits above it (lo == hi: every key equal, pre = that key and top = -1)
+__device__ __forceinline__ void sel_start(uint64_t lo, uint64_t hi, int& top, uint64_t& pre) {
+  if (lo == hi) {
+    top = -1;
+    pre = lo;
+    return;
+  }
+  top = 63 - __clzll((long long)(lo ^ hi));
+  pre = top >= 63 ? 0ull : (lo & (~0ull << (top + 1)));
+}
+
+// One WAVE per column of at most 64*R entries, the keys held in registers (R per lane, all loads
+// of a column in flight at once), the 256 bins in a per-wave LDS slice.
+template <int R>
+__global__ __launch_bounds__(256) void kselect_wave_kernel(const int64_t* __restrict__ jc, const int64_t* __restrict__ cp,
                                                            const double* __restrict__ num, int64_t nzc,
                                                            const int32_t* __restrict__ aidx, int64_t k,
                                                            double* __restrict__ out) {
-  __shared__ uint64_t keys[kSelStage];
-  __shared__ uint32_t h[256];
-  __shared__ uint64_t s_pre;
-  __shared__ int64_t s_rank;
-  const int tid = threadIdx.x, lane = tid & 63;
+  __shared__ uint32_t hist[4][256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t* h = hist[w];
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  for (int64_t s = (int64_t)blockIdx.x * 4 + w; s < nzc; s += nwaves) {
+    const int32_t ai = aidx[jc[s]];
+    const int64_t p0 = cp[s], n = cp[s + 1] - p0;
+    if (ai < 0 || n <= 0 || n > 64 * R) continue;  // uniform over the wave
+    uint64_t key[R];
+    uint64_t lo = ~0ull, hi = 0ull;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int64_t i = (int64_t)j * 64 + lane;
+      key[j] = i < n ? fkey(num[p0 + i]) : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      if ((int64_t)j * 64 + lane < n) {
+        lo = key[j] < lo ? key[j] : lo;
+        hi = key[j] > hi ? key[j] : hi;
+      }
+    sel_minmax_shfl(lo, hi);
+    int64_t r = (n >= k ? k : n) - 1;
+    int top;
+    uint64_t pre;
+    sel_start(lo, hi, top, pre);
+    while (top >= 0) {
+      const int shift = top >= 7 ? top - 7 : 0;
+      const uint64_t himask = top >= 63 ? 0ull : (~0ull << (top + 1));
+      const uint32_t dmask = (uint32_t)((2u << (top - shift)) - 1u);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) h[lane * 4 + j] = 0u;
+      wave_lds_sync();
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if ((int64_t)j * 64 + lane < n && (key[j] & himask) == pre) atomicAdd(&h[(uint32_t)(key[j] >> shift) & dmask], 1u);
+      wave_lds_sync();
+      uint32_t c[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c[j] = h[255 - 4 * lane - j];
+      const SelPick pk = sel_pick(c, r);
+      wave_lds_sync();  // every lane has read its bins before the next digit clears them
+      pre |= (uint64_t)pk.d << shift;
+      r = pk.r;
+      top = shift - 1;
+      if (pk.one && top >= 0) {  // one key left under the prefix: it is the answer
+        const uint64_t m2 = ~0ull << shift;
+        uint64_t found = 0;
+        bool has = false;
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+          if ((int64_t)j * 64 + lane < n && (key[j] & m2) == pre) {
+            found = key[j];
+            has = true;
+          }
+        pre = __shfl(found, __ffsll((long long)__ballot(has)) - 1);
+        break;
+      }
+    }
+    if (lane == 0) out[ai] = fval(pre);
+  }
+}
+
+// One WORKGROUP of 256 threads per column of min_n < n <= max_n entries.
+// REG (max_n <= 256*R): the keys in registers. Otherwise the keys are streamed (HBM / L2): the
+// min/max and the first digit's histogram take one read each, then the candidates under the first
+// digit move into LDS (one more read) when at most kSelCand of them are left -- the usual case --
+// and the remaining digits run on them; a larger remainder keeps streaming.
+constexpr int kSelCand = 4096;
+template <int R, bool REG>
+__global__ __launch_bounds__(256) void kselect_block_kernel(const int64_t* __restrict__ jc, const int64_t* __restrict__ cp,
+                                                            const double* __restrict__ num, int64_t nzc,
+                                                            const int32_t* __restrict__ aidx, int64_t k,
+                                                            double* __restrict__ out, int64_t min_n, int64_t max_n) {
+  constexpr int RK = REG ? R : 1;
+  __shared__ uint64_t cand[REG ? 1 : kSelCand];
+  __shared__ uint32_t h[4][256];
+  __shared__ uint64_t s_mm[2][4];
+  __shared__ uint64_t s_key;
+  __shared__ int s_d, s_one;
+  __shared__ uint32_t s_nc;
+  __shared__ int64_t s_r;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int64_t s = blockIdx.x; s < nzc; s += gridDim.x) {
     const int32_t ai = aidx[jc[s]];
     const int64_t p0 = cp[s], n = cp[s + 1] - p0;
-    if (ai < 0 || n <= 0) continue;  // uniform over the workgroup
-    const bool staged = n <= kSelStage;
-    if (staged)
-      for (int64_t i = tid; i < n; i += 256) keys[i] = fkey(num[p0 + i]);
-    int64_t r = (n >= k ? k : n) - 1;
-    uint64_t pre = 0;
-    for (int shift = 56; shift >= 0; shift -= 8) {
-      h[tid] = 0u;
-      __syncthreads();
-      const uint64_t himask = shift >= 56 ? 0ull : (~0ull << (shift + 8));
-      for (int64_t i = tid; i < n; i += 256) {
-        const uint64_t key = staged ? keys[i] : fkey(num[p0 + i]);
-        if ((key & himask) == pre) atomicAdd(&h[(key >> shift) & 255u], 1u);
+    if (ai < 0 || n <= min_n || n > max_n) continue;  // uniform over the workgroup
+    uint64_t key[RK];
+    int64_t nk = n;       // keys in the current source
+    int src = REG ? 0 : 1;  // 0 registers, 1 HBM stream, 2 LDS candidates
+    if (REG) {
+#pragma unroll
+      for (int j = 0; j < RK; ++j) {
+        const int64_t i = (int64_t)j * 256 + tid;
+        key[j] = i < n ? fkey(num[p0 + i]) : 0ull;
       }
+    }
+    // f(key) over this thread's valid keys of the current source
+    auto each = [&](auto&& f) {
+      if (src == 0) {
+#pragma unroll
+        for (int j = 0; j < RK; ++j)
+          if ((int64_t)j * 256 + tid < nk) f(key[j]);
+      } else if (src == 1) {
+        for (int64_t i = tid; i < nk; i += 256) f(fkey(num[p0 + i]));
+      } else {
+        for (int64_t i = tid; i < nk; i += 256) f(cand[i]);
+      }
+    };
+    uint64_t lo = ~0ull, hi = 0ull;
+    each([&](uint64_t x) {
+      lo = x < lo ? x : lo;
+      hi = x > hi ? x : hi;
+    });
+    sel_minmax_shfl(lo, hi);
+    if (lane == 0) {
+      s_mm[0][w] = lo;
+      s_mm[1][w] = hi;
+    }
+    __syncthreads();
+    lo = s_mm[0][0];
+    hi = s_mm[1][0];
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      lo = s_mm[0][j] < lo ? s_mm[0][j] : lo;
+      hi = s_mm[1][j] > hi ? s_mm[1][j] : hi;
+    }
+    int64_t r = (n >= k ? k : n) - 1;
+    int top;
+    uint64_t pre;
+    sel_start(lo, hi, top, pre);
+    while (top >= 0) {
+      const int shift = top >= 7 ? top - 7 : 0;
+      const uint64_t himask = top >= 63 ? 0ull : (~0ull << (top + 1));
+      const uint32_t dmask = (uint32_t)((2u << (top - shift)) - 1u);
+      h[0][tid] = h[1][tid] = h[2][tid] = h[3][tid] = 0u;
+      __syncthreads();
+      each([&](uint64_t x) {
+        if ((x & himask) == pre) atomicAdd(&h[w][(uint32_t)(x >> shift) & dmask], 1u);
+      });
       __syncthreads();
       if (tid < 64) {
-        uint32_t c[4], sum = 0;
+        uint32_t c[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          c[j] = h[255 - 4 * lane - j];
-          sum += c[j];
+          const int b = 255 - 4 * lane - j;
+          c[j] = h[0][b] + h[1][b] + h[2][b] + h[3][b];
         }
-        uint32_t incl = sum;
+        const SelPick pk = sel_pick(c, r);
+        if (lane == 0) {
+          s_d = pk.d;
+          s_r = pk.r;
+          s_one = pk.one;
+        }
+        // the chosen bin's count, for the move into LDS
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t t = __shfl_up(incl, o);
-          if (lane >= o) incl += t;
-        }
-        const uint64_t m = __ballot((int64_t)incl > r);
-        const int L = __ffsll((long long)m) - 1;
-        if (lane == L) {
-          int64_t rr = r - (int64_t)(incl - sum);
-          int d = 255 - 4 * lane;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if (rr < (int64_t)c[j]) {
-              d = 255 - 4 * lane - j;
-              break;
-            }
-            rr -= c[j];
-          }
-          s_pre = pre | ((uint64_t)d << shift);
-          s_rank = rr;
-        }
+        for (int j = 0; j < 4; ++j)
+          if (255 - 4 * lane - j == pk.d) s_nc = c[j];
       }
       __syncthreads();
-      pre = s_pre;
-      r = s_rank;
+      pre |= (uint64_t)s_d << shift;
+      r = s_r;
+      top = shift - 1;
+      const uint64_t m2 = ~0ull << shift;
+      if (s_one && top >= 0) {  // one key left under the prefix: it is the answer
+        each([&](uint64_t x) {
+          if ((x & m2) == pre) s_key = x;
+        });
+        __syncthreads();
+        pre = s_key;
+        break;
+      }
+      if (!REG && src == 1 && top >= 0 && s_nc <= (uint32_t)kSelCand) {  // candidates -> LDS
+        const uint32_t nc = s_nc;
+        __syncthreads();  // s_nc read by every thread before it is reused as the fill counter
+        if (tid == 0) s_nc = 0;
+        __syncthreads();
+        each([&](uint64_t x) {
+          if ((x & m2) == pre) cand[atomicAdd(&s_nc, 1u)] = x;
+        });
+        __syncthreads();
+        src = 2;
+        nk = nc;
+      }
     }
     if (tid == 0) out[ai] = fval(pre);
     __syncthreads();
   }
+}
+
+// The longest columns (a near-dense column of an MCL iterate can hold millions of entries, which
+// one workgroup would stream alone for every round): every such column is cut into chunks of
+// kSelChunk entries, each radix pass runs
+// over all chunks of all long columns at once (LDS histogram per chunk, added to the column's
+// global 256 bins), and kselect_pick_kernel picks the digit per column between passes.
+constexpr int kSelChunk = 8192;
+__global__ void kselect_long_flag_kernel(const int64_t* __restrict__ jc, const int64_t* __restrict__ cp, int64_t nzc,
+                                         const int32_t* __restrict__ aidx, int64_t min_n, int64_t* __restrict__ flag) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > nzc) return;
+  flag[s] = (s < nzc && aidx[jc[s]] >= 0 && cp[s + 1] - cp[s] > min_n) ? 1 : 0;
+}
+// list[l] = slot of long column l; nch[l] = its chunk count; rank / prefix initialised
+__global__ void kselect_long_list_kernel(const int64_t* __restrict__ cp, int64_t nzc, const int64_t* __restrict__ flag,
+                                         const int64_t* __restrict__ pos, int64_t k, int64_t* __restrict__ list,
+                                         int64_t* __restrict__ nch, int64_t* __restrict__ rank,
+                                         uint64_t* __restrict__ prefix) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nzc || !flag[s]) return;
+  const int64_t l = pos[s], n = cp[s + 1] - cp[s];
+  list[l] = s;
+  nch[l] = (n + kSelChunk - 1) / kSelChunk;
+  rank[l] = (n >= k ? k : n) - 1;
+  prefix[l] = 0;
+}
+__global__ void kselect_long_map_kernel(int64_t nl, const int64_t* __restrict__ nch, const int64_t* __restrict__ cpos,
+                                        int32_t* __restrict__ map) {
+  const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= nl) return;
+  for (int64_t c = 0; c < nch[l]; ++c) map[cpos[l] + c] = (int32_t)l;
+}
+__global__ __launch_bounds__(256) void kselect_long_hist_kernel(const int64_t* __restrict__ cp,
+                                                                const double* __restrict__ num,
+                                                                const int64_t* __restrict__ list,
+                                                                const int64_t* __restrict__ cpos,
+                                                                const int32_t* __restrict__ map, int64_t nchunks,
+                                                                const uint64_t* __restrict__ prefix, int shift,
+                                                                uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[256];
+  const int tid = threadIdx.x;
+  const uint64_t himask = shift >= 56 ? 0ull : (~0ull << (shift + 8));
+  for (int64_t g = blockIdx.x; g < nchunks; g += gridDim.x) {
+    const int32_t l = map[g];
+    const int64_t s = list[l], c = g - cpos[l];
+    const int64_t p1 = cp[s + 1], b0 = cp[s] + c * kSelChunk, b1 = b0 + kSelChunk < p1 ? b0 + kSelChunk : p1;
+    const uint64_t pre = prefix[l];
+    h[tid] = 0u;
+    __syncthreads();
+    for (int64_t p = b0 + tid; p < b1; p += 256) {
+      const uint64_t key = fkey(num[p]);
+      if ((key & himask) == pre) atomicAdd(&h[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (h[tid]) atomicAdd(&hist[(int64_t)l * 256 + tid], h[tid]);
+    __syncthreads();
+  }
+}
+__global__ void kselect_long_out_kernel(int64_t nl, const int64_t* __restrict__ list, const int64_t* __restrict__ jc,
+                                        const int32_t* __restrict__ aidx, const uint64_t* __restrict__ prefix,
+                                        double* __restrict__ out) {
+  const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l < nl) out[aidx[jc[list[l]]]] = fval(prefix[l]);
 }
 
 // keep entry (i, col) iff !(v < thresh[col]): pass 1 counts per slot, pass 2 copies

@@ -2876,13 +2876,65 @@ int cbh_kselect_cols(cbh_ctx* ctx, const cbh_mat* A, const int32_t* active_index
   if (k < 1) return fail(ctx, CBH_E_ARG, "k must be >= 1");
   if (nactive <= 0) return CBH_OK;
   if (!active_index || !out) return fail(ctx, CBH_E_ARG, "null argument");
-  if (A->nzc > 0) {
-    const int64_t grid = A->nzc < 8192 ? A->nzc : 8192;  // workgroups stride over the slots
-    hipLaunchKernelGGL(kselect_cols_kernel, dim3((unsigned)grid), dim3(256), 0, ctx->stream, A->jc, A->cp,
-                       reinterpret_cast<const double*>(A->num), A->nzc, active_index, k, out);
-    CBH_HIP(ctx, hipGetLastError());
+  const int64_t nzc = A->nzc;
+  if (nzc <= 0) return CBH_OK;
+  const double* num = reinterpret_cast<const double*>(A->num);
+  // columns of <= 64*R entries: a wave each (keys in registers); <= 256*RB: a workgroup each (keys
+  // in registers); <= kSelLong: a workgroup each streaming the keys every round
+  constexpr int R = 48, RB = 32;
+  constexpr int64_t kSelLong = 1 << 17;
+  const int64_t wgrid = std::min<int64_t>((nzc + 3) / 4, 16384);
+  hipLaunchKernelGGL(kselect_wave_kernel<R>, dim3((unsigned)wgrid), dim3(256), 0, ctx->stream, A->jc, A->cp, num, nzc,
+                     active_index, k, out);
+  const int64_t grid = std::min<int64_t>(nzc, 8192);  // workgroups stride over the slots
+  hipLaunchKernelGGL((kselect_block_kernel<RB, true>), dim3((unsigned)grid), dim3(256), 0, ctx->stream, A->jc, A->cp,
+                     num, nzc, active_index, k, out, (int64_t)64 * R, (int64_t)256 * RB);
+  hipLaunchKernelGGL((kselect_block_kernel<1, false>), dim3((unsigned)grid), dim3(256), 0, ctx->stream, A->jc, A->cp,
+                     num, nzc, active_index, k, out, (int64_t)256 * RB, kSelLong);
+  CBH_HIP(ctx, hipGetLastError());
+  // longer columns: chunked over workgroups, 8 radix passes with per-column global histograms
+  Scratch S(ctx);
+  int64_t *flag, *pos;
+  CBH_TRY(S.get(&flag, nzc + 1));
+  CBH_TRY(S.get(&pos, nzc + 1));
+  hipLaunchKernelGGL(kselect_long_flag_kernel, dim3(blocks_for(nzc + 1, 256)), dim3(256), 0, ctx->stream, A->jc, A->cp,
+                     nzc, active_index, kSelLong, flag);
+  CBH_TRY(exclusive_scan_i64(ctx, S, flag, pos, nzc + 1));
+  int64_t nl = 0;
+  CBH_HIP(ctx, hipMemcpyAsync(&nl, pos + nzc, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (nl == 0) return CBH_OK;
+  int64_t *list, *nch, *cpos, *rank;
+  uint64_t* prefix;
+  uint32_t* hist;
+  CBH_TRY(S.get(&list, nl));
+  CBH_TRY(S.get(&nch, nl + 1));
+  CBH_TRY(S.get(&cpos, nl + 1));
+  CBH_TRY(S.get(&rank, nl));
+  CBH_TRY(S.get(&prefix, nl));
+  CBH_TRY(S.get(&hist, 256 * nl));
+  CBH_HIP(ctx, hipMemsetAsync(nch + nl, 0, sizeof(int64_t), ctx->stream));
+  hipLaunchKernelGGL(kselect_long_list_kernel, dim3(blocks_for(nzc, 256)), dim3(256), 0, ctx->stream, A->cp, nzc, flag,
+                     pos, k, list, nch, rank, prefix);
+  CBH_TRY(exclusive_scan_i64(ctx, S, nch, cpos, nl + 1));
+  int64_t nchunks = 0;
+  CBH_HIP(ctx, hipMemcpyAsync(&nchunks, cpos + nl, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  int32_t* map;
+  CBH_TRY(S.get(&map, nchunks));
+  hipLaunchKernelGGL(kselect_long_map_kernel, dim3(blocks_for(nl, 256)), dim3(256), 0, ctx->stream, nl, nch, cpos, map);
+  const unsigned hgrid = (unsigned)std::min<int64_t>(nchunks, 16384);
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    CBH_HIP(ctx, hipMemsetAsync(hist, 0, sizeof(uint32_t) * 256 * (size_t)nl, ctx->stream));
+    hipLaunchKernelGGL(kselect_long_hist_kernel, dim3(hgrid), dim3(256), 0, ctx->stream, A->cp, num, list, cpos, map,
+                       nchunks, prefix, shift, hist);
+    hipLaunchKernelGGL(kselect_pick_kernel, dim3(blocks_for(nl, 256)), dim3(256), 0, ctx->stream, nl, hist, prefix, rank,
+                       shift);
   }
-  return CBH_OK;
+  hipLaunchKernelGGL(kselect_long_out_kernel, dim3(blocks_for(nl, 256)), dim3(256), 0, ctx->stream, nl, list, A->jc,
+                     active_index, prefix, out);
+  CBH_HIP(ctx, hipGetLastError());
+  return CBH_OK;  // (the scratch returns to the stream-ordered cache)
 }
 
 static int prune_columns_impl(cbh_ctx* ctx, const cbh_mat* A, const double* thresh, cbh_arena* ar, cbh_mat** C);

@@ -229,13 +229,17 @@ def test_kselect_edge_cases(ctx):
     rng = np.random.default_rng(1)
     cols = [[3.0, 1.0, 2.0], [5.0, 5.0, 5.0, 1.0], [-1.0, -7.5, 0.0, -0.0, 2.5], [4.0], [], [9.0, 8.0],
             list(rng.standard_normal(3000)), list(rng.standard_normal(5000)),  # LDS-staged / re-read from HBM
-            list(np.round(rng.standard_normal(6000), 1))]  # many ties
+            list(np.round(rng.standard_normal(6000), 1)),  # many ties
+            list(rng.uniform(0.001, 0.01, 2500)),  # common sign/exponent bits (the digits start below them)
+            [1.0, np.nextafter(1.0, 2.0), 1.0, np.nextafter(1.0, 2.0), np.nextafter(1.0, 0.0)],  # last-bit keys
+            list(rng.uniform(0.0, 1.0, 9000)),  # 1024-thread workgroup
+            list(np.round(rng.uniform(0.0, 1.0, 40000), 3))]  # chunked over workgroups (ties too)
     rows, cc, vv = [], [], []
     for j, c in enumerate(cols):
         rows += list(range(len(c)))
         cc += [j] * len(c)
         vv += c
-    d = H.Dcsc.from_coo(8000, len(cols), np.array(rows), np.array(cc), np.array(vv, np.float64))
+    d = H.Dcsc.from_coo(40000, len(cols), np.array(rows), np.array(cc), np.array(vv, np.float64))
     dA = _dev(ctx, d)
 
     class MultiPass:  # the backend without the one-launch select: the per-pass histogram path
@@ -248,8 +252,9 @@ def test_kselect_edge_cases(ctx):
             return getattr(self.be, name)
 
     for be in (HipBackend(ctx), MultiPass(HipBackend(ctx))):
-        for k in (1, 2, 3, 5, 100, 4500, 7000):
-            active = torch.tensor([True, True, True, True, True, False, True, True, True], device=ctx.tdevice)
+        for k in (1, 2, 3, 5, 100, 4500, 7000, 8500, 39000):
+            active = torch.tensor([True, True, True, True, True, False, True, True, True, True, True, True, True],
+                                  device=ctx.tdevice)
             got = pf.Kselect(be, dA, active, k).cpu().numpy()
             for j, c in enumerate(cols):
                 if not bool(active[j]):
