@@ -32,11 +32,11 @@ template <typename IT, typename NT>
 void SUMMALayer(combblas_hip::SpDCColsDev<IT, NT>& SplitA, combblas_hip::SpDCColsDev<IT, NT>& SplitB,
                 std::vector<combblas_hip::SpDCColsDev<IT, NT>*>& C, CCGrid& CMG, bool isBT, bool threaded) {
   typedef PlusTimesSRing<NT, NT> PTNN;
-  (void)threaded;  // both of the reference's local kernels give the same product
-  if (isBT) {
-    std::fprintf(stderr, "combblas_hip: SUMMALayer on device blocks takes B untransposed (isBT = false)\n");
-    MPI_Abort(MPI_COMM_WORLD, CBH_E_ARG);
-  }
+  // the outer-product mode (mpipspgemm.cpp:176-179: SplitB locally transposed, threaded = false ->
+  // MultiplyReturnTuples(A, B, false, isBT), SUMMALayer.h:80-86): every received B block is
+  // transposed back on the device (cbh_transpose) and the product runs as in the threaded mode;
+  // with threaded = true the reference's LocalSpGEMM ignores isBT, and so does this overload
+  const bool transposeB = isBT && !threaded;
   const int stages = CMG.GridCols;
   auto Asizes = combblas_hip::GetSetSizes(SplitA, CMG.rowWorld);
   auto Bsizes = combblas_hip::GetSetSizes(SplitB, CMG.colWorld);
@@ -51,7 +51,16 @@ void SUMMALayer(combblas_hip::SpDCColsDev<IT, NT>& SplitA, combblas_hip::SpDCCol
     combblas_hip::hip_check(hipStreamSynchronize(reinterpret_cast<hipStream_t>(cbh_ctx_stream(combblas_hip::context()))), "hipStreamSynchronize");
     comm_bcast += MPI_Wtime() - bcast_beg;
     const double summa_beg = MPI_Wtime();
-    cbh_mat* Ci = combblas_hip::local_multiply<PTNN, NT, NT, NT>(Ai.mat(), Bi.mat());
+    cbh_mat* Ci;
+    if (transposeB) {
+      cbh_mat* Bt = nullptr;
+      const int rc = cbh_transpose(combblas_hip::context(), Bi.mat(), &Bt);
+      if (rc != CBH_OK) combblas_hip::die(combblas_hip::context(), rc, "cbh_transpose");
+      Ci = combblas_hip::local_multiply<PTNN, NT, NT, NT>(Ai.mat(), Bt);
+      cbh_mat_free(combblas_hip::context(), Bt);
+    } else {
+      Ci = combblas_hip::local_multiply<PTNN, NT, NT, NT>(Ai.mat(), Bi.mat());
+    }
     comp_summa += MPI_Wtime() - summa_beg;
     C.push_back(new combblas_hip::SpDCColsDev<IT, NT>(Ci));  // received blocks are freed with Arecv / Brecv
   }

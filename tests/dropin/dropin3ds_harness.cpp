@@ -14,7 +14,10 @@
 // Every rank prints an order-sensitive digest of its block of C; tests/test_dropin3d_gpu.py
 // compares the binaries rank by rank (a third, oracle/_ref/devpath3ds_harness, -DCBH_DEVPATH, runs
 // the device-resident overloads of the same layer, see below). Values are edge multiplicities: every double sum is exact.
-//   mpirun -np P dropin3ds_harness <scale> <layers>   (P / layers a square: 1x1xc or 2x2xc)
+//   mpirun -np P dropin3ds_harness <scale> <layers> [bt]   (P / layers a square: 1x1xc or 2x2xc)
+// bt: mpipspgemm.cpp's outer-product case (:176-179): splitB transposed locally, multiply(splitA,
+// splitB, CMG, true, false) -- the reference's MultiplyReturnTuples(..., isBT) stock, the device
+// overload's transpose-back on the device with -DCBH_DEVPATH.
 #include <mpi.h>
 
 #include <cmath>
@@ -89,6 +92,7 @@ int main(int argc, char** argv) {
   MPI_Init_thread(&argc, &argv, MPI_THREAD_SERIALIZED, &provided);
   const int scale = argc > 1 ? std::atoi(argv[1]) : 10;
   const int layers = argc > 2 ? std::atoi(argv[2]) : 2;
+  const bool bt = argc > 3 && std::strcmp(argv[3], "bt") == 0;
   int nprocs, myrank;
   MPI_Comm_size(MPI_COMM_WORLD, &nprocs);
   MPI_Comm_rank(MPI_COMM_WORLD, &myrank);
@@ -107,21 +111,22 @@ int main(int argc, char** argv) {
     SplitMat(CMG, B, splitB, true);  // row split
     delete A;
     delete B;
+    if (bt) splitB.Transpose();  // locally transposed for the outer product
 #ifdef CBH_DEVPATH
     combblas_hip::SpDCColsDev<int64_t, double> dA(splitA), dB(splitB);
-    delete multiply(dA, dB, CMG, false, true);  // first call: HIP context, code objects, communicators
+    delete multiply(dA, dB, CMG, bt, !bt);  // first call: HIP context, code objects, communicators
     MPI_Barrier(MPI_COMM_WORLD);
     const double t0 = MPI_Wtime();
-    combblas_hip::SpDCColsDev<int64_t, double>* Cd = multiply(dA, dB, CMG, false, true);
+    combblas_hip::SpDCColsDev<int64_t, double>* Cd = multiply(dA, dB, CMG, bt, !bt);
     const double t1 = MPI_Wtime();
     DCols* C = Cd->to_host();
     delete Cd;
 #else
-    DCols* C = multiply(splitA, splitB, CMG, false, true);  // first call: HIP context, code objects
+    DCols* C = multiply(splitA, splitB, CMG, bt, !bt);  // first call: HIP context, code objects
     delete C;
     MPI_Barrier(MPI_COMM_WORLD);
     const double t0 = MPI_Wtime();
-    C = multiply(splitA, splitB, CMG, false, true);
+    C = multiply(splitA, splitB, CMG, bt, !bt);
     const double t1 = MPI_Wtime();
 #endif
     const uint64_t dg = block_digest(*C);

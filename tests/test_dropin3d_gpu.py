@@ -36,9 +36,9 @@ DEV3DS = os.path.join(H.REPO, "oracle", "_ref", "dropin3ds_harness")
 STOCK3DS = os.path.join(H.REPO, "oracle", "_ref", "stock3ds_harness")
 
 
-def _blocks(binary, ranks, layers, scale):
-    r = subprocess.run(["/opt/conda/bin/mpirun", "-np", str(ranks), binary, str(scale), str(layers)], env=ENV,
-                       capture_output=True, text=True, timeout=170, cwd="/tmp")
+def _blocks(binary, ranks, layers, scale, mode=None, env=None):
+    cmd = ["/opt/conda/bin/mpirun", "-np", str(ranks), binary, str(scale), str(layers)] + ([mode] if mode else [])
+    r = subprocess.run(cmd, env=env or ENV, capture_output=True, text=True, timeout=170, cwd="/tmp")
     out = r.stdout + r.stderr
     assert r.returncode == 0, out
     blocks = sorted(l.split()[1:] for l in out.splitlines() if l.startswith("BLOCK3DS "))
@@ -82,3 +82,21 @@ def test_device_resident_standalone_3d_layer(ranks, layers):
     stock, tot_stock = _blocks(STOCK3DS, ranks, layers, 11)
     assert dev == stock, (dev, stock)
     print(f"DEVPATH3DSTANDALONE {tot_stock.split()[1]} OK {tot_stock.split()[2]} ranks={ranks}")
+
+
+@pytest.mark.parametrize("ranks,layers", [(1, 1), (2, 2), (4, 1)])
+def test_device_resident_outer_product_mode(ranks, layers):
+    """mpipspgemm.cpp's outer-product case (:176-179): splitB transposed locally and
+    multiply(splitA, splitB, CMG, isBT = true, threaded = false). The device SUMMALayer transposes
+    every received B block back on the device (cbh_transpose) where the reference calls
+    MultiplyReturnTuples(..., isBT): every rank's block of C equals the stock layer's in the same
+    mode (which equals the column-threaded mode's)."""
+    for b in (DEVPATH3DS, STOCK3DS):
+        assert os.path.exists(b), f"{b} missing: run __graft_entry__.build() with the reference"
+    env = dict(ENV, COMBBLAS_HIP_COMM="mpi") if ranks > 1 else ENV
+    dev, _ = _blocks(DEVPATH3DS, ranks, layers, 11, "bt", env)
+    stock_bt, tot = _blocks(STOCK3DS, ranks, layers, 11, "bt")
+    stock, _ = _blocks(STOCK3DS, ranks, layers, 11)
+    assert stock_bt == stock
+    assert dev == stock_bt, (dev, stock_bt)
+    print(f"DEVPATH3DSBT {tot.split()[1]} OK {tot.split()[2]} ranks={ranks}")
