@@ -29,6 +29,11 @@
 // Columns with more than EMAX entries are processed in entry chunks whose cursors live in HBM
 // between sub-tiles (double-buffered, so that a retried sub-tile restarts from committed ones).
 #pragma once
+
+// CBH_GATHER_PIN (default 1): pin the window gathers before the updates (sweep() below)
+#ifndef CBH_GATHER_PIN
+#define CBH_GATHER_PIN 1
+#endif
 #include "block_ops.h"
 
 namespace cbh {
@@ -726,6 +731,10 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
       CBH_STAMP(4);
       if (__hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
       // branch-free gather: lanes past the window re-read product 0 and are masked afterwards
+#if CBH_GATHER_PIN
+      a_t ar[U];  // numeric: A's value of each product; the multiply waits until all U are loaded
+      int oi[U];
+#endif
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int x0 = tid + u * BS;
@@ -736,9 +745,36 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
         if constexpr (NUM && MERGE) {
           if (with_vals) av[u] = valsA[q + s_vdelta[i]];
         } else if constexpr (NUM) {
+#if CBH_GATHER_PIN
+          if (with_vals) {
+            ar[u] = reinterpret_cast<const a_t*>(a.Anum)[q];
+            oi[u] = i;
+          }
+#else
           if (with_vals) av[u] = SR::multiply(reinterpret_cast<const a_t*>(a.Anum)[q], escale[i]);
+#endif
         }
       }
+#if CBH_GATHER_PIN
+      // every gathered row and value is materialised here, after all U gathers were issued, and
+      // the multiplies follow: otherwise the compiler sinks product 0's value load into upd's
+      // bounds-checked branch behind a vmcnt(0) for its row (two dependent HBM round trips per
+      // window), or, with a multiply right after each load, waits out each load in turn
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        asm volatile("" ::"v"(r[u]));
+        if constexpr (NUM && MERGE && std::is_arithmetic<val_t>::value && (sizeof(val_t) == 4 || sizeof(val_t) == 8))
+          if (with_vals) asm volatile("" ::"v"(av[u]));
+        if constexpr (NUM && !MERGE && std::is_arithmetic<a_t>::value && (sizeof(a_t) == 4 || sizeof(a_t) == 8))
+          if (with_vals) asm volatile("" ::"v"(ar[u]));
+      }
+      if constexpr (NUM && !MERGE) {
+        if (with_vals) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) av[u] = SR::multiply(ar[u], escale[oi[u]]);
+        }
+      }
+#endif
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (tid + u * BS < wn) upd(u);
