@@ -24,7 +24,8 @@ MODES = {0: "sym", 1: "num", 2: "dense"}
 
 def bin_of(name):
     if "dense_kernel<" in name:  # device/dense_kernel.h (round 5): numeric dense / symbolic bitmap
-        kind = name.split("dense_kernel<")[1].split(">")[0].split(",")[-1].strip()
+        m = re.search(r"dense_kernel<.*, (\d+)>", name.split("(")[0])
+        kind = m.group(1) if m else "?"
         return {"0": "num_dense", "1": "sym_bmp", "2": "num_large"}.get(kind, "dense_" + kind)
     m = PAT.search(name)
     if not m:
