@@ -911,7 +911,13 @@ static double phase_frac() {
 }
 // compression ratio (quarters) a dense candidate's flops are divided by before the dense test
 // (5/4, 6/4, 8/4 and 12/4 measured flat or slower than 4/4)
-constexpr int64_t kBmpCr4 = 4;
+static int64_t bmp_cr4() {  // CBH_BMP_CR4 overrides (A/B)
+  static int64_t v = [] {
+    const char* e = std::getenv("CBH_BMP_CR4");
+    return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(4);
+  }();
+  return v;
+}
 static double bmp_frac() {
   static double v = [] {
     const char* e = std::getenv("CBH_BMP_FRAC");
@@ -1170,7 +1176,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
     CBH_HIP(ctx, hipMemsetAsync(cw, 0, sizeof(unsigned long long) * kBmpClasses, ctx->stream));
     hipLaunchKernelGGL(bmp_count_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.twork, P.tlo, P.thi,
                        P.ntasks, kSplitHashT, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSymMidCap, (int64_t)kDRatio4,
-                       kBmpCr4, 0, bw, cw);
+                       bmp_cr4(), 0, bw, cw);
     CBH_HIP(ctx, hipGetLastError());
     unsigned long long hc[kBmpClasses];
     CBH_HIP(ctx, hipMemcpyAsync(hc, cw, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream));
@@ -1187,7 +1193,7 @@ static int run_symbolic(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_ma
     if (min_class > 0 && words > 0)  // drop the classes that did not fit
       hipLaunchKernelGGL(bmp_count_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, ctx->stream, P.twork, P.tlo, P.thi,
                          P.ntasks, kSplitHashT, (int64_t)CD::CAPD, (int64_t)CD::NWB, kSymMidCap, (int64_t)kDRatio4,
-                         kBmpCr4, min_class, bw, nullptr);
+                         bmp_cr4(), min_class, bw, nullptr);
     CBH_HIP(ctx, hipMemsetAsync(bw + P.ntasks, 0, sizeof(int64_t), ctx->stream));
     CBH_TRY(exclusive_scan_i64(ctx, S, bw, P.boff, P.ntasks + 1));
     if (words > 0) CBH_TRY(S.get(&P.bmp, (size_t)words));
