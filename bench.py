@@ -273,8 +273,10 @@ def host_flops(A):
     return int(np.dot(colnnz, rownnz))
 
 
-CPP_BENCH = os.path.join(HERE, "cxx", "_build", "bench_summa")
-MPIRUN = "/opt/conda/bin/mpirun"
+# (CBH_BENCH_SUMMA / CBH_MPIRUN: test hooks, tests/test_bench_launcher.py runs the launcher on CPU
+# with a stand-in binary)
+CPP_BENCH = os.environ.get("CBH_BENCH_SUMMA", os.path.join(HERE, "cxx", "_build", "bench_summa"))
+MPIRUN = os.environ.get("CBH_MPIRUN", "/opt/conda/bin/mpirun")
 KNOWN_NNZC = {22: 24766243778, 20: 3284757756, 18: 425342972, 16: 53638834, 14: 6471508}
 
 
