@@ -230,10 +230,21 @@ inline cbh_mat* fiber_reduce_scatter(cbh_semiring sr, cbh_mat* P, const std::vec
 
 // The SUMMA stage pairs of C = A * B for a phase loop. The reference re-broadcasts the stage blocks
 // and re-multiplies them in every phase (ParFriends.h:560-669 inside its phase loop); here every
-// stage block is broadcast ONCE and kept in HBM, and each stage pair gets ONE symbolic pass
-// (cbh_plan_create), so a phase runs only the numeric pass of its columns (cbh_plan_spgemm_slots)
-// and the memory model reads the exact per-stage nnz off the plans instead of a separate
-// EstPerProcessNnzSUMMA pass.
+// stage block is broadcast ONCE and kept in HBM. Default (round 5): the stages' blocks are then
+// concatenated into this rank's strips A(r, :) = [A_0 ... A_{s-1}] and B(:, c) = [B_0; ...; B_{s-1}]
+// and planned as ONE product -- sum_i A_i B_i in one pass, no stage partial written and no
+// MultiwayMerge (the Python drivers' form; C is the same matrix, f64 sums in
+// another order). COMBBLAS_HIP_STAGE_PLANS=per-stage keeps one plan per stage pair and merges the
+// stage partials per phase, as the reference does. Either way a phase runs only the numeric pass of
+// its columns (cbh_plan_spgemm_slots) and the memory model reads the exact nnz off the plans
+// instead of a separate EstPerProcessNnzSUMMA pass.
+inline bool per_stage_plans() {
+  static const bool v = [] {
+    const char* e = std::getenv("COMBBLAS_HIP_STAGE_PLANS");
+    return e && std::strcmp(e, "per-stage") == 0;
+  }();
+  return v;
+}
 template <class IU, class NU1, class NU2>
 class StagePlans {
  public:
@@ -244,9 +255,12 @@ class StagePlans {
     auto Asizes = GetSetSizes(Aloc, GA->GetRowWorld());
     auto Bsizes = GetSetSizes(Bloc, GB->GetColWorld());
     const int Aself = GA->GetRankInProcRow(), Bself = GB->GetRankInProcCol();
-    // every stage's plan stays resident through the phase loop: their stored dense-task bitmaps
-    // share ONE budget (0.4 of the device) instead of taking up to 0.4 each
-    if (stages > 1) cbh_ctx_set_bitmap_fraction(context(), 0.4 / stages);
+    const bool concat = stages > 1 && !per_stage_plans();
+    // per-stage plans stay resident through the phase loop: their stored dense-task bitmaps share
+    // ONE budget (0.4 of the device) instead of taking up to 0.4 each
+    if (stages > 1 && !concat) cbh_ctx_set_bitmap_fraction(context(), 0.4 / stages);
+    std::vector<SpDCColsDev<IU, NU1>*> As;
+    std::vector<SpDCColsDev<IU, NU2>*> Bs;
     for (int i = 0; i < stages; ++i) {
       SpDCColsDev<IU, NU1>* Ai = &Aloc;
       SpDCColsDev<IU, NU2>* Bi = &Bloc;
@@ -260,22 +274,42 @@ class StagePlans {
       }
       BCastMatrix(GridC->GetRowWorld(), *Ai, Asizes[i], i);
       BCastMatrix(GridC->GetColWorld(), *Bi, Bsizes[i], i);
-      cbh_plan* p = nullptr;
-      std::vector<int64_t> jc;
-      if (Ai->getnnz() > 0 && Bi->getnnz() > 0) {
-        int rc = cbh_plan_create(context(), Ai->mat(), Bi->mat(), &p);
-        if (rc != CBH_OK) die(context(), rc, "cbh_plan_create");
-        int64_t f = 0, z = 0;
-        cbh_plan_info(p, &f, &z);
-        nnz += z;
-        jc.resize((size_t)Bi->getnzc());
-        rc = cbh_mat_copy_out(context(), Bi->mat(), nullptr, jc.data(), nullptr, nullptr, 0);
-        if (rc != CBH_OK) die(context(), rc, "cbh_mat_copy_out");
+      if (concat) {
+        As.push_back(Ai);
+        Bs.push_back(Bi);
+      } else {
+        add_plan(*Ai, *Bi);
       }
-      plans.push_back(p);
-      bjc.push_back(std::move(jc));
     }
-    if (stages > 1) cbh_ctx_set_bitmap_fraction(context(), -1.0);
+    if (concat) {
+      // A strip: the stage blocks side by side; B strip: stacked, as the transpose of the side-by-side
+      // transposes (rows stay ascending in every column)
+      std::vector<const cbh_mat*> ap;
+      for (auto* a : As) ap.push_back(a->mat());
+      cbh_mat* ac = nullptr;
+      int rc = cbh_mat_col_concat(context(), (int)ap.size(), ap.data(), &ac);
+      if (rc != CBH_OK) die(context(), rc, "cbh_mat_col_concat");
+      Acat.reset(new SpDCColsDev<IU, NU1>(ac));
+      std::vector<cbh_mat*> bt;
+      for (auto* b : Bs) {
+        cbh_mat* t = nullptr;
+        rc = cbh_transpose(context(), b->mat(), &t);
+        if (rc != CBH_OK) die(context(), rc, "cbh_transpose");
+        bt.push_back(t);
+      }
+      cbh_mat *btc = nullptr, *bc = nullptr;
+      rc = cbh_mat_col_concat(context(), (int)bt.size(), const_cast<const cbh_mat* const*>(bt.data()), &btc);
+      if (rc != CBH_OK) die(context(), rc, "cbh_mat_col_concat");
+      for (cbh_mat* t : bt) cbh_mat_free(context(), t);
+      rc = cbh_transpose(context(), btc, &bc);
+      if (rc != CBH_OK) die(context(), rc, "cbh_transpose");
+      cbh_mat_free(context(), btc);
+      Bcat.reset(new SpDCColsDev<IU, NU2>(bc));
+      Ahold.clear();  // the received stage blocks are copied into the strips
+      Bhold.clear();
+      add_plan(*Acat, *Bcat);
+    }
+    if (stages > 1 && !concat) cbh_ctx_set_bitmap_fraction(context(), -1.0);
   }
   ~StagePlans() {
     for (cbh_plan* p : plans)
@@ -333,6 +367,7 @@ class StagePlans {
     if (csize > 1) MPI_Allreduce(MPI_IN_PLACE, cnt.data(), (int)n, MPI_INT64_T, MPI_SUM, comm);
     return cnt;
   }
+  bool merges() const { return plans.size() > 1; }  // a phase merges per-stage partials
   std::shared_ptr<combblas::CommGrid> GridC;
   int stages = 0;
   int64_t m = 0;
@@ -341,8 +376,27 @@ class StagePlans {
  private:
   std::vector<std::unique_ptr<SpDCColsDev<IU, NU1>>> Ahold;  // received stage blocks
   std::vector<std::unique_ptr<SpDCColsDev<IU, NU2>>> Bhold;
+  std::unique_ptr<SpDCColsDev<IU, NU1>> Acat;  // the concatenated strips (default form)
+  std::unique_ptr<SpDCColsDev<IU, NU2>> Bcat;
   std::vector<cbh_plan*> plans;
-  std::vector<std::vector<int64_t>> bjc;  // host column ids of every stage's B block
+  std::vector<std::vector<int64_t>> bjc;  // host column ids of every plan's B operand
+  // one symbolic pass over A_i * B_i: its exact nnz and B's column ids (the phase cuts' slots)
+  void add_plan(SpDCColsDev<IU, NU1>& Ai, SpDCColsDev<IU, NU2>& Bi) {
+    cbh_plan* p = nullptr;
+    std::vector<int64_t> jc;
+    if (Ai.getnnz() > 0 && Bi.getnnz() > 0) {
+      int rc = cbh_plan_create(context(), Ai.mat(), Bi.mat(), &p);
+      if (rc != CBH_OK) die(context(), rc, "cbh_plan_create");
+      int64_t f = 0, z = 0;
+      cbh_plan_info(p, &f, &z);
+      nnz += z;
+      jc.resize((size_t)Bi.getnzc());
+      rc = cbh_mat_copy_out(context(), Bi.mat(), nullptr, jc.data(), nullptr, nullptr, 0);
+      if (rc != CBH_OK) die(context(), rc, "cbh_mat_copy_out");
+    }
+    plans.push_back(p);
+    bjc.push_back(std::move(jc));
+  }
 };
 
 // the product 3D grid of C (ParFriends.h:3200-3203 / 3700: a fresh CommGrid3D of A's shape)
@@ -466,9 +520,8 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
   }
   std::vector<cbh_mat*> toconcatenate;
   // the pruned pieces go back to back into one arena whose arrays become C's: the memory beside
-  // A, B, the plans and the largest phase product (its exact nnz; twice that when the stage
-  // partials of a multi-stage grid are merged, plus 10 % for the prune's scratch), at most the
-  // unpruned nnz
+  // A, B, the plans and the largest phase product (its exact nnz; twice that when per-stage
+  // partials are merged, plus 10 % for the prune's scratch), at most the unpruned nnz
   cbh_arena* arena = nullptr;
   int64_t* arena_hint = nullptr;
   {
@@ -476,7 +529,7 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
     int64_t live = 0, cached = 0, fr = 0, tot = 0;
     cbh_ctx_memory(ctx, &live, &cached, &fr, &tot);
     const int64_t eb = (int64_t)(sizeof(int32_t) + sizeof(NUO));
-    const int64_t phase_bytes = (int64_t)(1.1 * (double)max_phase_nnz * (SP.stages > 1 ? 2 : 1)) * eb;
+    const int64_t phase_bytes = (int64_t)(1.1 * (double)max_phase_nnz * (SP.merges() ? 2 : 1)) * eb;
     int64_t cap = (fr + cached - phase_bytes - (int64_t(8) << 30)) / eb;
     cap = std::min<int64_t>(cap, SP.nnz);
     // an MCL iteration prunes to about the previous call's size: an arena sized from it (+15 %)

@@ -21,10 +21,10 @@ HARNESS = os.path.join(H.REPO, "oracle", "_ref", "devpath3d_harness")
 ENV = dict(os.environ, LD_LIBRARY_PATH="/usr/lib/x86_64-linux-gnu:/opt/conda/lib", OMP_NUM_THREADS="1")
 
 
-def _run(np_, scale, layers, expect, transport):
+def _run(np_, scale, layers, expect, transport, **extra_env):
     assert os.path.exists(HARNESS), "oracle/_ref/devpath3d_harness missing: run __graft_entry__.build() with the reference"
     cmd = [HARNESS, str(scale), str(layers)]
-    env = dict(ENV)
+    env = dict(ENV, **extra_env)
     if np_ > 1:
         cmd = ["/opt/conda/bin/mpirun", "-np", str(np_)] + cmd
         env["COMBBLAS_HIP_COMM"] = "mpi"
@@ -48,3 +48,14 @@ def test_devpath3d_1x1x2_shared_gpu():
 
 def test_devpath3d_2x2x2_shared_gpu():
     _run(8, 10, 2, 3, "mpi")
+
+
+def test_devpath3d_2x2_per_stage_plans():
+    """the reference's per-stage form of the phased drivers (one plan per SUMMA stage pair, stage
+    partials merged per phase; COMBBLAS_HIP_STAGE_PLANS=per-stage) against the stock drivers; the
+    tests above run the default concatenated strips"""
+    _run(4, 11, 0, 3, "mpi", COMBBLAS_HIP_STAGE_PLANS="per-stage")
+
+
+def test_devpath3d_2x2x2_per_stage_plans():
+    _run(8, 10, 2, 3, "mpi", COMBBLAS_HIP_STAGE_PLANS="per-stage")
