@@ -131,7 +131,7 @@ __device__ __forceinline__ void block_excl_sum2(int& a, int& b, int* red, int& t
 // probing, rank commit without a sort); a sub-tile that overflows its probes is
 // retried with half the rows, so its entries' cursors commit only after it succeeded.
 template <class SR, int BS, int EL, int U, int LDSB, int KIND = KDENSE>
-__global__ __launch_bounds__(BS, 4) void dense_kernel(TaskArgs a) {  // 16 waves per CU
+__global__ __launch_bounds__(BS, BS >= 1024 ? 4 : 6) void dense_kernel(TaskArgs a) {  // 16 (24) waves per CU
   constexpr bool SYM = KIND == KSYMB;
   using C = DenseCfg<SR, BS, EL, U, LDSB, KIND>;
   using val_t = typename SR::val_t;

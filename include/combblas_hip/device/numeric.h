@@ -233,12 +233,19 @@ struct TSym2 {
 // scale-22 digests pass on it) but slower at scale 22, hash 269.9 -> 343.8 ms (A/B r5f,
 // profiles/r05/hash): the hash tasks are short (~9 K outputs, ~2.4 of its sub-tiles each), and one
 // workgroup per CU leaves their per-task setup and block scans uncovered, which task_kernel's three
-// 53 KB workgroups per CU overlap. TNumHash stays the shipped hash kernel.
+// 53 KB workgroups per CU overlap. Two 512-thread groups per CU (80 KB, ~3.5 K slots) and four
+// 256-thread groups (40 KB) were slower still: hash 280.7 / 279.5 vs 234.1 ms (r5h2,
+// profiles/r05/hash). TNumHash stays the shipped hash kernel.
 #ifndef CBH_HASH_V2
 #define CBH_HASH_V2 0
 #endif
+#ifndef CBH_HASH2_BS  // (A/B hooks: build variants only)
+#define CBH_HASH2_BS 1024
+#define CBH_HASH2_EL 1024
+#define CBH_HASH2_LDS 163776
+#endif
 struct THash2 {
-  static constexpr int BS = 1024, EL = 1024, U = 4, LDSB = 163776;
+  static constexpr int BS = CBH_HASH2_BS, EL = CBH_HASH2_EL, U = 4, LDSB = CBH_HASH2_LDS;
 };
 
 // Numeric tasks of the small bin: one per wave (wave_kernel.h); wide user value types keep the
