@@ -13,10 +13,12 @@ cd "$R" || exit 1
 step() { echo "== $(date +%T) $*"; }
 # PART=2 runs only the application lines (C5, C3, C4), so the two halves fit one call each
 if [ "${PART:-1}" = 2 ]; then
-  for app in mcl galerkin tc; do
+  for app in mcl mcl_cpp galerkin tc c1; do
     step "bench_$app"
-    timeout -k 10 700 python -u bench_$app.py > "$OUT/bench_$app.json" 2> "$OUT/bench_$app.err" || { tail -20 "$OUT/bench_$app.err"; exit 1; }
-    cat "$OUT/bench_$app.json"
+    args=""
+    [ "$app" = mcl_cpp ] && args="--driver cpp"
+    timeout -k 10 700 python -u bench_${app%_cpp}.py $args > "$OUT/bench_$app.json" 2> "$OUT/bench_$app.err" || { tail -20 "$OUT/bench_$app.err"; exit 1; }
+    tail -c 600 "$OUT/bench_$app.json"; echo
   done
   step done
   exit 0
