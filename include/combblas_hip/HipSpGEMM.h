@@ -170,7 +170,7 @@ cbh_mat* upload(const combblas::SpTuples<IT, NT>& T, bool sort_rows = false) {
   h.n = T.getncol();
   h.nnz = T.getnnz();
   if (h.m > std::numeric_limits<int32_t>::max()) die(context(), CBH_E_DIMMISMATCH, "local rows exceed int32");
-  std::vector<int64_t> cp(1, 0), jc;
+  std::vector<int64_t> cp, jc;
   std::vector<int32_t> ir(h.nnz);
   std::unique_ptr<NT[]> num(new NT[h.nnz > 0 ? h.nnz : 1]);  // not std::vector: vector<bool> has no data()
 #pragma omp parallel for schedule(static)
@@ -178,15 +178,32 @@ cbh_mat* upload(const combblas::SpTuples<IT, NT>& T, bool sort_rows = false) {
     ir[i] = static_cast<int32_t>(T.rowindex(i));
     num[i] = T.numvalue(i);
   }
-  for (int64_t i = 0; i < h.nnz; ++i) {  // column heads (the tuples are column-sorted)
-    const IT c = T.colindex(i);
-    if (jc.empty() || jc.back() != c) {
-      if (!jc.empty()) cp.push_back(i);
-      jc.push_back(c);
-    }
+  // column heads (the tuples are column-sorted): counted per block, offsets by a scan over the
+  // blocks, written per block -- both passes parallel
+  constexpr int64_t kBlocks = 256;
+  const int64_t bl = (h.nnz + kBlocks - 1) / kBlocks;
+  std::vector<int64_t> heads(kBlocks + 1, 0);
+  auto head = [&T](int64_t i) { return i == 0 || T.colindex(i) != T.colindex(i - 1); };
+#pragma omp parallel for schedule(static)
+  for (int64_t b = 0; b < kBlocks; ++b) {
+    int64_t c = 0;
+    for (int64_t i = b * bl, e = std::min(h.nnz, (b + 1) * bl); i < e; ++i) c += head(i) ? 1 : 0;
+    heads[b + 1] = c;
   }
-  if (!jc.empty()) cp.push_back(h.nnz);
-  h.nzc = (int64_t)jc.size();
+  for (int64_t b = 0; b < kBlocks; ++b) heads[b + 1] += heads[b];
+  h.nzc = heads[kBlocks];
+  cp.resize(h.nzc + 1);
+  jc.resize(h.nzc);
+#pragma omp parallel for schedule(static)
+  for (int64_t b = 0; b < kBlocks; ++b) {
+    int64_t k = heads[b];
+    for (int64_t i = b * bl, e = std::min(h.nnz, (b + 1) * bl); i < e; ++i)
+      if (head(i)) {
+        cp[k] = i;
+        jc[k++] = T.colindex(i);
+      }
+  }
+  cp[h.nzc] = h.nnz;
   const int64_t ncols_up = (int64_t)cp.size() - 1;
   if (sort_rows)
 #pragma omp parallel for schedule(dynamic, 256)
