@@ -224,8 +224,11 @@ hipError_t launch_dense_numeric(const TaskArgs& a, int64_t first, int64_t count,
 #ifndef CBH_SYM_V2
 #define CBH_SYM_V2 1
 #endif
+#ifndef CBH_SYM2_U  // (A/B hook: build variants only)
+#define CBH_SYM2_U 8
+#endif
 struct TSym2 {
-  static constexpr int BS = 1024, EL = 1024, U = 8, LDSB = 163776;
+  static constexpr int BS = 1024, EL = 1024, U = CBH_SYM2_U, LDSB = 163776;
 };
 // The numeric hash tasks of the large bin on the same kernel (KHASH: ~7.4 K-slot order-preserving
 // table, sub-tiles of ~3.7 K outputs instead of task_kernel's 1 K; U 4: U 8 spills at the 128-VGPR
