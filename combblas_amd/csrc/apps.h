@@ -356,7 +356,11 @@ __device__ __forceinline__ void dot_piece(const DotArgs& a, const int32_t* __res
     }
   } else {
     // much longer other list: every element binary-searches it (an interpolation start measured
-    // slower: 9.7 vs 8.1 s at scale 24 -- the bisection's first levels are shared L2 hits)
+    // slower: 9.7 vs 8.1 s at scale 24 -- the bisection's first levels are shared L2 hits). Round 5
+    // measured this branch at 3.5 of the 8.1 s (a build without the search: 4.6 s) and two ways to
+    // shorten it, both slower: an 8-ary search with 7 splitter loads per level (15.3 s: its deep
+    // levels fetch 7 distinct lines each) and the top levels from an LDS sample of the longer
+    // list, 1024 rows per wave (8.24 vs 8.14 s: the shared top levels were never the cost)
     for (int64_t base = s0; base < s1 && lo < hi; base += 64) {
       const int64_t s = base + lane;
       int64_t q = hi;
