@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <vector>
 
@@ -131,53 +132,70 @@ inline void rccl_check(ncclResult_t r, const char* what) {
   }
 }
 
-// ncclComm_t mirroring one MPI communicator (ncclUniqueId from its rank 0 over MPI_Bcast). The
-// ncclComm is cached as an MPI attribute of that communicator, so it lives exactly as long as the
-// communicator: the reference's ProductGrid makes a new CommGrid per product and its destructor
-// MPI_Comm_free's the row/column worlds (CommGrid.h:49-56), which runs the delete callback below
-// (ncclCommDestroy). A handle value MPI later reuses for another communicator carries no attribute,
-// so it can never return an ncclComm with the wrong members.
-inline int rccl_comm_delete(MPI_Comm, int, void* attr, void*) {
-  auto* c = static_cast<ncclComm_t*>(attr);
-  hip_check(hipStreamSynchronize(reinterpret_cast<hipStream_t>(cbh_ctx_stream(context()))), "hipStreamSynchronize");
-  ncclCommDestroy(*c);
-  delete c;
-  return MPI_SUCCESS;
+// ncclComm_t for an MPI communicator, one per MEMBERSHIP (the communicator's ranks in
+// MPI_COMM_WORLD, in communicator rank order): created collectively (ncclUniqueId from the
+// communicator's rank 0 over MPI_Bcast) the first time a communicator with those members is used,
+// then kept for the process. The reference's ProductGrid builds a fresh CommGrid -- fresh row and
+// column MPI communicators -- for every product (CommGrid.cpp:164-180), so a communicator-keyed
+// ncclComm paid ncclCommInitRank's bootstrap on every call (round 4 keyed it by the MPI handle and
+// destroyed it with the communicator). Every member of a membership ran the same creation (SPMD),
+// so all of them find it in their caches. An attribute on the MPI communicator remembers the
+// lookup (no delete callback: the ncclComm outlives the communicator).
+inline std::map<std::vector<int>, ncclComm_t>& rccl_cache() {
+  static std::map<std::vector<int>, ncclComm_t> m;
+  return m;
 }
 inline int rccl_keyval() {
   static int kv = [] {
     int k = MPI_KEYVAL_INVALID;
-    MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, rccl_comm_delete, &k, nullptr);
+    MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, MPI_COMM_NULL_DELETE_FN, &k, nullptr);
     return k;
   }();
   return kv;
+}
+inline std::vector<int> world_ranks(MPI_Comm comm) {
+  MPI_Group g, wg;
+  MPI_Comm_group(comm, &g);
+  MPI_Comm_group(MPI_COMM_WORLD, &wg);
+  int n = 0;
+  MPI_Group_size(g, &n);
+  std::vector<int> in(n), out(n);
+  for (int i = 0; i < n; ++i) in[i] = i;
+  MPI_Group_translate_ranks(g, n, in.data(), wg, out.data());
+  MPI_Group_free(&g);
+  MPI_Group_free(&wg);
+  return out;
 }
 inline ncclComm_t rccl_comm_for(MPI_Comm comm) {
   void* attr = nullptr;
   int found = 0;
   MPI_Comm_get_attr(comm, rccl_keyval(), &attr, &found);
   if (found && attr) return *static_cast<ncclComm_t*>(attr);
-  int rank = 0, size = 1;
-  MPI_Comm_rank(comm, &rank);
-  MPI_Comm_size(comm, &size);
-  ncclUniqueId id;
-  if (rank == 0) rccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
-  MPI_Bcast(&id, (int)sizeof(id), MPI_BYTE, 0, comm);
-  // the context selects this rank's device; when less than 8 GB of device memory is free, cached
-  // blocks go back to HIP (largest first, as many as make 8 GB free), so that RCCL's own buffers
-  // find the memory (the block cache may hold a large share of the HBM). (Trimming the
-  // whole cache made every phased call -- a new ProductGrid, new communicators -- re-map it:
-  // 3 s per C5 step.)
-  {
-    int64_t fr = 0, tot = 0;
-    const int64_t want = int64_t(8) << 30;
-    cbh_ctx_memory(context(), nullptr, nullptr, &fr, &tot);
-    if (fr < want) cbh_ctx_release(context(), want - fr);
+  auto& cache = rccl_cache();
+  const std::vector<int> key = world_ranks(comm);
+  auto it = cache.find(key);
+  if (it == cache.end()) {
+    int rank = 0, size = 1;
+    MPI_Comm_rank(comm, &rank);
+    MPI_Comm_size(comm, &size);
+    ncclUniqueId id;
+    if (rank == 0) rccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    MPI_Bcast(&id, (int)sizeof(id), MPI_BYTE, 0, comm);
+    // the context selects this rank's device; when less than 8 GB of device memory is free, cached
+    // blocks go back to HIP (largest first, as many as make 8 GB free), so that RCCL's own buffers
+    // find the memory (the block cache may hold a large share of the HBM)
+    {
+      int64_t fr = 0, tot = 0;
+      const int64_t want = int64_t(8) << 30;
+      cbh_ctx_memory(context(), nullptr, nullptr, &fr, &tot);
+      if (fr < want) cbh_ctx_release(context(), want - fr);
+    }
+    ncclComm_t c;
+    rccl_check(ncclCommInitRank(&c, size, id, rank), "ncclCommInitRank");
+    it = cache.emplace(key, c).first;
   }
-  auto* c = new ncclComm_t;
-  rccl_check(ncclCommInitRank(c, size, id, rank), "ncclCommInitRank");
-  MPI_Comm_set_attr(comm, rccl_keyval(), c);
-  return *c;
+  MPI_Comm_set_attr(comm, rccl_keyval(), &it->second);  // std::map nodes are stable
+  return it->second;
 }
 
 // SpParHelper::BCastMatrix (SpParHelper.cpp:581-599) on device blocks, in two halves: non-root
