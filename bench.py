@@ -103,7 +103,7 @@ def parse():
                    help="N>1: cpp = the C++ host path (cxx/bench_summa under mpirun), python = combblas_amd's "
                         "drivers; auto = cpp when it is built, python if it fails to start")
     p.add_argument("--phases", type=int, default=0, help="N>1 cpp driver: column phases (0 = planned)")
-    p.add_argument("--cpp-timeout", type=float, default=1200.0, help="N>1 cpp driver: seconds before it is killed "
+    p.add_argument("--cpp-timeout", type=float, default=600.0, help="N>1 cpp driver: seconds before it is killed "
                                                                        "(auto: the python drivers run instead)")
     return p.parse_args()
 
