@@ -14,6 +14,7 @@ import sys
 import pytest
 
 import helpers as H
+from dist_util import _free_port
 
 pytestmark = pytest.mark.gpu
 
@@ -24,7 +25,7 @@ BENCH = os.path.join(H.REPO, "cxx", "_build", "bench_summa")
                                                (2, 0, "MemEfficientSpGEMM3D"), (2, 2, "MemEfficientSpGEMM3D")])
 def test_bench_cpp_driver(ranks, phases, host):
     assert os.path.exists(BENCH), "cxx/_build/bench_summa missing: run __graft_entry__.build() with the reference"
-    port = 29700 + ranks * 10 + phases
+    port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(H.REPO, "bench.py"),
            "--gpus", str(ranks), "--steps", "1", "--warmup", "1", "--scale", "14", "--share-gpu",

@@ -15,6 +15,7 @@ import sys
 import pytest
 
 import helpers as H
+from dist_util import _free_port
 
 STUB = r'''#!/bin/bash
 # stand-in for mpirun: $1 = -np, $2 = N, $3 = binary, then scale steps warmup phases
@@ -52,7 +53,7 @@ def _run(tmp_path, fail, driver, port):
 
 
 def test_launcher_runs_the_cpp_driver(tmp_path):
-    r, flops, envfile, argfile = _run(tmp_path, False, "cpp", 29811)
+    r, flops, envfile, argfile = _run(tmp_path, False, "cpp", _free_port())
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -70,6 +71,6 @@ def test_launcher_runs_the_cpp_driver(tmp_path):
 
 
 def test_launcher_reports_a_failed_cpp_run(tmp_path):
-    r, _, _, _ = _run(tmp_path, True, "cpp", 29821)
+    r, _, _, _ = _run(tmp_path, True, "cpp", _free_port())
     assert r.returncode != 0
     assert "C++ driver failed" in r.stderr
