@@ -190,8 +190,7 @@ inline cbh_mat* fiber_reduce_scatter(cbh_semiring sr, cbh_mat* P, const std::vec
           hip_check(hipMemcpyAsync(hs.data(), a.p[k], a.b[k], hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
           hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
         }
-        MPI_Sendrecv(hs.data(), (int)a.b[k], MPI_BYTE, to, k, hr.data(), (int)b.b[k], MPI_BYTE, from, k, fiber,
-                     MPI_STATUS_IGNORE);
+        mpi_sendrecv_bytes(hs.data(), a.b[k], to, hr.data(), b.b[k], from, k, fiber);
         if (b.b[k]) {
           hip_check(hipMemcpyAsync(b.p[k], hr.data(), b.b[k], hipMemcpyHostToDevice, s), "hipMemcpyAsync");
           hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");

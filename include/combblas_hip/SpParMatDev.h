@@ -125,6 +125,29 @@ inline void hip_check(hipError_t e, const char* what) {
   }
 }
 
+// host-staged transport (COMBBLAS_HIP_COMM=mpi): MPI counts are int, so messages go in pieces of
+// at most 1 GiB
+constexpr size_t kMpiPiece = size_t(1) << 30;
+inline void mpi_bcast_bytes(void* buf, size_t bytes, int root, MPI_Comm comm) {
+  for (size_t o = 0; o < bytes; o += kMpiPiece)
+    MPI_Bcast(static_cast<char*>(buf) + o, (int)std::min(kMpiPiece, bytes - o), MPI_BYTE, root, comm);
+}
+inline void mpi_sendrecv_bytes(const void* sbuf, size_t sbytes, int to, void* rbuf, size_t rbytes, int from, int tag,
+                               MPI_Comm comm) {
+  // pieces in order, each side counting its own (MPI keeps the order of one pair's messages)
+  std::vector<MPI_Request> req;
+  for (size_t o = 0; o < rbytes; o += kMpiPiece) {
+    req.emplace_back();
+    MPI_Irecv(static_cast<char*>(rbuf) + o, (int)std::min(kMpiPiece, rbytes - o), MPI_BYTE, from, tag, comm, &req.back());
+  }
+  for (size_t o = 0; o < sbytes; o += kMpiPiece) {
+    req.emplace_back();
+    MPI_Isend(static_cast<const char*>(sbuf) + o, (int)std::min(kMpiPiece, sbytes - o), MPI_BYTE, to, tag, comm,
+              &req.back());
+  }
+  if (!req.empty()) MPI_Waitall((int)req.size(), req.data(), MPI_STATUSES_IGNORE);
+}
+
 inline void rccl_check(ncclResult_t r, const char* what) {
   if (r != ncclSuccess) {
     std::fprintf(stderr, "combblas_hip: %s failed: %s\n", what, ncclGetErrorString(r));
@@ -246,7 +269,7 @@ void bcast_arrays(MPI_Comm comm, SpDCColsDev<IT, NT>& M, const std::vector<IT>& 
         hip_check(hipMemcpyAsync(h.data(), x.p, x.bytes, hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
         hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
       }
-      MPI_Bcast(h.data(), (int)x.bytes, MPI_BYTE, root, comm);
+      mpi_bcast_bytes(h.data(), x.bytes, root, comm);
       if (rank != root) {
         hip_check(hipMemcpyAsync(x.p, h.data(), x.bytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync");
         hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
