@@ -197,7 +197,7 @@ inline cbh_mat* fiber_reduce_scatter(cbh_semiring sr, cbh_mat* P, const std::vec
         }
       }
     }
-  } else {
+  } else if (L > 1) {
     ncclComm_t nc = rccl_comm_for(fiber);
     rccl_check(ncclGroupStart(), "ncclGroupStart");
     for (int j = 0; j < L; ++j) {
@@ -480,6 +480,7 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
   if (phases < 1 || phases >= A.getncol()) phases = 1;
   // the plans (and their scratch) live for the phase loop only: the concatenation of the pruned
   // pieces below needs a second copy of them in HBM
+  combblas_hip::ensure_device_free();
   combblas_hip::memdiag("MemEfficientSpGEMM start");
   std::unique_ptr<combblas_hip::StagePlans<IU, NU1, NU2>> SPp(
       new combblas_hip::StagePlans<IU, NU1, NU2>(A.seq(), A.getcommgrid().get(), B.seq(), B.getcommgrid().get()));
@@ -529,7 +530,9 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
     cbh_ctx_memory(ctx, &live, &cached, &fr, &tot);
     const int64_t eb = (int64_t)(sizeof(int32_t) + sizeof(NUO));
     const int64_t phase_bytes = (int64_t)(1.1 * (double)max_phase_nnz * (SP.merges() ? 2 : 1)) * eb;
-    int64_t cap = (fr + cached - phase_bytes - (int64_t(8) << 30)) / eb;
+    // (12 GB beside the phase: the phase piece's own scratch and whatever else the device holds --
+    // 8 GB fitted C5 only while a per-call RCCL communicator's buffers kept the arena smaller)
+    int64_t cap = (fr + cached - phase_bytes - (int64_t(12) << 30)) / eb;
     cap = std::min<int64_t>(cap, SP.nnz);
     // an MCL iteration prunes to about the previous call's size: an arena sized from it (+15 %)
     // leaves the phase blocks in the allocator's cache from call to call (an undersized arena only
@@ -608,6 +611,7 @@ SpParMat3D<IU, NUO, UDERO> MemEfficientSpGEMM3D(SpParMat3D<IU, NU1, combblas_hip
     MPI_Abort(MPI_COMM_WORLD, DIMMISMATCH);
   }
   if (phases < 1 || phases >= B.getncol()) phases = 1;
+  combblas_hip::ensure_device_free();
   auto g3 = A.getcommgrid3D();
   // the layer SUMMA's stage pairs, planned once for every phase (freed before the concatenation)
   std::unique_ptr<combblas_hip::StagePlans<IU, NU1, NU2>> SPp(new combblas_hip::StagePlans<IU, NU1, NU2>(

@@ -148,6 +148,16 @@ inline void mpi_sendrecv_bytes(const void* sbuf, size_t sbytes, int to, void* rb
   if (!req.empty()) MPI_Waitall((int)req.size(), req.data(), MPI_STATUSES_IGNORE);
 }
 
+// when less than `want` bytes of device memory are free, cached blocks of the context allocator go
+// back to HIP (largest first, as many as make `want` free): before RCCL allocates a communicator's
+// buffers, and at the start of a phased product, whose arena and phase pieces are sized from the
+// free memory (the block cache may hold a large share of the HBM)
+inline void ensure_device_free(int64_t want = int64_t(8) << 30) {
+  int64_t fr = 0, tot = 0;
+  cbh_ctx_memory(context(), nullptr, nullptr, &fr, &tot);
+  if (fr < want) cbh_ctx_release(context(), want - fr);
+}
+
 inline void rccl_check(ncclResult_t r, const char* what) {
   if (r != ncclSuccess) {
     std::fprintf(stderr, "combblas_hip: %s failed: %s\n", what, ncclGetErrorString(r));
@@ -194,6 +204,7 @@ inline ncclComm_t rccl_comm_for(MPI_Comm comm) {
   int found = 0;
   MPI_Comm_get_attr(comm, rccl_keyval(), &attr, &found);
   if (found && attr) return *static_cast<ncclComm_t*>(attr);
+  ensure_device_free();  // RCCL's buffers are not the context allocator's
   auto& cache = rccl_cache();
   const std::vector<int> key = world_ranks(comm);
   auto it = cache.find(key);
@@ -204,15 +215,6 @@ inline ncclComm_t rccl_comm_for(MPI_Comm comm) {
     ncclUniqueId id;
     if (rank == 0) rccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
     MPI_Bcast(&id, (int)sizeof(id), MPI_BYTE, 0, comm);
-    // the context selects this rank's device; when less than 8 GB of device memory is free, cached
-    // blocks go back to HIP (largest first, as many as make 8 GB free), so that RCCL's own buffers
-    // find the memory (the block cache may hold a large share of the HBM)
-    {
-      int64_t fr = 0, tot = 0;
-      const int64_t want = int64_t(8) << 30;
-      cbh_ctx_memory(context(), nullptr, nullptr, &fr, &tot);
-      if (fr < want) cbh_ctx_release(context(), want - fr);
-    }
     ncclComm_t c;
     rccl_check(ncclCommInitRank(&c, size, id, rank), "ncclCommInitRank");
     it = cache.emplace(key, c).first;
@@ -247,8 +249,10 @@ void BCastMatrix(MPI_Comm comm, SpDCColsDev<IT, NT>& M, const std::vector<IT>& e
 template <class IT, class NT>
 void bcast_arrays(MPI_Comm comm, SpDCColsDev<IT, NT>& M, const std::vector<IT>& ess, int root, hipStream_t s,
                   bool grouped) {
-  int rank = 0;
+  int rank = 0, csize = 1;
   MPI_Comm_rank(comm, &rank);
+  MPI_Comm_size(comm, &csize);
+  if (csize == 1) return;  // the root's own block: nothing moves (and no communicator is created)
   const int64_t *cp, *jc;
   const int32_t* ir;
   const void* num;
@@ -387,8 +391,11 @@ void summa_overlap(SpDCColsDev<IU, NU1>& Aloc, combblas::CommGrid* GA, SpDCColsD
   std::vector<hipEvent_t> done(stages, nullptr);
   if (overlap) {
     MPI_Comm rw = GridC->GetRowWorld(), cw = GridC->GetColWorld();
-    (void)rccl_comm_for(rw);  // communicators exist before the grouped calls
-    (void)rccl_comm_for(cw);
+    int rws = 1, cws = 1;
+    MPI_Comm_size(rw, &rws);
+    MPI_Comm_size(cw, &cws);
+    if (rws > 1) (void)rccl_comm_for(rw);  // communicators exist before the grouped calls
+    if (cws > 1) (void)rccl_comm_for(cw);
     hipEvent_t ready;
     if (hipEventCreateWithFlags(&ready, hipEventDisableTiming) != hipSuccess) die(context(), CBH_E_HIP, "hipEventCreate");
     hip_check(hipEventRecord(ready, ks), "hipEventRecord");  // the receive blocks' memory: ordered after the context stream's work
