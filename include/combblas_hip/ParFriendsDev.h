@@ -479,8 +479,9 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
   }
   if (phases < 1 || phases >= A.getncol()) phases = 1;
   // the plans (and their scratch) live for the phase loop only: the concatenation of the pruned
-  // pieces below needs a second copy of them in HBM
-  combblas_hip::ensure_device_free();
+  // pieces below needs a second copy of them in HBM (no cache release here: the block cache
+  // holds the previous call's phase blocks, which this call's phases reuse -- releasing them first
+  // made C5's third MCL call run out of memory)
   combblas_hip::memdiag("MemEfficientSpGEMM start");
   std::unique_ptr<combblas_hip::StagePlans<IU, NU1, NU2>> SPp(
       new combblas_hip::StagePlans<IU, NU1, NU2>(A.seq(), A.getcommgrid().get(), B.seq(), B.getcommgrid().get()));
