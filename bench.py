@@ -347,9 +347,12 @@ def _cpp_rank0(args, world, cb):
     d = json.loads(lines[-1])
     step_s = d["ms_per_step"] / 1e3
     known = KNOWN_NNZC.get(args.scale)
+    gold = reference_digest(args.scale, args.edgefactor)
+    dg = d.get("digest")
     check = {"nnzC": d["nnzC"], "expected_nnzC": known, "value_sum": d["value_sum"],
-             "expected_value_sum": float(closed_sum), "digest": None, "reference_digest": None}
-    check["ok"] = bool((known is None or d["nnzC"] == known) and d["value_sum"] == float(closed_sum))
+             "expected_value_sum": float(closed_sum), "digest": dg, "reference_digest": gold}
+    check["ok"] = bool((known is None or d["nnzC"] == known) and d["value_sum"] == float(closed_sum)
+                       and (gold is None or dg == gold))
     ks = {k: {"ms": v[0], "launches": v[1], "alg_bytes": v[2]} for k, v in d.get("kernel_stats_rank0", {}).items()}
     roofline = kernel_roofline(ks, KERNELS) if ks else None
     if roofline:
@@ -371,6 +374,7 @@ def _cpp_rank0(args, world, cb):
 
 def main():
     args = parse()
+    cpp_fallback = None
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -383,6 +387,7 @@ def main():
             return
         except RuntimeError as e:
             log(f"C++ driver did not run ({e}); python drivers instead")
+            cpp_fallback = str(e)[:500]  # recorded in the JSON line: the line is NOT the C++ host path
     import torch
     import torch.distributed as dist
     import combblas_amd as cb
@@ -550,7 +555,7 @@ def main():
             "data": "synthetic: packed Graph500 R-MAT (seed 0xDECAFBAD), bit-identical to the reference generator",
             "config": {"workload": f"rmat{args.scale}_ef{args.edgefactor}_AxA_PlusTimes_f64", "scale": args.scale,
                        "edgefactor": args.edgefactor, "nnzA": nnzA, "flops": int(flops), "nnzC": int(nnzC),
-                       "phases": st["phases"], "parallelism": parallelism,
+                       "phases": st["phases"], "parallelism": parallelism, "cpp_fallback": cpp_fallback,
                        "kernel_ms": {n: round(v["ms"] / max(args.steps, 1), 3) for n, v in ks.items()}},
             "roofline": roofline, "cpu_baseline": base, "check": check, "merge": merge,
         }

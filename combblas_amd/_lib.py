@@ -56,6 +56,11 @@ SIGNATURES = {
     "cbh_version": (ctypes.c_char_p, []),
     "cbh_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbh_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "cbh_device_pci_id": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
+    "cbh_ctx_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
+    "cbh_ctx_alloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_ctx_free": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "cbh_ctx_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "cbh_ctx_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
     "cbh_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
@@ -120,6 +125,9 @@ SIGNATURES = {
     "cbh_transpose": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_mat_checksum": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_uint64)]),
+    "cbh_mat_checksum_global": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                                ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                                ctypes.POINTER(ctypes.c_uint64)]),
     "cbh_ewise_mult": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_col_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p]),

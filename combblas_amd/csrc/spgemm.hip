@@ -113,6 +113,9 @@ static size_t dtype_size(int dt) {
   return 0;
 }
 
+// a HIP call's status as a library code (the context's error text set), for paths that must free
+// what they hold before returning instead of CBH_HIP's early return
+static int hip_rc(cbh_ctx* ctx, hipError_t e, const char* what);
 #define CBH_HIP(ctx, call)                                                                       \
   do {                                                                                           \
     hipError_t e_ = (call);                                                                      \
@@ -131,6 +134,11 @@ static size_t dtype_size(int dt) {
 static int fail(cbh_ctx* ctx, int code, const std::string& msg) {
   if (ctx) ctx->err = msg;
   return code;
+}
+static int hip_rc(cbh_ctx* ctx, hipError_t e, const char* what) {
+  if (e == hipSuccess) return CBH_OK;
+  return fail(ctx, (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) ? CBH_E_OOM : CBH_E_HIP,
+              std::string(what) + ": " + hipGetErrorString(e));
 }
 
 // Default device allocator: a per-context cache of hipMalloc'd blocks, reused in stream order.
@@ -511,13 +519,18 @@ template <class VT>
 __global__ __launch_bounds__(256) void checksum_kernel(const int64_t* __restrict__ colid, const int64_t* __restrict__ cp,
                                                        int64_t cbase, int64_t ncols, const int32_t* __restrict__ ir,
                                                        const VT* __restrict__ num, int64_t gbase,
-                                                       double* __restrict__ vsum, unsigned long long* __restrict__ dig) {
+                                                       double* __restrict__ vsum, unsigned long long* __restrict__ dig,
+                                                       const int64_t* __restrict__ colpos = nullptr,
+                                                       int64_t row_off = 0, int64_t col_off = 0) {
   const int lane = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   double s = 0;
   uint64_t d = 0;
   if (c < ncols) {
-    const uint64_t col = (uint64_t)colid[c];
+    const uint64_t col = (uint64_t)(colid[c] + col_off);
+    // colpos (a block of a distributed C): the global position of the column's first entry, so that
+    // the blocks' digests add up to the whole product's
+    if (colpos) gbase = colpos[c] - (cp[c] - cbase);
     for (int64_t p = cp[c] - cbase + lane; p < cp[c + 1] - cbase; p += 64) {
       const VT v = num[p];
       uint64_t bits;
@@ -525,7 +538,7 @@ __global__ __launch_bounds__(256) void checksum_kernel(const int64_t* __restrict
       else if constexpr (sizeof(VT) == 4) bits = (uint64_t)__builtin_bit_cast(uint32_t, v);
       else bits = (uint64_t)v;
       s += (double)v;
-      d += mix64((uint64_t)(gbase + p) ^ mix64(col ^ mix64((uint64_t)(uint32_t)ir[p] ^ mix64(bits))));
+      d += mix64((uint64_t)(gbase + p) ^ mix64(col ^ mix64((uint64_t)(uint32_t)(ir[p] + row_off) ^ mix64(bits))));
     }
   }
 #pragma unroll
@@ -1366,6 +1379,24 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
   return CBH_OK;
 }
 
+// The reference-order pass (device/order_kernel.h) over C's tasks after the throughput pass
+template <class SR>
+static int run_reference_order(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat* B, Plan& P, cbh_mat* out,
+                               uint32_t flags) {
+  const int branch = (flags & CBH_ORDER_HEAP) ? 1 : ((flags & CBH_ORDER_HASH) ? 2 : 0);
+  TaskArgs a = task_args(A, B, P, ctx);
+  a.twork = P.tcnt;
+  a.toff = P.toff;
+  a.cbase = 0;
+  a.Cir = out->ir;
+  a.Cnum = out->num;
+  a.ccap = P.total_nnz;
+  unsigned char* scratch;
+  CBH_TRY(S.get(&scratch, (int64_t)ord_scratch_bytes<SR>(B->nnz, P.ntasks, P.total_nnz)));
+  CBH_HIP(ctx, (launch_reference_order<Ordered<SR>>(a, scratch, B->nnz, P.total_nnz, branch, ctx->stream)));
+  return check_err(ctx);
+}
+
 // ============================================================================ semiring dispatch
 template <class F>
 static int dispatch_sr(cbh_ctx* ctx, cbh_semiring sr, int dtype, F&& f) {
@@ -1463,6 +1494,27 @@ static float ev_ms(cbh_ctx* ctx, int a, int b) {
 extern "C" {
 
 const char* cbh_version(void) { return "combblas_hip 0.1 (gfx950)"; }
+
+int cbh_device_count(int* n) {
+  if (!n) return CBH_E_ARG;
+  *n = 0;
+  if (hipGetDeviceCount(n) != hipSuccess || *n <= 0) {
+    *n = 0;
+    return CBH_E_NODEVICE;
+  }
+  return CBH_OK;
+}
+
+int cbh_device_pci_id(int device, char* buf, int len) {
+  if (!buf || len < 13) return CBH_E_ARG;
+  return hipDeviceGetPCIBusId(buf, len, device) == hipSuccess ? CBH_OK : CBH_E_HIP;
+}
+
+int cbh_ctx_device(cbh_ctx* ctx, int* device) {
+  if (!ctx || !device) return CBH_E_ARG;
+  *device = ctx->device;
+  return CBH_OK;
+}
 
 int cbh_ctx_create(int device, cbh_ctx** out) {
   if (!out) return CBH_E_ARG;
@@ -1562,6 +1614,21 @@ int cbh_ctx_release(cbh_ctx* ctx, int64_t bytes) {
 }
 
 const char* cbh_last_error(cbh_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int cbh_ctx_alloc(cbh_ctx* ctx, int64_t bytes, void** p) {
+  if (!ctx || !p || bytes < 0) return CBH_E_ARG;
+  *p = nullptr;
+  unsigned char* q = nullptr;
+  CBH_TRY(dalloc(ctx, &q, (size_t)(bytes > 0 ? bytes : 1)));
+  *p = q;
+  return CBH_OK;
+}
+
+int cbh_ctx_free(cbh_ctx* ctx, void* p) {
+  if (!ctx) return CBH_E_ARG;
+  if (p) dfree(ctx, p);
+  return CBH_OK;
+}
 
 int cbh_hash_config(int64_t* table_slots, int64_t* threads, int64_t* per_thread) {
 #if CBH_HASH_V2
@@ -1950,16 +2017,21 @@ int cbh_spgemm(cbh_ctx* ctx, cbh_semiring sr, const cbh_mat* A, const cbh_mat* B
     CBH_TRY(new_result(ctx, S, P, A->m, B->n, P.total_nnz, nzcC, A->dtype, &out));
     int64_t launches = 0;
     int rc = run_numeric<SR>(ctx, S, A, B, P, 0, P.ntasks, 0, out->ir, out->num, &launches, P.total_nnz);
+    if (rc == CBH_OK && (flags & (CBH_ORDER_HYBRID | CBH_ORDER_HEAP | CBH_ORDER_HASH)))
+      rc = run_reference_order<SR>(ctx, S, A, B, P, out, flags);
     if (rc == CBH_OK) {
       if (keep) {
-        (void)hipMemcpyAsync(out->jc, B->jc, sizeof(int64_t) * P.nzcB, hipMemcpyDeviceToDevice, ctx->stream);
-        (void)hipMemcpyAsync(out->cp, P.Ccp, sizeof(int64_t) * (P.nzcB + 1), hipMemcpyDeviceToDevice, ctx->stream);
+        rc = hip_rc(ctx, hipMemcpyAsync(out->jc, B->jc, sizeof(int64_t) * P.nzcB, hipMemcpyDeviceToDevice, ctx->stream),
+                    "hipMemcpyAsync(C.jc)");
+        if (rc == CBH_OK)
+          rc = hip_rc(ctx, hipMemcpyAsync(out->cp, P.Ccp, sizeof(int64_t) * (P.nzcB + 1), hipMemcpyDeviceToDevice, ctx->stream),
+                      "hipMemcpyAsync(C.cp)");
       } else {
         hipLaunchKernelGGL(compact_cols_kernel, dim3(blocks_for(P.nzcB, 256)), dim3(256), 0, ctx->stream, P.nnz, pos,
                            B->jc, P.Ccp, P.nzcB, out->jc, out->cp);
       }
       ev_record(ctx, 2);
-      rc = check_err(ctx);
+      if (rc == CBH_OK) rc = check_err(ctx);
     }
     if (rc != CBH_OK) {
       cbh_mat_free(ctx, out);
@@ -2512,9 +2584,12 @@ int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* p
                                                                  CBH_K_MERGE_NUM, eb * (bl.units[0] + bl.units[1]));
     }
     if (rc == CBH_OK) {
-      (void)hipMemcpyAsync(out->jc, jcC, sizeof(int64_t) * ncols, hipMemcpyDeviceToDevice, ctx->stream);
-      (void)hipMemcpyAsync(out->cp, Ccp, sizeof(int64_t) * (ncols + 1), hipMemcpyDeviceToDevice, ctx->stream);
-      rc = check_err(ctx);
+      rc = hip_rc(ctx, hipMemcpyAsync(out->jc, jcC, sizeof(int64_t) * ncols, hipMemcpyDeviceToDevice, ctx->stream),
+                  "hipMemcpyAsync(C.jc)");
+      if (rc == CBH_OK)
+        rc = hip_rc(ctx, hipMemcpyAsync(out->cp, Ccp, sizeof(int64_t) * (ncols + 1), hipMemcpyDeviceToDevice, ctx->stream),
+                    "hipMemcpyAsync(C.cp)");
+      if (rc == CBH_OK) rc = check_err(ctx);
     }
     if (rc != CBH_OK) {
       cbh_mat_free(ctx, out);
@@ -2530,19 +2605,26 @@ int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* p
 
 }  // extern "C"
 
-extern "C" int cbh_mat_checksum(cbh_ctx* ctx, const cbh_mat* M, double* value_sum, uint64_t* digest) {
+static int mat_checksum(cbh_ctx* ctx, const cbh_mat* M, int64_t row_off, int64_t col_off, const int64_t* col_pos,
+                        double* value_sum, uint64_t* digest) {
   if (!ctx || !M || !value_sum || !digest) return fail(ctx, CBH_E_ARG, "null argument");
   Scratch S(ctx);
   double* d_sum;
   unsigned long long* d_dig;
+  int64_t* d_pos = nullptr;
   CBH_TRY(S.get(&d_sum, 1));
   CBH_TRY(S.get(&d_dig, 1));
+  if (col_pos && M->nzc > 0) {
+    CBH_TRY(S.get(&d_pos, M->nzc));
+    CBH_HIP(ctx, hipMemcpyAsync(d_pos, col_pos, sizeof(int64_t) * M->nzc, hipMemcpyHostToDevice, ctx->stream));
+  }
   CBH_HIP(ctx, hipMemsetAsync(d_sum, 0, sizeof(double), ctx->stream));
   CBH_HIP(ctx, hipMemsetAsync(d_dig, 0, sizeof(unsigned long long), ctx->stream));
   auto run = [&](auto tag) {
     using VT = decltype(tag);
     hipLaunchKernelGGL(checksum_kernel<VT>, dim3(blocks_for(M->nzc, 4)), dim3(256), 0, ctx->stream, M->jc, M->cp,
-                       (int64_t)0, M->nzc, M->ir, reinterpret_cast<const VT*>(M->num), (int64_t)0, d_sum, d_dig);
+                       (int64_t)0, M->nzc, M->ir, reinterpret_cast<const VT*>(M->num), (int64_t)0, d_sum, d_dig, d_pos,
+                       row_off, col_off);
   };
   if (M->nzc > 0) {
     switch (M->dtype) {
@@ -2563,6 +2645,16 @@ extern "C" int cbh_mat_checksum(cbh_ctx* ctx, const cbh_mat* M, double* value_su
   *value_sum = hs;
   *digest = hd;
   return CBH_OK;
+}
+
+extern "C" int cbh_mat_checksum(cbh_ctx* ctx, const cbh_mat* M, double* value_sum, uint64_t* digest) {
+  return mat_checksum(ctx, M, 0, 0, nullptr, value_sum, digest);
+}
+
+extern "C" int cbh_mat_checksum_global(cbh_ctx* ctx, const cbh_mat* M, int64_t row_off, int64_t col_off,
+                                       const int64_t* col_pos, double* value_sum, uint64_t* digest) {
+  if (!col_pos && M && M->nzc > 0) return fail(ctx, CBH_E_ARG, "checksum_global: col_pos is required");
+  return mat_checksum(ctx, M, row_off, col_off, col_pos, value_sum, digest);
 }
 
 extern "C" int cbh_transpose(cbh_ctx* ctx, const cbh_mat* A, cbh_mat** AT) {

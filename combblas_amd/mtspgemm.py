@@ -32,19 +32,37 @@ def _spgemm(SR: Semiring, A: SpDCCols, B: SpDCCols, clearA, clearB, flags=0) -> 
     return C
 
 
-def LocalHybridSpGEMM(SR: Semiring, A: SpDCCols, B: SpDCCols, clearA=False, clearB=False, aux=None) -> SpDCCols:
-    """mtSpGEMM.h:213-460 -- C = A*B, rows ascending within each column."""
-    return _spgemm(SR, A, B, clearA, clearB)
+# cbh_spgemm's reference-order flags (combblas_hip.h): every output re-folded in the named kernel's order
+CBH_ORDER_HYBRID, CBH_ORDER_HEAP, CBH_ORDER_HASH = 0x200, 0x400, 0x800
 
 
-def LocalSpGEMMHash(SR: Semiring, A: SpDCCols, B: SpDCCols, clearA=False, clearB=False, sort=True) -> SpDCCols:
-    """mtSpGEMM.h:463-656 (sort=False is satisfied by the sorted result)."""
-    return _spgemm(SR, A, B, clearA, clearB)
+def _order(order, flag):
+    if order in (None, "arrival"):
+        return 0
+    if order == "reference":
+        return flag
+    raise ValueError(f"order must be None, 'arrival' or 'reference', not {order!r}")
 
 
-def LocalSpGEMM(SR: Semiring, A: SpDCCols, B: SpDCCols, clearA=False, clearB=False) -> SpDCCols:
-    """mtSpGEMM.h:74-202 (heap SpGEMM) -- same numeric contract as the hybrid."""
-    return _spgemm(SR, A, B, clearA, clearB)
+def LocalHybridSpGEMM(SR: Semiring, A: SpDCCols, B: SpDCCols, clearA=False, clearB=False, aux=None,
+                      order=None) -> SpDCCols:
+    """mtSpGEMM.h:213-460 -- C = A*B, rows ascending within each column. order="reference": every
+    output folded in the reference's own order (heap branch for cr < 2, hash branch otherwise), so
+    floating-point sums are bit-identical to the stock kernel's; default: arrival order."""
+    return _spgemm(SR, A, B, clearA, clearB, _order(order, CBH_ORDER_HYBRID))
+
+
+def LocalSpGEMMHash(SR: Semiring, A: SpDCCols, B: SpDCCols, clearA=False, clearB=False, sort=True,
+                    order=None) -> SpDCCols:
+    """mtSpGEMM.h:463-656 (sort=False is satisfied by the sorted result); order="reference": the
+    hash kernel's fold order (products in B-entry order, add(new, old))."""
+    return _spgemm(SR, A, B, clearA, clearB, _order(order, CBH_ORDER_HASH))
+
+
+def LocalSpGEMM(SR: Semiring, A: SpDCCols, B: SpDCCols, clearA=False, clearB=False, order=None) -> SpDCCols:
+    """mtSpGEMM.h:74-202 (heap SpGEMM) -- same numeric contract as the hybrid; order="reference":
+    the heap kernel's pop order (libstdc++ heap, add(old, new))."""
+    return _spgemm(SR, A, B, clearA, clearB, _order(order, CBH_ORDER_HEAP))
 
 
 def estimateFLOPandNNZ(A: SpDCCols, B: SpDCCols, per_column=False):

@@ -15,14 +15,16 @@
 // Input: the packed Graph500 R-MAT of the reference (DistEdgeList::GenGraph500Data, scramble,
 // edge factor 16; values = edge multiplicities as double), A and B separate copies.
 // Timing: `warmup` untimed steps, then exactly `steps` steps bracketed by device synchronize +
-// MPI_Barrier, max over ranks. Then one untimed verification step: nnz and value sum of C
-// (cbh_mat_checksum per block), summed over ranks. Rank 0 prints one JSON line.
+// MPI_Barrier, max over ranks. Then an untimed verification (verify_product): nnz, value sum and
+// the reference's order-sensitive digest of the whole product assembled from the ranks' pieces.
+// Rank 0 prints one JSON line.
 #include <mpi.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <memory>
 #include <string>
 #include <tuple>
@@ -95,20 +97,9 @@ static PMat make_input(int scale, int gr, int gc) {
   return PMat(new DCols(tup, false), grid);
 }
 
-struct Sums {  // this rank's share of C
-  int64_t nnz = 0;
-  double vsum = 0.0;
-};
-static void add_block(Sums& s, const DDev& blk, bool checksum) {
-  s.nnz += blk.getnnz();
-  if (checksum && blk.getnnz() > 0) {
-    double v = 0;
-    uint64_t d = 0;
-    const int rc = cbh_mat_checksum(combblas_hip::context(), blk.mat(), &v, &d);
-    if (rc != CBH_OK) combblas_hip::die(combblas_hip::context(), rc, "cbh_mat_checksum");
-    s.vsum += v;
-  }
-}
+// A final piece of this rank's share of C: the block and the offset of its first column inside the
+// rank's column range (2D: the rank's block of C; 3D: its fiber chunk of the layer block)
+typedef std::function<void(cbh_mat*, int64_t)> Consumer;
 
 // phases such that every phase's partials and its merge / exchange output (3 x 12 bytes per
 // entry of the largest local product) fit in half the free HBM of the tightest rank
@@ -127,25 +118,20 @@ static int plan_phases(int64_t local_nnz) {
 // columns with the stage partials merged (2D: MemEfficientSpGEMM's loop, ParFriends.h:449-730,
 // without the prune) or the layer partial fiber-reduce-scattered (3D: MemEfficientSpGEMM3D's loop,
 // :3214-3705 -- phase p = piece p of each of the L column chunks of B's layer block).
-static Sums phased_step(DDev& Aloc, CommGrid* GA, DDev& Bloc, CommGrid* GB, CommGrid3D* g3, const std::vector<int64_t>& div3,
-                        int& phases, bool checksum) {
+static void phased_step(DDev& Aloc, CommGrid* GA, DDev& Bloc, CommGrid* GB, CommGrid3D* g3, const std::vector<int64_t>& div3,
+                        int& phases, const Consumer& consume) {
   const cbh_semiring sr = combblas_hip::semiring_traits<PTDD>::code;
   const int dt = combblas_hip::dtype_of<double>::value;
-  Sums s;
   combblas_hip::StagePlans<int64_t, double, double> SP(Aloc, GA, Bloc, GB);
   if (phases <= 0) phases = plan_phases(SP.nnz);
-  auto consume = [&](cbh_mat* C) {
-    DDev blk(C);  // frees the piece
-    add_block(s, blk, checksum);
-  };
   if (!g3) {
     const int64_t n = Bloc.getncol();
     const auto cuts = phases == 1 ? std::vector<int64_t>{0, n}
                                   : combblas_hip::balanced_cuts(SP.col_nnz(n, SP.GridC->GetColWorld()), phases);
-    for (size_t p = 0; p + 1 < cuts.size(); ++p) consume(SP.piece(sr, dt, 8, cuts[p], cuts[p + 1]));
-    return s;
+    for (size_t p = 0; p + 1 < cuts.size(); ++p) consume(SP.piece(sr, dt, 8, cuts[p], cuts[p + 1]), cuts[p]);
+    return;
   }
-  const int L = (int)div3.size();
+  const int L = (int)div3.size(), me = g3->GetRankInFiber();
   std::vector<std::vector<int64_t>> piece(L);
   int64_t c0 = 0;
   for (int c = 0; c < L; ++c) {
@@ -161,9 +147,111 @@ static Sums phased_step(DDev& Aloc, CommGrid* GA, DDev& Bloc, CommGrid* GB, Comm
       lb[c] = piece[c][p + 1] - piece[c][p];
     }
     cbh_mat* P = combblas_hip::col_concat(parts);
-    consume(combblas_hip::fiber_reduce_scatter(sr, P, lb, g3->GetFiberWorld(), dt, 8));
+    consume(combblas_hip::fiber_reduce_scatter(sr, P, lb, g3->GetFiberWorld(), dt, 8), piece[me][p] - piece[me][0]);
   }
+}
+
+static int64_t exscan_i64(int64_t v, MPI_Comm comm) {
+  int64_t out = 0;
+  MPI_Exscan(&v, &out, 1, MPI_INT64_T, MPI_SUM, comm);
+  int r = 0;
+  MPI_Comm_rank(comm, &r);
+  return r == 0 ? 0 : out;
+}
+
+// Where this rank's share of C sits in the whole product: the first global row and column of its
+// column range, its column count, and the communicator of the ranks holding the same columns
+// (ordered by their rows: the processor column of the 2D grid, or of the layer grid for one fiber
+// chunk in 3D)
+struct Share {
+  int64_t row_off = 0, col_off = 0, ncols = 0;
+  MPI_Comm colcomm = MPI_COMM_NULL;
+};
+static Share share_of(DDev& Aloc, CommGrid* GA, DDev& Bloc, CommGrid* GB, CommGrid3D* g3, const std::vector<int64_t>& div3) {
+  Share s;
+  s.row_off = exscan_i64(Aloc.getnrow(), GA->GetColWorld());  // C's rows are A's block rows
+  s.col_off = exscan_i64(Bloc.getncol(), GB->GetRowWorld());
+  s.ncols = Bloc.getncol();
+  int color = GB->GetRankInProcRow();
+  if (g3) {
+    const int me = g3->GetRankInFiber(), L = (int)div3.size();
+    for (int c = 0; c < me; ++c) s.col_off += div3[c];
+    s.ncols = div3[me];
+    color = color * L + me;
+  }
+  // ranks with the same column range: same processor column (and fiber chunk); key = row offset
+  MPI_Comm_split(MPI_COMM_WORLD, color, (int)std::min<int64_t>(s.row_off, INT32_MAX), &s.colcomm);
   return s;
+}
+
+// The reference's order-sensitive digest of the WHOLE product from the distributed pieces
+// (tests/golden/make_golden_s22.py's definition; cbh_mat_checksum_global): every entry's position
+// in C's global DCSC order is (entries of the global columns before its column) + (entries of its
+// column in the row ranges above this rank's) + (its index in the piece's column). Pass 1 counts
+// the entries per column of this rank's range, the collective sums place every column's first
+// entry, pass 2 digests the pieces of a second run of the product.
+struct Verify {
+  int64_t nnz = 0;
+  double vsum = 0;
+  uint64_t digest = 0;
+};
+static Verify verify_product(const std::function<void(const Consumer&)>& product, const Share& sh) {
+  cbh_ctx* ctx = combblas_hip::context();
+  Verify v;
+  std::vector<int64_t> cnt((size_t)sh.ncols, 0);
+  product([&](cbh_mat* M, int64_t rel) {
+    DDev blk(M);  // frees the piece
+    const int64_t nzc = blk.getnzc();
+    v.nnz += blk.getnnz();
+    if (blk.getnnz() == 0) return;
+    double vs = 0;
+    uint64_t dg = 0;
+    int rc = cbh_mat_checksum(ctx, M, &vs, &dg);
+    if (rc != CBH_OK) combblas_hip::die(ctx, rc, "cbh_mat_checksum");
+    v.vsum += vs;
+    std::vector<int64_t> cp((size_t)nzc + 1), jc((size_t)nzc);
+    rc = cbh_mat_copy_out(ctx, M, cp.data(), jc.data(), nullptr, nullptr, 0);
+    if (rc != CBH_OK) combblas_hip::die(ctx, rc, "cbh_mat_copy_out");
+    for (int64_t k = 0; k < nzc; ++k) cnt[(size_t)(rel + jc[k])] += cp[k + 1] - cp[k];
+  });
+  // column starts: rows above (exclusive scan over the column communicator), column totals, and the
+  // entries of every column range left of this one (one leader per range)
+  std::vector<int64_t> above((size_t)sh.ncols, 0), tot((size_t)sh.ncols, 0);
+  int crank = 0;
+  MPI_Comm_rank(sh.colcomm, &crank);
+  MPI_Exscan(cnt.data(), above.data(), (int)sh.ncols, MPI_INT64_T, MPI_SUM, sh.colcomm);
+  if (crank == 0) std::fill(above.begin(), above.end(), 0);
+  MPI_Allreduce(cnt.data(), tot.data(), (int)sh.ncols, MPI_INT64_T, MPI_SUM, sh.colcomm);
+  int64_t range_total = 0;
+  for (int64_t t : tot) range_total += t;
+  int np = 1;
+  MPI_Comm_size(MPI_COMM_WORLD, &np);
+  int64_t mine[3] = {sh.col_off, range_total, crank == 0 ? 1 : 0};
+  std::vector<int64_t> all(3 * (size_t)np);
+  MPI_Allgather(mine, 3, MPI_INT64_T, all.data(), 3, MPI_INT64_T, MPI_COMM_WORLD);
+  int64_t base = 0;
+  for (int r = 0; r < np; ++r)
+    if (all[3 * r + 2] && all[3 * r] < sh.col_off) base += all[3 * r + 1];
+  std::vector<int64_t> start((size_t)sh.ncols);
+  for (int64_t j = 0; j < sh.ncols; ++j) {
+    start[(size_t)j] = base + above[(size_t)j];
+    base += tot[(size_t)j];
+  }
+  product([&](cbh_mat* M, int64_t rel) {
+    DDev blk(M);
+    const int64_t nzc = blk.getnzc();
+    if (blk.getnnz() == 0) return;
+    std::vector<int64_t> jc((size_t)nzc), pos((size_t)nzc);
+    int rc = cbh_mat_copy_out(ctx, M, nullptr, jc.data(), nullptr, nullptr, 0);
+    if (rc != CBH_OK) combblas_hip::die(ctx, rc, "cbh_mat_copy_out");
+    for (int64_t k = 0; k < nzc; ++k) pos[(size_t)k] = start[(size_t)(rel + jc[k])];
+    double vs = 0;
+    uint64_t dg = 0;
+    rc = cbh_mat_checksum_global(ctx, M, sh.row_off, sh.col_off + rel, pos.data(), &vs, &dg);
+    if (rc != CBH_OK) combblas_hip::die(ctx, rc, "cbh_mat_checksum_global");
+    v.digest += dg;
+  });
+  return v;
 }
 
 int main(int argc, char** argv) {
@@ -211,20 +299,20 @@ int main(int argc, char** argv) {
     const double setup_s = MPI_Wtime() - tg;
     // one product. 2D with one phase: the reference's PSpGEMM itself (-> the device
     // Mult_AnXBn_Synch of SpParMatDev.h); otherwise the phased loop above
-    auto product = [&](bool checksum) {
+    auto product = [&](const Consumer& consume) {
       if (twod && phases == 1) {
-        Sums s;
         DMat C = PSpGEMM<PTDD>(*Ad, *Bd);
-        add_block(s, C.seq(), checksum);
-        return s;
+        consume(C.seq().release(), 0);
+        return;
       }
       if (twod)
         return phased_step(Ad->seq(), Ad->getcommgrid().get(), Bd->seq(), Bd->getcommgrid().get(), nullptr, div3,
-                           phases, checksum);
+                           phases, consume);
       return phased_step(*A3d->GetLayerMat()->seqptr(), A3d->GetLayerMat()->getcommgrid().get(),
                          *B3d->GetLayerMat()->seqptr(), B3d->GetLayerMat()->getcommgrid().get(),
-                         A3d->getcommgrid3D().get(), div3, phases, checksum);
+                         A3d->getcommgrid3D().get(), div3, phases, consume);
     };
+    const Consumer discard = [](cbh_mat* M, int64_t) { cbh_mat_free(combblas_hip::context(), M); };
     if (phases <= 0) {  // plan the phase count once (a symbolic pass), outside the timed region
       std::unique_ptr<combblas_hip::StagePlans<int64_t, double, double>> SP;
       if (twod)
@@ -237,14 +325,14 @@ int main(int argc, char** argv) {
       phases = plan_phases(SP->nnz);  // with the plans (and their stored bitmaps) still resident
     }
     if (myrank == 0) std::fprintf(stderr, "[bench_summa] setup %.1f s, %d phase(s); warm-up\n", setup_s, phases);
-    for (int w = 0; w < warmup; ++w) product(false);
+    for (int w = 0; w < warmup; ++w) product(discard);
     cbh_ctx_synchronize(combblas_hip::context());
     cbh_ctx_enable_timing(combblas_hip::context(), 1);  // per-kind HIP-event totals of the timed steps
     cbh_kernel_stats_reset(combblas_hip::context());
     if (myrank == 0) std::fprintf(stderr, "[bench_summa] %d timed step(s)\n", steps);
     MPI_Barrier(MPI_COMM_WORLD);
     const double t0 = MPI_Wtime();
-    for (int k = 0; k < steps; ++k) product(false);
+    for (int k = 0; k < steps; ++k) product(discard);
     cbh_ctx_synchronize(combblas_hip::context());
     MPI_Barrier(MPI_COMM_WORLD);
     double dt = (MPI_Wtime() - t0) / std::max(steps, 1), mx = 0;
@@ -264,20 +352,31 @@ int main(int argc, char** argv) {
       }
     }
     if (myrank == 0) std::fprintf(stderr, "[bench_summa] %.1f ms/step; verification step\n", mx * 1e3);
-    const Sums v = product(true);  // verification (untimed)
+    // verification (untimed, two runs of the product): nnz, value sum and the whole product's digest
+    const Share sh = twod ? share_of(Ad->seq(), Ad->getcommgrid().get(), Bd->seq(), Bd->getcommgrid().get(), nullptr, div3)
+                          : share_of(*A3d->GetLayerMat()->seqptr(), A3d->GetLayerMat()->getcommgrid().get(),
+                                     *B3d->GetLayerMat()->seqptr(), B3d->GetLayerMat()->getcommgrid().get(),
+                                     A3d->getcommgrid3D().get(), div3);
+    const Verify v = verify_product(product, sh);
     cbh_ctx_synchronize(combblas_hip::context());
     int64_t nnz = 0;
     double vsum = 0;
     MPI_Allreduce(&v.nnz, &nnz, 1, MPI_INT64_T, MPI_SUM, MPI_COMM_WORLD);
     MPI_Allreduce(&v.vsum, &vsum, 1, MPI_DOUBLE, MPI_SUM, MPI_COMM_WORLD);
+    std::vector<uint64_t> digs((size_t)nprocs);  // summed mod 2^64 on rank 0 (MPI_SUM on unsigned may not wrap)
+    MPI_Gather(&v.digest, 1, MPI_UINT64_T, digs.data(), 1, MPI_UINT64_T, 0, MPI_COMM_WORLD);
+    uint64_t digest = 0;
+    for (uint64_t d : digs) digest += d;
+    MPI_Comm colcomm = sh.colcomm;
+    MPI_Comm_free(&colcomm);
     if (myrank == 0) {
       const char* drv = twod ? (phases == 1 ? "PSpGEMM -> Mult_AnXBn_Synch (SpParMatDev.h)"
                                             : "MemEfficientSpGEMM phase loop without prune (ParFriendsDev.h StagePlans)")
                              : "MemEfficientSpGEMM3D phase loop without prune (layer SUMMA + fiber reduce-scatter)";
       std::printf("{\"ms_per_step\": %.3f, \"steps\": %d, \"warmup\": %d, \"ranks\": %d, \"grid\": \"%s\", "
-                  "\"driver\": \"%s\", \"phases\": %d, \"nnzC\": %lld, \"value_sum\": %.1f, \"setup_s\": %.3f, "
+                  "\"driver\": \"%s\", \"phases\": %d, \"nnzC\": %lld, \"value_sum\": %.1f, \"digest\": \"%llu\", \"setup_s\": %.3f, "
                   "\"transport\": \"%s\", \"kernel_stats_rank0\": {%s}}\n",
-                  mx * 1e3, steps, warmup, nprocs, grid, drv, phases, (long long)nnz, vsum, setup_s,
+                  mx * 1e3, steps, warmup, nprocs, grid, drv, phases, (long long)nnz, vsum, (unsigned long long)digest, setup_s,
                   combblas_hip::use_mpi_transport() ? "mpi (host staged)" : "rccl", kstats.c_str());
       std::fflush(stdout);
     }

@@ -68,6 +68,15 @@ typedef enum cbh_dtype {
 /* cbh_spgemm flags */
 #define CBH_SORTED_ROWS 0x1u   /* rows sorted within each column (LocalHybridSpGEMM, LocalSpGEMMHash sort=true) */
 #define CBH_KEEP_EMPTY_COLS 0x2u /* keep C columns of B's nzc even when empty (SpTuples view); default drops them (DCSC) */
+/* Reference-order accumulation (device/order_kernel.h): after the throughput pass, every output is
+ * re-folded in exactly the order the reference folds it, so floating-point sums (and any
+ * non-commutative add) are bit-identical to the stock kernel's: CBH_ORDER_HYBRID follows
+ * LocalHybridSpGEMM (heap branch for columns with cr = flops / nnz < 2, hash branch otherwise,
+ * mtSpGEMM.h:310), CBH_ORDER_HEAP LocalSpGEMM, CBH_ORDER_HASH LocalSpGEMMHash. Without them the
+ * products of one output are summed in arrival order (exact for integer, bool, min and max). */
+#define CBH_ORDER_HYBRID 0x200u
+#define CBH_ORDER_HEAP 0x400u
+#define CBH_ORDER_HASH 0x800u
 
 /* ---------------------------------------------------------------- matrices
  * A local sparse block in DCSC form (combblas::Dcsc: cp[nzc+1], jc[nzc], ir[nnz], numx[nnz]).
@@ -86,6 +95,13 @@ typedef struct cbh_mat cbh_mat; /* a device-resident DCSC block */
 
 int cbh_ctx_create(int device, cbh_ctx** ctx);
 int cbh_ctx_destroy(cbh_ctx* ctx);
+/* Visible HIP devices (CBH_E_NODEVICE when none) and the PCI bus id of one ("0000:xx:00.0"): the
+ * C++ adaptors resolve a rank's device with them and check that node-local RCCL peers hold
+ * distinct devices (HipSpGEMM.h context(), SpParMatDev.h rccl_comm_for). */
+int cbh_device_count(int* n);
+int cbh_device_pci_id(int device, char* buf, int len);
+/* The device a context drives. */
+int cbh_ctx_device(cbh_ctx* ctx, int* device);
 /* Use an existing hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = own stream. */
 int cbh_ctx_set_stream(cbh_ctx* ctx, void* hip_stream);
 void* cbh_ctx_stream(cbh_ctx* ctx);
@@ -97,6 +113,12 @@ int cbh_ctx_trim(cbh_ctx* ctx);
  * first (all of them if fewer are cached); live blocks and the phase workspace stay. */
 int cbh_ctx_release(cbh_ctx* ctx, int64_t bytes);
 const char* cbh_last_error(cbh_ctx* ctx);
+/* Device scratch from the context's allocator (its block cache, and on OOM its fallback of
+ * returning cached blocks to HIP), stream-ordered on the context's stream: the caller's kernels
+ * that use it must run on that stream (cbh_ctx_stream), and cbh_ctx_free may be called as soon as
+ * they are enqueued. */
+int cbh_ctx_alloc(cbh_ctx* ctx, int64_t bytes, void** ptr);
+int cbh_ctx_free(cbh_ctx* ctx, void* ptr);
 /* Sub-tiles the task kernels retried with half the row range (table overflow, commit queue) since
  * the last call; resets the counter (diagnostics and tests). */
 int cbh_ctx_take_retries(cbh_ctx* ctx, int64_t* subtile_retries);
@@ -299,6 +321,12 @@ int cbh_transpose(cbh_ctx* ctx, const cbh_mat* A, cbh_mat** AT);
  * CBH_PHASE_CHECKSUM and the oracle use: sum over entries p (in DCSC order) of
  * mix64(p ^ mix64(col ^ mix64(row ^ mix64(value bits)))) mod 2^64. Built-in dtypes only.        */
 int cbh_mat_checksum(cbh_ctx* ctx, const cbh_mat* M, double* value_sum, uint64_t* digest);
+/* The same for one block of a distributed C: its rows and column ids are offset by row_off /
+ * col_off, and col_pos (host, M's nzc entries) holds the position of each nonzero column's first
+ * entry in the WHOLE product's DCSC order, so that the blocks' digests sum (mod 2^64) to the
+ * whole product's (bench_summa checks the N-rank product against the reference's digest). */
+int cbh_mat_checksum_global(cbh_ctx* ctx, const cbh_mat* M, int64_t row_off, int64_t col_off, const int64_t* col_pos,
+                            double* value_sum, uint64_t* digest);
 /* C = A .* B (SpParMat::EWiseMult(B, false) -> Friends.h:834-887): intersection, values A*B. */
 int cbh_ewise_mult(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, cbh_mat** C);
 /* HipMCL column operations on f64 blocks (ParFriends.h:185-353). Vectors are device arrays over

@@ -71,18 +71,50 @@ inline void die(cbh_ctx* ctx, int rc, const char* what) {
   MPI_Abort(MPI_COMM_WORLD, rc);
 }
 
-// One context per process (one rank drives one GPU, CommGrid semantics). Device = local rank
-// modulo visible devices unless COMBBLAS_HIP_DEVICE is set.
+// One context per process (one rank drives one GPU, CommGrid semantics). The device is
+// COMBBLAS_HIP_DEVICE when set, else the node-local rank (LOCAL_RANK, MPI_LOCALRANKID,
+// OMPI_COMM_WORLD_LOCAL_RANK). A device that cannot be opened is fatal: no silent fallback to
+// GPU 0, where a mis-set rank would share a device with another rank (RCCL refuses that). More
+// local ranks than devices is allowed only as an explicit rehearsal -- COMBBLAS_HIP_SHARE_DEVICE=1
+// or the host-staged transport COMBBLAS_HIP_COMM=mpi -- and then maps local rank modulo devices.
+// The RCCL transport also checks that the members of each communicator on one node hold distinct
+// devices (SpParMatDev.h, rccl_comm_for).
+inline bool device_sharing_allowed() {
+  const char* s = std::getenv("COMBBLAS_HIP_SHARE_DEVICE");
+  const char* c = std::getenv("COMBBLAS_HIP_COMM");
+  return (s && std::atoi(s) != 0) || (c && std::strcmp(c, "mpi") == 0);
+}
+inline int local_rank_env() {
+  for (const char* k : {"LOCAL_RANK", "MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK"})
+    if (const char* v = std::getenv(k)) return std::atoi(v);
+  return 0;
+}
 inline cbh_ctx* context() {
   static cbh_ctx* ctx = nullptr;
   if (!ctx) {
-    int dev = 0;
-    if (const char* e = std::getenv("COMBBLAS_HIP_DEVICE")) dev = std::atoi(e);
-    else if (const char* l = std::getenv("LOCAL_RANK")) dev = std::atoi(l);
-    else if (const char* m = std::getenv("MPI_LOCALRANKID")) dev = std::atoi(m);
+    int ndev = 0;
+    if (cbh_device_count(&ndev) != CBH_OK) die(nullptr, CBH_E_NODEVICE, "cbh_device_count (no GPU)");
+    int dev;
+    if (const char* e = std::getenv("COMBBLAS_HIP_DEVICE")) {
+      dev = std::atoi(e);
+    } else {
+      dev = local_rank_env();
+      if (dev >= ndev) {
+        if (!device_sharing_allowed()) {
+          std::fprintf(stderr,
+                       "combblas_hip: node-local rank %d but only %d visible GPU(s); set COMBBLAS_HIP_DEVICE, or "
+                       "COMBBLAS_HIP_SHARE_DEVICE=1 to share devices (host-staged rehearsals only)\n",
+                       dev, ndev);
+          MPI_Abort(MPI_COMM_WORLD, CBH_E_NODEVICE);
+        }
+        dev %= ndev;
+      }
+    }
     int rc = cbh_ctx_create(dev, &ctx);
-    if (rc != CBH_OK) rc = cbh_ctx_create(0, &ctx);
-    if (rc != CBH_OK) die(nullptr, rc, "cbh_ctx_create");
+    if (rc != CBH_OK) {
+      std::fprintf(stderr, "combblas_hip: cannot open GPU %d of %d\n", dev, ndev);
+      die(nullptr, rc, "cbh_ctx_create");
+    }
   }
   return ctx;
 }
@@ -335,10 +367,21 @@ inline cbh_mat* merge_all(cbh_semiring sr, std::vector<cbh_mat*> parts) {
   return parts[0];
 }
 
+// COMBBLAS_HIP_ORDER=reference (read per call): the built-in semirings also fold every output in
+// the reference's own order (cbh_spgemm's CBH_ORDER_* flags, device/order_kernel.h), so that
+// floating-point sums are bit-identical to the stock kernel named by `branch` -- 0
+// LocalHybridSpGEMM, 1 LocalSpGEMM (heap), 2 LocalSpGEMMHash (hash). Default: arrival order
+// (exact for integer, bool, min and max; f64 sums within the Higham bound).
+inline uint32_t order_flags(int branch) {
+  const char* e = std::getenv("COMBBLAS_HIP_ORDER");
+  if (!e || std::strcmp(e, "reference") != 0) return 0u;
+  return branch == 1 ? CBH_ORDER_HEAP : (branch == 2 ? CBH_ORDER_HASH : CBH_ORDER_HYBRID);
+}
+
 template <class SR, class NTO, class IT, class NT1, class NT2>
 combblas::SpTuples<IT, NTO>* LocalHybridSpGEMM(const combblas::SpDCCols<IT, NT1>& A,
                                                const combblas::SpDCCols<IT, NT2>& B, bool clearA, bool clearB,
-                                               IT* aux = nullptr) {
+                                               IT* aux = nullptr, int branch = 0) {
   static_assert(std::is_same<NT1, NTO>::value && std::is_same<NT2, NTO>::value,
                 "device path: input and output value types must match (T1 == T2 == T_promote)");
   (void)aux;
@@ -350,7 +393,7 @@ combblas::SpTuples<IT, NTO>* LocalHybridSpGEMM(const combblas::SpDCCols<IT, NT1>
     MatGuard a, b, c;
     a.m = upload(A);
     b.m = upload(B);
-    int rc = cbh_spgemm(context(), semiring_traits<SR>::code, a.m, b.m, CBH_SORTED_ROWS, &c.m);
+    int rc = cbh_spgemm(context(), semiring_traits<SR>::code, a.m, b.m, CBH_SORTED_ROWS | order_flags(branch), &c.m);
     if (rc != CBH_OK) die(context(), rc, "cbh_spgemm");
     out = download_tuples<IT, NTO>(c.m);
   }
@@ -364,13 +407,13 @@ combblas::SpTuples<IT, NTO>* LocalSpGEMMHash(const combblas::SpDCCols<IT, NT1>& 
                                              const combblas::SpDCCols<IT, NT2>& B, bool clearA, bool clearB,
                                              bool sort = true) {
   (void)sort;  // ascending rows are a valid order for the unsorted contract
-  return combblas_hip::LocalHybridSpGEMM<SR, NTO>(A, B, clearA, clearB);
+  return combblas_hip::LocalHybridSpGEMM<SR, NTO>(A, B, clearA, clearB, (IT*)nullptr, 2);
 }
 
 template <class SR, class NTO, class IT, class NT1, class NT2>
 combblas::SpTuples<IT, NTO>* LocalSpGEMM(const combblas::SpDCCols<IT, NT1>& A, const combblas::SpDCCols<IT, NT2>& B,
                                          bool clearA, bool clearB) {
-  return combblas_hip::LocalHybridSpGEMM<SR, NTO>(A, B, clearA, clearB);
+  return combblas_hip::LocalHybridSpGEMM<SR, NTO>(A, B, clearA, clearB, (IT*)nullptr, 1);
 }
 
 template <class SR, class IT, class NT>
@@ -490,7 +533,7 @@ combblas::SpParMat<IU, NU, combblas::SpDCCols<IU, NU>> mult_synch_host(
       b.m = upload(*BRecv);
       const double t1 = now_s();
       cbh_mat* Ci = nullptr;
-      int rc = cbh_spgemm(context(), semiring_traits<SR>::code, a.m, b.m, CBH_SORTED_ROWS, &Ci);
+      int rc = cbh_spgemm(context(), semiring_traits<SR>::code, a.m, b.m, CBH_SORTED_ROWS | order_flags(0), &Ci);
       if (rc != CBH_OK) die(context(), rc, "cbh_spgemm");
       T.upload += t1 - t0;
       T.kernel += now_s() - t1;

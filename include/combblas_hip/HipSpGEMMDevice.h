@@ -18,28 +18,52 @@
 // The semiring-independent half (symbolic pass, task plan, binning, C's allocation, column
 // compaction) runs in libcombblas_hip.so through the cbh_plan_* C-ABI (include/combblas_hip.h).
 //
-// Exact-parity note: the throughput kernels accumulate the products of one output in arrival
-// order, so a semiring whose add is commutative and associative (integers, bool, min/max, structs
-// of such) matches the reference bit for bit. A semiring marked reference_order (below: the
-// reference's Select2ndSRing; any application semiring it specializes) instead runs the
-// reference's own per-column algorithm on the device -- heap branch for cr < 2 with libstdc++'s
-// heap order and add(old, new), hash branch otherwise with add(new, old) in B-entry order
-// (mtSpGEMM.h:311-437, device/order_kernel.h) -- so even a non-commutative add, or floating-point
-// sums, match the stock path bit for bit. That pass walks a column per thread: a correctness
-// path, not the throughput one.
+// Exact-parity contract: the throughput kernels accumulate the products of one output in arrival
+// order, which is exact only when add is commutative and associative on the values (integers,
+// bool, min / max). Arrival order is therefore OPT-IN: a semiring runs in it only when
+// arrival_order_ok<SR> says so -- true for the built-in PlusTimes / SelectMax / MinPlus over
+// integer and bool values and for SelectMax / MinPlus over floating values; an application marks
+// its own commutative semiring with
+//   template <> struct combblas_hip::arrival_order_ok<MySR> : std::true_type {};
+// Every other semiring -- any unmarked user semiring, PlusTimes over float / double, the
+// reference's Select2ndSRing -- gets the reference's own accumulation order on the device: after
+// the throughput pass, every output is re-folded as LocalHybridSpGEMM folds it (heap branch for
+// cr < 2 with libstdc++'s heap order and add(old, new), a thread per column; hash branch
+// otherwise, add(new, old) in B-entry order, a wave per task; mtSpGEMM.h:311-437,
+// device/order_kernel.h), so even a non-commutative add, or floating-point sums, match the stock
+// path bit for bit. reference_order<SR> forces that order for a semiring marked arrival_order_ok.
+// (Built-in semirings through COMBBLAS_HIP_INSTANTIATE run the library's kernels: arrival order
+// unless the caller passes cbh_spgemm's CBH_ORDER_* flags.)
 #pragma once
 
 #include "HipSpGEMM.h"
 
 namespace combblas_hip {
-// semirings computed in the reference's own accumulation order (device/order_kernel.h). An
-// application marks its own semiring with
-//   template <> struct combblas_hip::reference_order<MySR> : std::true_type {};
-// visible in both translation units (before COMBBLAS_HIP_DEVICE_KERNELS).
+template <class SR>
+struct arrival_order_ok : std::false_type {};
+template <class T1, class T2>
+struct arrival_order_ok<combblas::PlusTimesSRing<T1, T2>>
+    : std::integral_constant<bool, !std::is_floating_point<T1>::value && !std::is_floating_point<T2>::value> {};
+template <class T1, class T2>
+struct arrival_order_ok<combblas::SelectMaxSRing<T1, T2>> : std::true_type {};  // max: exact in any order
+template <class T1, class T2>
+struct arrival_order_ok<combblas::MinPlusSRing<T1, T2>> : std::true_type {};    // min: exact in any order
+// forces the reference's order for a semiring marked arrival_order_ok (visible in both
+// translation units, before COMBBLAS_HIP_DEVICE_KERNELS)
 template <class SR>
 struct reference_order : std::false_type {};
 template <class T1, class T2, class OUT>
 struct reference_order<combblas::Select2ndSRing<T1, T2, OUT>> : std::true_type {};  // add(x, y) = y
+// the order the device pass uses for SR over these value types (a PlusTimes sum in a floating
+// output type is not order-free, whatever SR's own template arguments say)
+template <class SR>
+struct is_plus_times : std::false_type {};
+template <class T1, class T2>
+struct is_plus_times<combblas::PlusTimesSRing<T1, T2>> : std::true_type {};
+template <class SR, class NT1, class NT2, class NTO>
+struct ordered_semiring
+    : std::integral_constant<bool, reference_order<SR>::value || !arrival_order_ok<SR>::value ||
+                                       (is_plus_times<SR>::value && std::is_floating_point<NTO>::value)> {};
 
 // defined in HipSpGEMMKernels.h, explicitly instantiated by COMBBLAS_HIP_DEVICE_KERNELS (hipcc).
 // branch: which reference kernel a reference_order semiring follows -- 0 LocalHybridSpGEMM (heap for

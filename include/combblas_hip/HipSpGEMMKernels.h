@@ -14,15 +14,18 @@
 
 namespace combblas_hip {
 
-// reference semiring type -> device functor
+// reference semiring type -> device functor; every semiring not known to be order-free runs in the
+// reference's accumulation order (ordered_semiring, HipSpGEMMDevice.h)
 template <class SR, class NT1, class NT2, class NTO>
 struct device_semiring {
-  using type = cbh::UserSRD<SR, NT1, NT2, NTO, reference_order<SR>::value>;
+  using type = cbh::UserSRD<SR, NT1, NT2, NTO, ordered_semiring<SR, NT1, NT2, NTO>::value>;
 };
 template <class T1, class T2, class NT1, class NT2, class NTO>
 struct device_semiring<combblas::PlusTimesSRing<T1, T2>, NT1, NT2, NTO> {
-  using type = typename std::conditional<std::is_same<NT1, NTO>::value && std::is_same<NT2, NTO>::value,
+  using base = typename std::conditional<std::is_same<NT1, NTO>::value && std::is_same<NT2, NTO>::value,
                                          cbh::PlusTimesD<NTO>, cbh::PlusTimesPromoteD<NT1, NT2, NTO>>::type;
+  using type = typename std::conditional<ordered_semiring<combblas::PlusTimesSRing<T1, T2>, NT1, NT2, NTO>::value,
+                                         cbh::Ordered<base>, base>::type;
 };
 
 // SelectMaxSRing / MinPlusSRing with NT1 != NT2: the reference's functions are host-only, so the
@@ -76,12 +79,29 @@ struct device_semiring<combblas::Select2ndSRing<T1, T2, OUT>, NT1, NT2, NTO> {
 };
 template <class T1, class T2, class NT1, class NT2, class NTO>
 struct device_semiring<combblas::SelectMaxSRing<T1, T2>, NT1, NT2, NTO> {
-  using type = SelectMaxPromoteD<NT1, NT2, NTO>;
+  using base = SelectMaxPromoteD<NT1, NT2, NTO>;
+  using type = typename std::conditional<ordered_semiring<combblas::SelectMaxSRing<T1, T2>, NT1, NT2, NTO>::value,
+                                         cbh::Ordered<base>, base>::type;
 };
 template <class T1, class T2, class NT1, class NT2, class NTO>
 struct device_semiring<combblas::MinPlusSRing<T1, T2>, NT1, NT2, NTO> {
-  using type = MinPlusPromoteD<NT1, NT2, NTO>;
+  using base = MinPlusPromoteD<NT1, NT2, NTO>;
+  using type = typename std::conditional<ordered_semiring<combblas::MinPlusSRing<T1, T2>, NT1, NT2, NTO>::value,
+                                         cbh::Ordered<base>, base>::type;
 };
+
+// returnedSAID (mtSpGEMM.h:337): the reference's heap branch drops a product for which the
+// semiring's multiply raised its "said" flag. A device multiply cannot raise a host flag, so a
+// semiring with a settable flag (returnedSAID(bool), Applications/TwitterEdge.h:261) is rejected at
+// compile time; one whose returnedSAID() is a plain query is checked once per call on the host.
+template <class SR, class = void>
+struct said_settable : std::false_type {};
+template <class SR>
+struct said_settable<SR, std::void_t<decltype(SR::returnedSAID(true))>> : std::true_type {};
+template <class SR, class = void>
+struct said_query : std::false_type {};
+template <class SR>
+struct said_query<SR, std::void_t<decltype(SR::returnedSAID())>> : std::true_type {};
 
 // C = A*B on the device for any (SR, NT1, NT2, NTO): library plan + caller-instantiated kernels.
 template <class SR, class NTO, class IT, class NT1, class NT2>
@@ -90,6 +110,11 @@ combblas::SpTuples<IT, NTO>* DeviceLocalSpGEMM(const combblas::SpDCCols<IT, NT1>
                                                int branch) {
   using DSR = typename device_semiring<SR, NT1, NT2, NTO>::type;
   static_assert(std::is_trivially_copyable<NTO>::value, "device values must be trivially copyable");
+  static_assert(!said_settable<SR>::value,
+                "combblas_hip: a semiring whose multiply sets a returnedSAID flag (mtSpGEMM.h:337) cannot run on "
+                "the device (its multiply would have to raise a host flag per product)");
+  if constexpr (said_query<SR>::value)
+    if (SR::returnedSAID()) die(nullptr, CBH_E_ARG, "returnedSAID() is true before the product (mtSpGEMM.h:337)");
   const IT mdim = A.getnrow(), ndim = B.getncol();
   combblas::SpTuples<IT, NTO>* out;
   if (A.isZero() || B.isZero()) {
@@ -111,12 +136,18 @@ combblas::SpTuples<IT, NTO>* DeviceLocalSpGEMM(const combblas::SpDCCols<IT, NT1>
     cbh_mat_device_arrays(c.m, &cp, &jc, &ir, &num);
     int64_t nnzC = 0;
     cbh_mat_info(c.m, nullptr, nullptr, &nnzC, nullptr, nullptr);
-    hipError_t e;
-    if constexpr (cbh::sr_ordered<DSR>::value)  // the reference's own per-column order
-      e = cbh::run_numeric_plan_ordered<DSR>(np, const_cast<int32_t*>(ir), const_cast<void*>(num), nnzC,
-                                              (int64_t)B.getnnz(), branch);
-    else
-      e = cbh::run_numeric_plan<DSR>(np, const_cast<int32_t*>(ir), const_cast<void*>(num), nnzC);
+    hipError_t e = cbh::run_numeric_plan<DSR>(np, const_cast<int32_t*>(ir), const_cast<void*>(num), nnzC);
+    if constexpr (cbh::sr_ordered<DSR>::value) {  // then every output re-folded in the reference's own order
+      if (e == hipSuccess) {
+        void* scratch = nullptr;
+        const int64_t nnzB = (int64_t)B.getnnz();
+        rc = cbh_ctx_alloc(ctx, (int64_t)cbh::ord_scratch_bytes<DSR>(nnzB, np.ntasks, nnzC), &scratch);
+        if (rc != CBH_OK) die(ctx, rc, "cbh_ctx_alloc (reference-order scratch)");
+        cbh::TaskArgs ta = cbh::numeric_args(np, 0, const_cast<int32_t*>(ir), const_cast<void*>(num), nnzC);
+        e = cbh::launch_reference_order<DSR>(ta, scratch, nnzB, nnzC, branch, reinterpret_cast<hipStream_t>(np.stream));
+        cbh_ctx_free(ctx, scratch);  // stream-ordered: the launches above run first
+      }
+    }
     if (e != hipSuccess) {
       std::fprintf(stderr, "combblas_hip: numeric launch failed: %s\n", hipGetErrorString(e));
       MPI_Abort(MPI_COMM_WORLD, CBH_E_HIP);

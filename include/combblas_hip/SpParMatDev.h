@@ -199,12 +199,62 @@ inline std::vector<int> world_ranks(MPI_Comm comm) {
   MPI_Group_free(&wg);
   return out;
 }
+// The members of an RCCL communicator that share a node must drive distinct GPUs (RCCL refuses two
+// ranks on one device, and a rank whose device resolution went wrong would otherwise surface as an
+// RCCL error deep inside a product): the node's members gather their devices' PCI bus ids.
+inline void check_distinct_devices(MPI_Comm comm) {
+  MPI_Comm node;
+  MPI_Comm_split_type(comm, MPI_COMM_TYPE_SHARED, 0, MPI_INFO_NULL, &node);
+  int n = 1;
+  MPI_Comm_size(node, &n);
+  if (n > 1) {
+    int dev = -1;
+    cbh_ctx_device(context(), &dev);
+    char mine[32] = {0};
+    if (cbh_device_pci_id(dev, mine, (int)sizeof(mine)) != CBH_OK) std::snprintf(mine, sizeof(mine), "dev%d", dev);
+    std::vector<char> all(32 * (size_t)n);
+    MPI_Allgather(mine, 32, MPI_CHAR, all.data(), 32, MPI_CHAR, node);
+    for (int i = 0; i < n; ++i)
+      for (int j = i + 1; j < n; ++j)
+        if (std::strncmp(&all[32 * (size_t)i], &all[32 * (size_t)j], 32) == 0) {
+          std::fprintf(stderr,
+                       "combblas_hip: node-local ranks %d and %d of an RCCL communicator share GPU %s (set one "
+                       "device per rank, or COMBBLAS_HIP_COMM=mpi for a shared-GPU rehearsal)\n",
+                       i, j, &all[32 * (size_t)i]);
+          MPI_Abort(MPI_COMM_WORLD, CBH_E_NODEVICE);
+        }
+  }
+  MPI_Comm_free(&node);
+}
+
+// The cached communicators are released when MPI finalizes (the delete callback of an attribute
+// on MPI_COMM_SELF runs first thing in MPI_Finalize): after the context stream has drained, each
+// is aborted -- a local teardown that waits on no peer, so ranks that finish at different times
+// cannot hang each other at exit (ncclCommDestroy's implicit finalize may synchronize with peers).
+inline int rccl_release_all(MPI_Comm, int, void*, void*) {
+  auto& cache = rccl_cache();
+  if (!cache.empty()) {
+    (void)cbh_ctx_synchronize(context());
+    for (auto& kv : cache) (void)ncclCommAbort(kv.second);
+    cache.clear();
+  }
+  return MPI_SUCCESS;
+}
+inline void rccl_register_teardown() {
+  static bool done = [] {
+    int kv = MPI_KEYVAL_INVALID;
+    MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, rccl_release_all, &kv, nullptr);
+    MPI_Comm_set_attr(MPI_COMM_SELF, kv, nullptr);
+    return true;
+  }();
+  (void)done;
+}
+
 inline ncclComm_t rccl_comm_for(MPI_Comm comm) {
   void* attr = nullptr;
   int found = 0;
   MPI_Comm_get_attr(comm, rccl_keyval(), &attr, &found);
   if (found && attr) return *static_cast<ncclComm_t*>(attr);
-  ensure_device_free();  // RCCL's buffers are not the context allocator's
   auto& cache = rccl_cache();
   const std::vector<int> key = world_ranks(comm);
   auto it = cache.find(key);
@@ -212,6 +262,12 @@ inline ncclComm_t rccl_comm_for(MPI_Comm comm) {
     int rank = 0, size = 1;
     MPI_Comm_rank(comm, &rank);
     MPI_Comm_size(comm, &size);
+    check_distinct_devices(comm);
+    rccl_register_teardown();
+    // RCCL's buffers are not the context allocator's: only a NEW communicator needs device memory
+    // freed (releasing on every uncached MPI communicator emptied the block cache the
+    // phased drivers reuse, as 783b081 found for the 2D driver's start)
+    ensure_device_free();
     ncclUniqueId id;
     if (rank == 0) rccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
     MPI_Bcast(&id, (int)sizeof(id), MPI_BYTE, 0, comm);

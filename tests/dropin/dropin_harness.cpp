@@ -16,6 +16,9 @@
 //     PlusTimesSRing<double,int64_t> -- promotion NT1 != NT2 -> T_promote = double
 //     Select2ndSRing<int64,int64,int64> -- non-commutative add (reference order, order_kernel.h)
 //     PTOrdDev    -- f64 PlusTimes marked reference_order: non-dyadic sums bit-exact
+//     AffineDev   -- an UNMARKED non-commutative f64 semiring: reference order by default
+//   PlusTimesSRing<double,double> again with COMBBLAS_HIP_ORDER=reference on non-dyadic values
+//     (library kernels + the reference-order pass, cbh_spgemm CBH_ORDER_HYBRID)
 //   dropin_harness <scale>      -> prints "DROPIN <case> OK nnz=..." lines, exit 0 on success
 #include <mpi.h>
 
@@ -75,6 +78,7 @@ COMBBLAS_HIP_INSTANTIATE_DEVICE(PTDI, int64_t, double, int64_t, double)
 typedef Select2ndSRing<int64_t, int64_t, int64_t> S2LL;
 COMBBLAS_HIP_INSTANTIATE_DEVICE(S2LL, int64_t, int64_t, int64_t, int64_t)
 COMBBLAS_HIP_INSTANTIATE_DEVICE(PTOrdDev, int64_t, double, double, double)
+COMBBLAS_HIP_INSTANTIATE_DEVICE(AffineDev, int64_t, double, double, double)
 
 template <class NT>
 static bool same(const SpDCCols<int64_t, NT>& x, const SpDCCols<int64_t, NT>& y) {
@@ -215,6 +219,13 @@ int main(int argc, char** argv) {
     set_values(Af, [](int64_t r, int64_t c, double x) { return x * (0.1 + 1e-3 * ((r * 7919 + c * 31) % 97)); });
     set_values(Bf, [](int64_t r, int64_t c, double x) { return x * (0.3 - 1e-3 * ((r * 104729 + c * 17) % 89)); });
     bad += run_case<double, PTOrdDev, PTOrdCpu>("PSpGEMM<PlusTimes<double> reference order, non-dyadic>", Af, Bf);
+    // an unmarked non-commutative, non-associative user semiring: reference order by default
+    bad += run_case<double, AffineDev, AffineCpu>("PSpGEMM<unmarked user affine f64, default reference order>", Af, Bf);
+    // the built-in f64 PlusTimes through the library kernels with COMBBLAS_HIP_ORDER=reference
+    setenv("COMBBLAS_HIP_ORDER", "reference", 1);
+    bad += run_case<double, PTDD, CpuPlusTimes<double>>("PSpGEMM<PlusTimes<double>> COMBBLAS_HIP_ORDER=reference, non-dyadic",
+                                                          Af, Bf);
+    unsetenv("COMBBLAS_HIP_ORDER");
   }
   MPI_Finalize();
   return bad ? 1 : 0;

@@ -11,3 +11,4 @@ COMBBLAS_HIP_DEVICE_KERNELS(PTDI, int64_t, double, int64_t, double)
 typedef combblas::Select2ndSRing<int64_t, int64_t, int64_t> S2LL;
 COMBBLAS_HIP_DEVICE_KERNELS(S2LL, int64_t, int64_t, int64_t, int64_t)
 COMBBLAS_HIP_DEVICE_KERNELS(PTOrdDev, int64_t, double, double, double)
+COMBBLAS_HIP_DEVICE_KERNELS(AffineDev, int64_t, double, double, double)

@@ -80,9 +80,27 @@ struct Select2ndCpu {
   static int64_t multiply(const int64_t&, const int64_t& b) { return b; }
   static void axpy(int64_t a, const int64_t& x, int64_t& y) { y = multiply(a, x); }
 };
+// an UNMARKED user semiring whose add is neither commutative nor associative, over non-dyadic
+// doubles: the device path must fold it in the reference's order by default (HipSpGEMMDevice.h)
+struct AffineDev {
+  static double id() { return 0.0; }
+  static bool returnedSAID() { return false; }
+  static MPI_Op mpi_op() { return MPI_SUM; }
+  CBH_HD static double add(const double& a, const double& b) { return 0.75 * a + b; }
+  CBH_HD static double multiply(const double& a, const double& b) { return a * b - 0.125 * b; }
+};
+struct AffineCpu {
+  static double id() { return 0.0; }
+  static bool returnedSAID() { return false; }
+  static MPI_Op mpi_op() { return MPI_SUM; }
+  static double add(const double& a, const double& b) { return 0.75 * a + b; }
+  static double multiply(const double& a, const double& b) { return a * b - 0.125 * b; }
+};
 namespace combblas_hip {
 template <>
 struct reference_order<PTOrdDev> : std::true_type {};
+template <>
+struct arrival_order_ok<MinMaxDev> : std::true_type {};  // min / max per field: order-free (opt-in)
 }  // namespace combblas_hip
 
 struct MinMaxCpu {

@@ -18,7 +18,10 @@ import helpers as H
 pytestmark = pytest.mark.gpu
 
 HARNESS = os.path.join(H.REPO, "oracle", "_ref", "dropin3d_harness")
-ENV = dict(os.environ, LD_LIBRARY_PATH="/usr/lib/x86_64-linux-gnu:/opt/conda/lib", OMP_NUM_THREADS="1")
+# the ranks share the box's one GPU: an explicit rehearsal (HipSpGEMM.h context() refuses more local
+# ranks than devices otherwise)
+ENV = dict(os.environ, LD_LIBRARY_PATH="/usr/lib/x86_64-linux-gnu:/opt/conda/lib", OMP_NUM_THREADS="1",
+           COMBBLAS_HIP_SHARE_DEVICE="1")
 
 
 @pytest.mark.parametrize("ranks,layers,ncases", [(1, 0, 4), (2, 2, 3), (4, 4, 7), (8, 2, 3)])

@@ -17,9 +17,14 @@ HARNESS = os.path.join(H.REPO, "oracle", "_ref", "dropin_harness")
 def test_reference_driver_uses_hip_kernels(scale):
     assert os.path.exists(HARNESS), "oracle/_ref/dropin_harness missing: run __graft_entry__.build() with the reference"
     env = dict(os.environ, LD_LIBRARY_PATH="/usr/lib/x86_64-linux-gnu:/opt/conda/lib", OMP_NUM_THREADS="8")
-    r = subprocess.run([HARNESS, str(scale)], env=env, capture_output=True, text=True, timeout=150, cwd="/tmp")
+    r = subprocess.run([HARNESS, str(scale)], env=env, capture_output=True, text=True, timeout=240, cwd="/tmp")
     out = r.stdout + r.stderr
     assert r.returncode == 0, out
     lines = [l for l in out.splitlines() if l.startswith("DROPIN")]
-    # 5 arrival-order cases + Select2nd (non-commutative add) and non-dyadic f64 in reference order
-    assert len(lines) == 7 and all(" OK " in l for l in lines), out
+    # built-in PlusTimes<double> / SelectMax<int64> (library kernels, arrival order: exact on integer-valued
+    # inputs), user KTips bool and promoted PlusTimes<double,int64> (default reference order), user struct
+    # MinMax (arrival_order_ok opt-in), Select2nd (non-commutative add), marked PlusTimes f64 and an unmarked
+    # non-commutative affine f64 semiring on non-dyadic values (reference order), and the built-in
+    # PlusTimes<double> on non-dyadic values with COMBBLAS_HIP_ORDER=reference -- all bit-identical to the
+    # stock driver (at scale 16: config C1 in the reference's own order, no tolerance)
+    assert len(lines) == 9 and all(" OK " in l for l in lines), out

@@ -80,3 +80,39 @@ def test_f64_rounding_within_summation_bound(ctx, oracle, scale):
     # single-product entries have a zero bound (bit-exact); enough entries sum several products
     # of mixed sign that the orders genuinely differ (heap vs hash on the CPU: ~7 % of entries)
     assert (bound > 0).mean() > 0.05
+
+
+# ---------------------------------------------------------------------------------------------
+# Reference order (cbh_spgemm's CBH_ORDER_* flags, device/order_kernel.h): every output re-folded
+# in the order the named reference kernel folds it -- no tolerance at all. Scale 16 is config C1;
+# the operands are the non-dyadic mixed-sign ones above, so every multi-product entry's rounding
+# depends on the order. The oracle restates the three reference kernels (pinned to the reference
+# itself at scales 6-12, tests/test_oracle.py), including their exact sequences: the heap branch's
+# libstdc++ pop order with add(old, new), the hash branch's B-entry order with add(new, old).
+@pytest.mark.parametrize("scale,kernel", [(13, "hybrid"), (13, "heap"), (13, "hash"), (16, "hybrid")])
+def test_reference_order_bit_exact(ctx, oracle, scale, kernel):
+    import time
+
+    import combblas_amd as cb
+
+    A = _operand(scale, 5 + scale)
+    hA = cb.HostDcsc(A.m, A.n, A.jc, A.cp, A.ir, A.num)
+    dA, dB = cb.SpDCCols.from_host(ctx, hA), cb.SpDCCols.from_host(ctx, hA)
+    call = {"hybrid": cb.LocalHybridSpGEMM, "heap": cb.LocalSpGEMM, "hash": cb.LocalSpGEMMHash}[kernel]
+    ms = {}
+    for order in ("arrival", "reference"):
+        call(cb.PlusTimesSRing, dA, dB, order=order).free()  # warm
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        C = call(cb.PlusTimesSRing, dA, dB, order=order)
+        ctx.synchronize()
+        ms[order] = (time.perf_counter() - t0) * 1e3
+        h = C.to_host()
+        C.free()
+    got = H.Dcsc(h.m, h.n, h.jc, h.cp, h.ir, h.num)
+    ref = oracle.spgemm(A, A, "plus_times", kernel, threads=8)
+    print(f"scale {scale} {kernel}: {ref.nnz} entries; arrival {ms['arrival']:.1f} ms, reference order "
+          f"{ms['reference']:.1f} ms")
+    assert np.array_equal(got.jc, ref.jc) and np.array_equal(got.cp, ref.cp) and np.array_equal(got.ir, ref.ir)
+    diff = np.flatnonzero(got.num.view(np.uint64) != ref.num.view(np.uint64))
+    assert diff.size == 0, f"{diff.size} of {ref.nnz} values differ in their bits (first at {diff[:5]})"
