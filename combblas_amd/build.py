@@ -54,7 +54,9 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False, vari
     lib = LIB.replace(".so", f"_{variant}.so") if variant else LIB
     if not force and not _stale(lib):
         return lib
-    cmd = [HIPCC, "-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17", "-Wall",
+    # -ffp-contract=off: no a*b+c fused into one rounding -- the reference's host build (g++, x86-64
+    # without FMA) rounds every product and every sum, and the reference-order pass reproduces it bit for bit
+    cmd = [HIPCC, "-O3", "-ffp-contract=off", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17", "-Wall",
            "-Wno-unused-function", "-Wl,-soname," + os.path.basename(lib), "-o", lib + ".tmp"] + \
         [f"-D{d}" for d in defines] + [os.path.join(CSRC, s) for s in SOURCES] + ["-lpthread"]
     if verbose:

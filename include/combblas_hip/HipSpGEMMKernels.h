@@ -7,10 +7,18 @@
 // (the same arguments as COMBBLAS_HIP_INSTANTIATE_DEVICE in the host translation units). Only
 // this definition of combblas_hip::DeviceLocalSpGEMM runs here: the reference drivers stay in
 // the host translation units, built by the application's own compiler.
+//
+// Floating-point contract: compile this translation unit with -ffp-contract=off. hipcc fuses a*b+c
+// into one fma by default, the reference's host build (g++ on x86-64) rounds the product and the
+// sum separately, and the reference-order pass reproduces the stock kernel's values bit for bit only
+// with the same roundings. The pragma below turns fusion off for everything parsed after this header
+// (a semiring defined in a header included later); a semiring defined before it needs the flag.
 #pragma once
 
 #include "HipSpGEMMDevice.h"
 #include "device/numeric.h"
+
+#pragma clang fp contract(off)
 
 namespace combblas_hip {
 
