@@ -49,9 +49,12 @@ inline cbh_mat* col_concat(std::vector<cbh_mat*>& parts) {
   return out;
 }
 // COMBBLAS_HIP_MEMDIAG=1: the device memory state at the phased drivers' milestones (stderr)
-inline void memdiag(const char* where) {
+inline bool memdiag_on() {
   static const bool on = std::getenv("COMBBLAS_HIP_MEMDIAG") != nullptr;
-  if (!on) return;
+  return on;
+}
+inline void memdiag(const char* where) {
+  if (!memdiag_on()) return;
   static double last = 0;
   cbh_ctx_synchronize(context());
   const double now = MPI_Wtime();
@@ -61,6 +64,37 @@ inline void memdiag(const char* where) {
               last > 0 ? (now - last) * 1e3 : 0.0, live / 1e9, cached / 1e9, fr / 1e9, tot / 1e9);
   std::fflush(stdout);
   last = now;
+}
+// Device bytes one phase of MemEfficientSpGEMM allocates beside its product piece (an upper bound
+// read off the library's allocations): the numeric pass's task binning (< 64 B per output entry
+// of the piece is generous: a task covers thousands), MCLPruneRecoverySelect's column arrays
+// (cbh_mcl_prune_recovery_select: 9 eight-byte words per column) and its three Kselect calls
+// (per active column: 4 words, and 256 four-byte digit counts when the columns are reduced over
+// a processor column), the merge of per-stage partials (a second piece), plus 2 GB for the
+// allocator's size classes and the runtime. Round 5 used a constant 12 GB here.
+inline int64_t phase_scratch_bytes(int64_t phase_nnz, int64_t phase_cols, bool merges) {
+  const int64_t numeric = phase_nnz / 8;
+  const int64_t prune = phase_cols * (9 * 8 + 3 * (4 * 8 + 256 * 4));
+  const int64_t merge = merges ? phase_nnz * 12 : 0;
+  return numeric + prune + merge + (int64_t(2) << 30);
+}
+// The output arena's capacity (entries) for a phased call of this context: the room `fit` left
+// beside the phase, at most `limit`, but the capacity of the context's previous arena when that
+// still fits -- identical requests are served from the allocator's cache by the block the previous
+// result freed (C5's C++ line: a smaller second arena could not use the first one's block, and
+// re-mapping ~200 GB inside the first timed call cost 5.9 s). Fresh sizes are
+// rounded down to 1 GiB of entries so that small changes in free memory repeat the same request.
+// Per-context state (round 5 kept a function-static `last_pruned` shared by every call site).
+inline int64_t arena_capacity(cbh_ctx* ctx, int64_t fit, int64_t limit) {
+  static std::map<const cbh_ctx*, int64_t> prev;
+  int64_t cap = std::min(fit, limit);
+  if (cap <= 0) return 0;
+  auto it = prev.find(ctx);
+  if (it != prev.end() && it->second <= cap) return it->second;
+  const int64_t g = int64_t(1) << 30;
+  if (cap > 2 * g) cap = cap / g * g;
+  prev[ctx] = cap;
+  return cap;
 }
 inline std::vector<int64_t> essentials(const cbh_mat* M) {  // {nnz, m, n, nzc}
   int64_t m = 0, n = 0, nnz = 0, nzc = 0;
@@ -351,14 +385,19 @@ class StagePlans {
     for (size_t i = 0; i < plans.size(); ++i) {
       if (!plans[i] || bjc[i].empty()) continue;
       const size_t nzc = bjc[i].size();
-      int64_t* d = nullptr;
-      hip_check(hipMalloc(reinterpret_cast<void**>(&d), nzc * sizeof(int64_t)), "hipMalloc");
-      const int rc = cbh_plan_col_nnz(plans[i], d);
+      // (scratch from the context allocator: the block cache deliberately holds the previous call's
+      // phase blocks, and its OOM path gives them back where a raw hipMalloc would abort)
+      void* dv = nullptr;
+      int rc = cbh_ctx_alloc(context(), (int64_t)(nzc * sizeof(int64_t)), &dv);
+      if (rc != CBH_OK) die(context(), rc, "cbh_ctx_alloc");
+      int64_t* d = static_cast<int64_t*>(dv);
+      rc = cbh_plan_col_nnz(plans[i], d);
       if (rc != CBH_OK) die(context(), rc, "cbh_plan_col_nnz");
       std::vector<int64_t> h(nzc);
-      hip_check(hipStreamSynchronize(reinterpret_cast<hipStream_t>(cbh_ctx_stream(context()))), "hipStreamSynchronize");
-      hip_check(hipMemcpy(h.data(), d, nzc * sizeof(int64_t), hipMemcpyDeviceToHost), "hipMemcpy");
-      hip_check(hipFree(d), "hipFree");
+      hipStream_t cs = reinterpret_cast<hipStream_t>(cbh_ctx_stream(context()));
+      hip_check(hipMemcpyAsync(h.data(), d, nzc * sizeof(int64_t), hipMemcpyDeviceToHost, cs), "hipMemcpyAsync");
+      hip_check(hipStreamSynchronize(cs), "hipStreamSynchronize");
+      cbh_ctx_free(context(), d);
       for (size_t sl = 0; sl < nzc; ++sl) cnt[(size_t)bjc[i][sl]] += h[sl];
     }
     int csize = 1;
@@ -521,26 +560,24 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
   }
   std::vector<cbh_mat*> toconcatenate;
   // the pruned pieces go back to back into one arena whose arrays become C's: the memory beside
-  // A, B, the plans and the largest phase product (its exact nnz; twice that when per-stage
-  // partials are merged, plus 10 % for the prune's scratch), at most the unpruned nnz
+  // A, B, the plans, the largest phase product (its exact nnz; twice that when per-stage partials
+  // are merged) and the scratch of one phase (combblas_hip::phase_scratch_bytes), at most the
+  // unpruned nnz; the same capacity as the previous call of this context when it still fits
+  // (arena_capacity), so that the block the previous result freed serves it again
   cbh_arena* arena = nullptr;
-  int64_t* arena_hint = nullptr;
   {
     cbh_ctx* ctx = combblas_hip::context();
     int64_t live = 0, cached = 0, fr = 0, tot = 0;
     cbh_ctx_memory(ctx, &live, &cached, &fr, &tot);
     const int64_t eb = (int64_t)(sizeof(int32_t) + sizeof(NUO));
-    const int64_t phase_bytes = (int64_t)(1.1 * (double)max_phase_nnz * (SP.merges() ? 2 : 1)) * eb;
-    // (12 GB beside the phase: the phase piece's own scratch and whatever else the device holds --
-    // 8 GB fitted C5 only while a per-call RCCL communicator's buffers kept the arena smaller)
-    int64_t cap = (fr + cached - phase_bytes - (int64_t(12) << 30)) / eb;
-    cap = std::min<int64_t>(cap, SP.nnz);
-    // an MCL iteration prunes to about the previous call's size: an arena sized from it (+15 %)
-    // leaves the phase blocks in the allocator's cache from call to call (an undersized arena only
-    // costs the copying concatenation)
-    static int64_t last_pruned = 0;
-    if (last_pruned > 0) cap = std::min<int64_t>(cap, last_pruned + last_pruned / 20 * 3);
-    arena_hint = &last_pruned;
+    int64_t max_phase_cols = 0;
+    for (int p = 0; p < phases; ++p) max_phase_cols = std::max<int64_t>(max_phase_cols, cuts[p + 1] - cuts[p]);
+    const int64_t phase_bytes = max_phase_nnz * (SP.merges() ? 2 : 1) * eb;
+    const int64_t reserve = combblas_hip::phase_scratch_bytes(max_phase_nnz, max_phase_cols, SP.merges());
+    const int64_t cap = combblas_hip::arena_capacity(ctx, (fr + cached - phase_bytes - reserve) / eb, SP.nnz);
+    if (combblas_hip::memdiag_on())
+      std::printf("[memdiag] arena %.2f GB (phase piece %.2f GB, phase scratch bound %.2f GB)\n", cap * eb / 1e9,
+                  phase_bytes / 1e9, reserve / 1e9);
     if (cap > 0 && sizeof(NUO) == 8 && cbh_arena_create(ctx, cap, (int64_t)sizeof(NUO), &arena) != CBH_OK)
       arena = nullptr;  // (no room: the pieces are allocated one by one and concatenated)
   }
@@ -569,11 +606,6 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, combblas_hip::SpDC
     Cm = combblas_hip::col_concat(toconcatenate);
   }
   combblas_hip::memdiag("concatenated");
-  if (arena_hint) {
-    int64_t nnz = 0;
-    cbh_mat_info(Cm, nullptr, nullptr, &nnz, nullptr, nullptr);
-    *arena_hint = nnz;
-  }
   (void)kselectVersion;
   return SpParMat<IU, NUO, UDERO>(new UDERO(Cm), GridC);
 }
@@ -612,7 +644,8 @@ SpParMat3D<IU, NUO, UDERO> MemEfficientSpGEMM3D(SpParMat3D<IU, NU1, combblas_hip
     MPI_Abort(MPI_COMM_WORLD, DIMMISMATCH);
   }
   if (phases < 1 || phases >= B.getncol()) phases = 1;
-  combblas_hip::ensure_device_free();
+  // (no cache release at the start, as in the 2D driver: the previous call's phase blocks are what
+  // this call's phases reuse; a new RCCL communicator frees what it needs itself, rccl_comm_for)
   auto g3 = A.getcommgrid3D();
   // the layer SUMMA's stage pairs, planned once for every phase (freed before the concatenation)
   std::unique_ptr<combblas_hip::StagePlans<IU, NU1, NU2>> SPp(new combblas_hip::StagePlans<IU, NU1, NU2>(
