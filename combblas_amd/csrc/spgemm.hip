@@ -24,6 +24,7 @@
 
 #include "../../include/combblas_hip.h"
 #include "../../include/combblas_hip/device/numeric.h"
+#include "../../include/combblas_hip/device/merge2.h"
 #include "apps.h"
 #include "convert.h"
 #include "blocks.h"
@@ -2419,6 +2420,81 @@ int cbh_plan_spgemm_slots(cbh_plan* p, cbh_semiring sr, int64_t s0, int64_t s1, 
   });
 }
 
+extern "C++" {
+// Two lists: the streaming merge path (device/merge2.h) -- head counts per chunk, a scan over the
+// chunks (C's offsets and column pointers), the write pass. CBH_MERGE2=0 keeps the task kernels'
+// hash merge for every list count (A/B hook).
+static bool merge2_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("CBH_MERGE2");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return v;
+}
+template <class SR>
+static int merge_two(cbh_ctx* ctx, Scratch& S, SR, const cbh_mat* const* parts, int64_t ncols, const int64_t* jcC,
+                     const int64_t* seg_start, const int64_t* seg_len, cbh_mat** C) {
+  const cbh_mat* P0 = parts[0];
+  int64_t *nch, *cstart;
+  CBH_TRY(S.get(&nch, ncols + 1));
+  CBH_TRY(S.get(&cstart, ncols + 1));
+  hipLaunchKernelGGL(merge2_nchunks_kernel, dim3(blocks_for(ncols, 256)), dim3(256), 0, ctx->stream, seg_len, ncols, nch);
+  CBH_HIP(ctx, hipMemsetAsync(nch + ncols, 0, sizeof(int64_t), ctx->stream));
+  CBH_TRY(exclusive_scan_i64(ctx, S, nch, cstart, ncols + 1));
+  int64_t nchunks = 0;
+  CBH_HIP(ctx, hipMemcpyAsync(&nchunks, cstart + ncols, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (nchunks > INT32_MAX) return fail(ctx, CBH_E_INTERNAL, "more than 2^31 merge chunks");
+  int32_t* chunk_col;
+  int64_t *ccnt, *coff, *Ccp;
+  CBH_TRY(S.get(&chunk_col, nchunks));
+  CBH_TRY(S.get(&ccnt, nchunks + 1));
+  CBH_TRY(S.get(&coff, nchunks + 1));
+  CBH_TRY(S.get(&Ccp, ncols + 1));
+  hipLaunchKernelGGL(merge2_fill_kernel, dim3(blocks_for(ncols, 256)), dim3(256), 0, ctx->stream, cstart, ncols,
+                     chunk_col);
+  constexpr int WPB = 4;
+  const unsigned grid = (unsigned)((nchunks + WPB - 1) / WPB);
+  const int64_t in = P0->nnz + parts[1]->nnz;
+  CBH_TRY(timed_launch(ctx, CBH_K_MERGE_SYM, 4.0 * (double)in, [&] {
+    hipLaunchKernelGGL((merge2_kernel<SR, false, WPB>), dim3(grid), dim3(64 * WPB), 0, ctx->stream, chunk_col, nchunks,
+                       cstart, seg_start, seg_len, P0->ir, P0->num, parts[1]->ir, parts[1]->num, ccnt,
+                       (const int64_t*)nullptr, (int32_t*)nullptr, (void*)nullptr);
+    return hipGetLastError();
+  }));
+  CBH_HIP(ctx, hipMemsetAsync(ccnt + nchunks, 0, sizeof(int64_t), ctx->stream));
+  CBH_TRY(exclusive_scan_i64(ctx, S, ccnt, coff, nchunks + 1));
+  hipLaunchKernelGGL(gather_i64_kernel, dim3(blocks_for(ncols + 1, 256)), dim3(256), 0, ctx->stream, coff, cstart,
+                     ncols + 1, Ccp);
+  int64_t total = 0;
+  CBH_HIP(ctx, hipMemcpyAsync(&total, coff + nchunks, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  CBH_TRY(check_err(ctx));
+  cbh_mat* out;
+  CBH_TRY(new_mat(ctx, P0->m, P0->n, total, ncols, P0->dtype, &out, P0->vbytes));
+  constexpr double eb = 4.0 + sizeof(typename SR::val_t);  // entries read + outputs written
+  int rc = timed_launch(ctx, CBH_K_MERGE_NUM, eb * (double)(in + total), [&] {
+    hipLaunchKernelGGL((merge2_kernel<SR, true, WPB>), dim3(grid), dim3(64 * WPB), 0, ctx->stream, chunk_col, nchunks,
+                       cstart, seg_start, seg_len, P0->ir, P0->num, parts[1]->ir, parts[1]->num, (int64_t*)nullptr,
+                       coff, out->ir, out->num);
+    return hipGetLastError();
+  });
+  if (rc == CBH_OK)
+    rc = hip_rc(ctx, hipMemcpyAsync(out->jc, jcC, sizeof(int64_t) * ncols, hipMemcpyDeviceToDevice, ctx->stream),
+                "hipMemcpyAsync(C.jc)");
+  if (rc == CBH_OK)
+    rc = hip_rc(ctx, hipMemcpyAsync(out->cp, Ccp, sizeof(int64_t) * (ncols + 1), hipMemcpyDeviceToDevice, ctx->stream),
+                "hipMemcpyAsync(C.cp)");
+  if (rc == CBH_OK) rc = check_err(ctx);
+  if (rc != CBH_OK) {
+    cbh_mat_free(ctx, out);
+    return rc;
+  }
+  *C = out;
+  return CBH_OK;
+}
+}  // extern "C++"
+
 int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* parts, cbh_mat** C) {
   if (!ctx || !C || nlists < 0 || (nlists > 0 && !parts)) return fail(ctx, CBH_E_ARG, "bad merge arguments");
   if (nlists > kMaxLists) return fail(ctx, CBH_E_ARG, "at most 16 lists per merge; merge hierarchically");
@@ -2488,6 +2564,7 @@ int cbh_merge(cbh_ctx* ctx, cbh_semiring sr, int nlists, const cbh_mat* const* p
         hipLaunchKernelGGL(merge_seg_kernel, dim3(blocks_for(parts[l]->nzc, 256)), dim3(256), 0, ctx->stream,
                            parts[l]->jc, parts[l]->cp, parts[l]->nzc, idx, l, nlists, seg_start, seg_len);
     }
+    if (nlists == 2 && merge2_enabled()) return merge_two(ctx, S, SR{}, parts, ncols, jcC, seg_start, seg_len, C);
     hipLaunchKernelGGL(merge_work_kernel, dim3(blocks_for(ncols, 256)), dim3(256), 0, ctx->stream, seg_start, seg_len,
                        nlists, lr, ncols, work, rmin, rmax);
     CBH_HIP(ctx, hipGetLastError());

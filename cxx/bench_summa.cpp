@@ -139,6 +139,10 @@ static void phased_step(DDev& Aloc, CommGrid* GA, DDev& Bloc, CommGrid* GB, Comm
     for (auto& x : piece[c]) x += c0;
     c0 += div3[c];
   }
+  // phase p's fiber exchange (communication stream) overlaps phase p+1's products (context
+  // stream): MemEfficientSpGEMM3D's schedule in ParFriendsDev.h
+  std::unique_ptr<combblas_hip::FiberExchange> inflight;
+  int inflight_p = -1;
   for (int p = 0; p < phases; ++p) {
     std::vector<cbh_mat*> parts;
     std::vector<int64_t> lb(L);
@@ -146,8 +150,20 @@ static void phased_step(DDev& Aloc, CommGrid* GA, DDev& Bloc, CommGrid* GB, Comm
       parts.push_back(SP.piece(sr, dt, 8, piece[c][p], piece[c][p + 1]));
       lb[c] = piece[c][p + 1] - piece[c][p];
     }
+    combblas_hip::trace("products issued", p);
     cbh_mat* P = combblas_hip::col_concat(parts);
-    consume(combblas_hip::fiber_reduce_scatter(sr, P, lb, g3->GetFiberWorld(), dt, 8), piece[me][p] - piece[me][0]);
+    if (inflight) {
+      consume(combblas_hip::fiber_exchange_finish(*inflight), piece[me][inflight_p] - piece[me][0]);
+      combblas_hip::trace("exchange merged", inflight_p);
+    }
+    inflight.reset(new combblas_hip::FiberExchange(
+        combblas_hip::fiber_exchange_start(sr, P, lb, g3->GetFiberWorld(), dt, 8)));
+    inflight_p = p;
+    combblas_hip::trace("exchange posted", p);
+  }
+  if (inflight) {
+    consume(combblas_hip::fiber_exchange_finish(*inflight), piece[me][inflight_p] - piece[me][0]);
+    combblas_hip::trace("exchange merged", inflight_p);
   }
 }
 
@@ -323,6 +339,9 @@ int main(int argc, char** argv) {
             *A3d->GetLayerMat()->seqptr(), A3d->GetLayerMat()->getcommgrid().get(), *B3d->GetLayerMat()->seqptr(),
             B3d->GetLayerMat()->getcommgrid().get()));
       phases = plan_phases(SP->nnz);  // with the plans (and their stored bitmaps) still resident
+      // 3D over RCCL: at least 4 phases, so that all but a quarter of the fiber exchange runs under
+      // the next phase's products (one phase would leave the whole exchange exposed)
+      if (!twod && !combblas_hip::use_mpi_transport()) phases = std::max(phases, 4);
     }
     if (myrank == 0) std::fprintf(stderr, "[bench_summa] setup %.1f s, %d phase(s); warm-up\n", setup_s, phases);
     for (int w = 0; w < warmup; ++w) product(discard);

@@ -174,29 +174,69 @@ inline cbh_mat* mcl_prune_block(const cbh_mat* A, MPI_Comm colworld, double hard
 // fiber rank j -- essentials by MPI_Alltoall, the arrays by grouped ncclSend / ncclRecv (host
 // staged with COMBBLAS_HIP_COMM=mpi) -- and the L pieces of this rank's chunk are merged
 // (MultiwayMergeHash there; the device merge keeps rows sorted). P is freed.
-inline cbh_mat* fiber_reduce_scatter(cbh_semiring sr, cbh_mat* P, const std::vector<int64_t>& div, MPI_Comm fiber,
-                                     int dtype, int64_t vbytes) {
-  int L = 1, me = 0;
-  MPI_Comm_size(fiber, &L);
-  MPI_Comm_rank(fiber, &me);
-  std::vector<cbh_mat*> send(L), recv(L, nullptr);
+//
+// In two halves so that a phase loop can overlap the exchange of phase p with the products of
+// phase p+1 (the reference's Mult_AnXBn_Overlap idea, ParFriends.h:1110-1235, applied to the 3D
+// drivers' fiber step, :3143-3183): fiber_exchange_start posts the transfers on the communication
+// stream (RCCL) behind an event that orders the freshly allocated receive blocks after the context
+// stream's work, and returns; fiber_exchange_finish makes the context stream wait for them, frees
+// the sent pieces (stream-ordered, after the wait) and merges. The host-staged transport completes
+// the exchange inside start (MPI is synchronous here). COMBBLAS_HIP_TRACE=1 prints when each half
+// is issued (the rehearsal's evidence of the schedule).
+struct FiberExchange {
+  std::vector<cbh_mat*> send, recv;
+  std::vector<int64_t> ress;
+  int me = 0, L = 1;
+  int64_t width = 0;
+  hipEvent_t done = nullptr;
+  cbh_semiring sr = CBH_SR_PLUS_TIMES;
+  int dtype = CBH_F64;
+  int64_t vbytes = 8;
+};
+inline bool trace_on() {
+  static const bool v = [] {
+    const char* e = std::getenv("COMBBLAS_HIP_TRACE");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+inline void trace(const char* what, int phase) {
+  if (!trace_on()) return;
+  int r = 0;
+  MPI_Comm_rank(MPI_COMM_WORLD, &r);
+  std::fprintf(stderr, "[trace] rank %d %.6f %s phase %d\n", r, MPI_Wtime(), what, phase);
+}
+inline FiberExchange fiber_exchange_start(cbh_semiring sr, cbh_mat* P, const std::vector<int64_t>& div, MPI_Comm fiber,
+                                          int dtype, int64_t vbytes) {
+  FiberExchange X;
+  X.sr = sr;
+  X.dtype = dtype;
+  X.vbytes = vbytes;
+  MPI_Comm_size(fiber, &X.L);
+  MPI_Comm_rank(fiber, &X.me);
+  const int L = X.L, me = X.me;
+  X.width = div[me];
+  X.send.assign(L, nullptr);
+  X.recv.assign(L, nullptr);
   int64_t c0 = 0;
   for (int j = 0; j < L; ++j) {
-    send[j] = col_slice(P, c0, c0 + div[j]);
+    X.send[j] = col_slice(P, c0, c0 + div[j]);
     c0 += div[j];
   }
   cbh_mat_free(context(), P);
-  std::vector<int64_t> sess(4 * (size_t)L), ress(4 * (size_t)L);
+  std::vector<int64_t> sess(4 * (size_t)L);
+  X.ress.assign(4 * (size_t)L, 0);
   for (int j = 0; j < L; ++j) {
-    const auto e = essentials(send[j]);
+    const auto e = essentials(X.send[j]);
     std::copy(e.begin(), e.end(), sess.begin() + 4 * j);
   }
-  MPI_Alltoall(sess.data(), 4, MPI_INT64_T, ress.data(), 4, MPI_INT64_T, fiber);
-  recv[me] = send[me];
+  MPI_Alltoall(sess.data(), 4, MPI_INT64_T, X.ress.data(), 4, MPI_INT64_T, fiber);
+  X.recv[me] = X.send[me];
+  X.send[me] = nullptr;
   for (int j = 0; j < L; ++j) {
     if (j == me) continue;
-    int rc = cbh_mat_create(context(), ress[4 * j + 1], ress[4 * j + 2], ress[4 * j], ress[4 * j + 3], (cbh_dtype)dtype,
-                            vbytes, &recv[j]);
+    int rc = cbh_mat_create(context(), X.ress[4 * j + 1], X.ress[4 * j + 2], X.ress[4 * j], X.ress[4 * j + 3],
+                            (cbh_dtype)dtype, vbytes, &X.recv[j]);
     if (rc != CBH_OK) die(context(), rc, "cbh_mat_create");
   }
   struct Arrs {
@@ -214,10 +254,10 @@ inline cbh_mat* fiber_reduce_scatter(cbh_semiring sr, cbh_mat* P, const std::vec
                  (size_t)vbytes * (size_t)e[0]}};
   };
   hipStream_t s = reinterpret_cast<hipStream_t>(cbh_ctx_stream(context()));
-  if (use_mpi_transport()) {  // host-staged pairwise exchange
+  if (use_mpi_transport()) {  // host-staged pairwise exchange (synchronous)
     for (int d = 1; d < L; ++d) {
       const int to = (me + d) % L, from = (me - d + L) % L;
-      const Arrs a = arrays(send[to]), b = arrays(recv[from]);
+      const Arrs a = arrays(X.send[to]), b = arrays(X.recv[from]);
       for (int k = 0; k < 4; ++k) {
         std::vector<char> hs(a.b[k]), hr(b.b[k]);
         if (a.b[k]) {
@@ -233,32 +273,56 @@ inline cbh_mat* fiber_reduce_scatter(cbh_semiring sr, cbh_mat* P, const std::vec
     }
   } else if (L > 1) {
     ncclComm_t nc = rccl_comm_for(fiber);
+    hipStream_t cs = comm_stream();
+    hipEvent_t ready;
+    hip_check(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventRecord(ready, s), "hipEventRecord");  // the slices and receive blocks exist
+    hip_check(hipStreamWaitEvent(cs, ready, 0), "hipStreamWaitEvent");
+    hip_check(hipEventDestroy(ready), "hipEventDestroy");
     rccl_check(ncclGroupStart(), "ncclGroupStart");
     for (int j = 0; j < L; ++j) {
       if (j == me) continue;
-      const Arrs a = arrays(send[j]), b = arrays(recv[j]);
+      const Arrs a = arrays(X.send[j]), b = arrays(X.recv[j]);
       for (int k = 0; k < 4; ++k) {
-        if (a.b[k]) rccl_check(ncclSend(a.p[k], a.b[k], ncclUint8, j, nc, s), "ncclSend");
-        if (b.b[k]) rccl_check(ncclRecv(b.p[k], b.b[k], ncclUint8, j, nc, s), "ncclRecv");
+        if (a.b[k]) rccl_check(ncclSend(a.p[k], a.b[k], ncclUint8, j, nc, cs), "ncclSend");
+        if (b.b[k]) rccl_check(ncclRecv(b.p[k], b.b[k], ncclUint8, j, nc, cs), "ncclRecv");
       }
     }
     rccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    hip_check(hipEventCreateWithFlags(&X.done, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventRecord(X.done, cs), "hipEventRecord");
   }
-  for (int j = 0; j < L; ++j)
-    if (j != me) cbh_mat_free(context(), send[j]);
+  return X;
+}
+inline cbh_mat* fiber_exchange_finish(FiberExchange& X) {
+  if (X.done) {  // the context stream waits for the transfers; the sent slices are freed after them
+    hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(cbh_ctx_stream(context())), X.done, 0),
+              "hipStreamWaitEvent");
+    hip_check(hipEventDestroy(X.done), "hipEventDestroy");
+    X.done = nullptr;
+  }
+  for (cbh_mat* m : X.send)
+    if (m) cbh_mat_free(context(), m);
+  X.send.clear();
   std::vector<cbh_mat*> nonempty;
-  for (int j = 0; j < L; ++j) {
-    if (essentials(recv[j])[0] > 0) nonempty.push_back(recv[j]);
-    else cbh_mat_free(context(), recv[j]);
+  for (int j = 0; j < X.L; ++j) {
+    if (essentials(X.recv[j])[0] > 0) nonempty.push_back(X.recv[j]);
+    else cbh_mat_free(context(), X.recv[j]);
   }
+  X.recv.clear();
   if (nonempty.empty()) {
     cbh_mat* C = nullptr;
-    int rc = cbh_mat_create(context(), ress[4 * me + 1], div[me], 0, 0, (cbh_dtype)dtype, vbytes, &C);
+    int rc = cbh_mat_create(context(), X.ress[4 * X.me + 1], X.width, 0, 0, (cbh_dtype)X.dtype, X.vbytes, &C);
     if (rc != CBH_OK) die(context(), rc, "cbh_mat_create");
     return C;
   }
   if (nonempty.size() == 1) return nonempty[0];
-  return merge_all(sr, nonempty);
+  return merge_all(X.sr, nonempty);
+}
+inline cbh_mat* fiber_reduce_scatter(cbh_semiring sr, cbh_mat* P, const std::vector<int64_t>& div, MPI_Comm fiber,
+                                     int dtype, int64_t vbytes) {
+  FiberExchange X = fiber_exchange_start(sr, P, div, fiber, dtype, vbytes);
+  return fiber_exchange_finish(X);
 }
 
 // The SUMMA stage pairs of C = A * B for a phase loop. The reference re-broadcasts the stage blocks
@@ -688,6 +752,16 @@ SpParMat3D<IU, NUO, UDERO> MemEfficientSpGEMM3D(SpParMat3D<IU, NU1, combblas_hip
     c0 += div3[c];
   }
   std::vector<cbh_mat*> toconcatenate;
+  // phase p's fiber exchange runs on the communication stream while phase p+1's products run on
+  // the context stream; its merge and prune follow them (fiber_exchange_start / _finish)
+  auto finish = [&](combblas_hip::FiberExchange& X, int p) {
+    cbh_mat* Cp = combblas_hip::fiber_exchange_finish(X);
+    combblas_hip::trace("exchange merged", p);
+    SpParMat<IU, NUO, UDERO> phaseResultantLayer(new UDERO(Cp), g3->GetLayerWorld());
+    MCLPruneRecoverySelect(phaseResultantLayer, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion);
+    toconcatenate.push_back(phaseResultantLayer.seq().release());
+  };
+  std::unique_ptr<combblas_hip::FiberExchange> inflight;
   for (int p = 0; p < phases; ++p) {
     // OnePieceOfB = piece p of every chunk (ParFriends.h:3414-3440): the layer product of those
     // columns is the concatenation of the chunk pieces' products
@@ -698,14 +772,15 @@ SpParMat3D<IU, NUO, UDERO> MemEfficientSpGEMM3D(SpParMat3D<IU, NU1, combblas_hip
                                (int64_t)sizeof(NUO), piece[c][p], piece[c][p + 1]));
       lb[c] = piece[c][p + 1] - piece[c][p];
     }
+    combblas_hip::trace("products issued", p);
     cbh_mat* P = combblas_hip::col_concat(parts);
-    cbh_mat* Cp = combblas_hip::fiber_reduce_scatter(combblas_hip::semiring_traits<SR>::code, P, lb,
-                                                     g3->GetFiberWorld(), combblas_hip::dtype_of<NUO>::value,
-                                                     (int64_t)sizeof(NUO));
-    SpParMat<IU, NUO, UDERO> phaseResultantLayer(new UDERO(Cp), g3->GetLayerWorld());
-    MCLPruneRecoverySelect(phaseResultantLayer, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion);
-    toconcatenate.push_back(phaseResultantLayer.seq().release());
+    if (inflight) finish(*inflight, p - 1);  // (after phase p's products were issued)
+    inflight.reset(new combblas_hip::FiberExchange(combblas_hip::fiber_exchange_start(
+        combblas_hip::semiring_traits<SR>::code, P, lb, g3->GetFiberWorld(), combblas_hip::dtype_of<NUO>::value,
+        (int64_t)sizeof(NUO))));
+    combblas_hip::trace("exchange posted", p);
   }
+  if (inflight) finish(*inflight, phases - 1);
   (void)me;
   SPp.reset();
   return SpParMat3D<IU, NUO, UDERO>(new UDERO(combblas_hip::col_concat(toconcatenate)),
