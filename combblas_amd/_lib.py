@@ -150,6 +150,8 @@ SIGNATURES = {
                                                            ctypes.c_int64, ctypes.c_int64, ctypes.c_double,
                                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                            ctypes.POINTER(ctypes.c_void_p)]),
+    "cbh_mat_col_view": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                         ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_mat_col_slice": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                          ctypes.POINTER(ctypes.c_void_p)]),
     "cbh_mat_col_concat": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,

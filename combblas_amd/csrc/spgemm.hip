@@ -1876,20 +1876,36 @@ int cbh_mat_download_chunks(cbh_ctx* ctx, const cbh_mat* M, int64_t* cp, int64_t
     CBH_HIP(ctx, hipEventRecord(ctx->pin_ev[h], ctx->stream));
     return CBH_OK;
   };
+  // CBH_XFER_DIAG=1: where a download's time goes -- waiting for the copy engine vs the caller's
+  // host-side conversion (take), per call on stderr
+  static const bool diag = std::getenv("CBH_XFER_DIAG") != nullptr;
+  const auto t_start = std::chrono::steady_clock::now();
+  double wait_s = 0, take_s = 0;
   if (nnz > 0) CBH_TRY(issue(0, 0));
   for (int64_t f = 0, k = 0; f < nnz; f += ch, ++k) {
     const int h = (int)(k & 1);
     if (f + ch < nnz) CBH_TRY(issue(f + ch, h ^ 1));  // the next chunk moves while this one is taken
+    const auto t0 = std::chrono::steady_clock::now();
     CBH_HIP(ctx, hipEventSynchronize(ctx->pin_ev[h]));
+    const auto t1 = std::chrono::steady_clock::now();
     const int64_t cnt = std::min(ch, nnz - f);
     const int r = take(user, f, cnt, reinterpret_cast<const int32_t*>(half[h]),
                        half[h] + (((size_t)ch * 4 + 255) & ~size_t(255)));
+    wait_s += std::chrono::duration<double>(t1 - t0).count();
+    take_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
     if (r != 0) {
       (void)hipStreamSynchronize(ctx->stream);
       return fail(ctx, r, "download take callback returned " + std::to_string(r));
     }
   }
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (diag && nnz > 0) {
+    const double tot = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+    std::fprintf(stderr, "[cbh xfer] download %lld entries (%.1f MB device format) in %lld chunks: %.2f ms total, "
+                         "copy-engine wait %.2f ms, take %.2f ms (%.1f GB/s device format)\n",
+                 (long long)nnz, nnz * (4.0 + vb) / 1e6, (long long)((nnz + ch - 1) / ch), tot * 1e3, wait_s * 1e3,
+                 take_s * 1e3, nnz * (4.0 + vb) / tot / 1e9);
+  }
   return CBH_OK;
 }
 
@@ -3202,6 +3218,46 @@ int cbh_mat_col_slice(cbh_ctx* ctx, const cbh_mat* M, int64_t c0, int64_t c1, cb
                                 hipMemcpyDeviceToDevice, ctx->stream));
   }
   CBH_HIP(ctx, hipGetLastError());
+  *out = C;
+  return CBH_OK;
+}
+
+int cbh_mat_col_view(cbh_ctx* ctx, const cbh_mat* M, int64_t c0, int64_t c1, cbh_mat** out) {
+  if (!ctx || !M || !out) return fail(ctx, CBH_E_ARG, "null argument");
+  if (c0 < 0 || c1 < c0 || c1 > M->n) return fail(ctx, CBH_E_ARG, "column range outside the block");
+  *out = nullptr;
+  if (M->nzc == 0) {
+    CBH_TRY(new_mat(ctx, M->m, c1 - c0, 0, 0, M->dtype, out, M->vbytes));
+    CBH_HIP(ctx, hipMemsetAsync((*out)->cp, 0, sizeof(int64_t), ctx->stream));
+    return CBH_OK;
+  }
+  Scratch S(ctx);
+  int64_t* d;
+  CBH_TRY(S.get(&d, 4));
+  hipLaunchKernelGGL(col_range_kernel, dim3(1), dim3(64), 0, ctx->stream, M->jc, M->cp, M->nzc, c0, c1, d);
+  CBH_HIP(ctx, hipGetLastError());
+  int64_t h[4];
+  CBH_HIP(ctx, hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+  CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  const int64_t nzc = h[1] - h[0], nnz = h[3] - h[2];
+  cbh_mat* C;
+  CBH_TRY(new_mat(ctx, M->m, c1 - c0, 0, nzc, M->dtype, &C, M->vbytes));
+  dfree(ctx, C->ir);
+  dfree(ctx, C->num);
+  C->nnz = nnz;
+  C->ir = M->ir + h[2];
+  C->num = static_cast<char*>(M->num) + h[2] * M->vbytes;
+  C->borrowed_rows = true;
+  hipLaunchKernelGGL(add_const_i64_kernel, dim3(blocks_for(nzc + 1, 256)), dim3(256), 0, ctx->stream, M->cp + h[0],
+                     nzc + 1, -h[2], C->cp);
+  if (nzc > 0)
+    hipLaunchKernelGGL(add_const_i64_kernel, dim3(blocks_for(nzc, 256)), dim3(256), 0, ctx->stream, M->jc + h[0], nzc,
+                       -c0, C->jc);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    cbh_mat_free(ctx, C);
+    return fail(ctx, CBH_E_HIP, std::string("col_view: ") + hipGetErrorString(e));
+  }
   *out = C;
   return CBH_OK;
 }

@@ -391,6 +391,10 @@ int cbh_arena_concat(cbh_ctx* ctx, int k, cbh_mat** parts, cbh_arena* arena, cbh
  *   cbh_mat_col_concat  the k blocks side by side (SpDCCols::ColConcatenate, SpDCCols.cpp:1014-1090):
  *                       rows = the largest m, columns offset by the earlier blocks' n            */
 int cbh_mat_col_slice(cbh_ctx* ctx, const cbh_mat* M, int64_t c0, int64_t c1, cbh_mat** out);
+/* The same column range as a VIEW: its column pointers and ids are its own (rebased), its rows and
+ * values are M's own arrays (not copied, not freed with the view): free the view before M. The 3D
+ * drivers' fiber exchange sends a layer partial's column pieces from it without copying them. */
+int cbh_mat_col_view(cbh_ctx* ctx, const cbh_mat* M, int64_t c0, int64_t c1, cbh_mat** view);
 int cbh_mat_col_concat(cbh_ctx* ctx, int k, const cbh_mat* const* parts, cbh_mat** out);
 /* The same, releasing the parts as they are consumed (one array kind at a time: pointers, rows,
  * values), so the peak is the parts plus the largest output array instead of twice the matrix;

@@ -24,6 +24,7 @@
 #pragma once
 
 #include <mpi.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <chrono>
@@ -264,6 +265,18 @@ cbh_mat* upload(const combblas::SpTuples<IT, NT>& T, bool sort_rows = false) {
   return out;
 }
 
+// The arrays a download fills are fresh allocations (SpDCCols / ::operator new): every 4 KB page
+// faults at its first write inside the take callback. Transparent huge pages for them (where the
+// host's THP mode is "madvise") fault 2 MB at a time; COMBBLAS_HIP_NO_THP=1 skips the advice.
+inline void advise_huge(void* p, size_t bytes) {
+  static const bool off = std::getenv("COMBBLAS_HIP_NO_THP") != nullptr;
+  constexpr uintptr_t kHuge = uintptr_t(2) << 20;
+  if (off || bytes < 2 * kHuge) return;
+  const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + kHuge - 1) & ~(kHuge - 1);
+  const uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(kHuge - 1);
+  if (e > b) (void)madvise(reinterpret_cast<void*>(b), e - b, MADV_HUGEPAGE);
+}
+
 // device DCSC -> SpTuples<IT,NT>* (column-sorted; ::operator new tuples, mtSpGEMM.h:272,453). The
 // tuples are packed from the pinned chunks by the OpenMP threads, blocks of 4096 entries each
 // finding their first column by one bisection of cp.
@@ -274,6 +287,7 @@ combblas::SpTuples<IT, NT>* download_tuples(cbh_mat* C) {
   if (nnz == 0) return new combblas::SpTuples<IT, NT>(0, (IT)m, (IT)n);
   std::vector<int64_t> cp(nzc + 1), jc(nzc);
   auto* tuples = static_cast<std::tuple<IT, IT, NT>*>(::operator new(sizeof(std::tuple<IT, IT, NT>) * nnz));
+  advise_huge(tuples, sizeof(std::tuple<IT, IT, NT>) * (size_t)nnz);
   struct Dst {
     std::tuple<IT, IT, NT>* t;
     const int64_t* cp;
@@ -334,6 +348,8 @@ combblas::SpDCCols<IT, NT>* download_dcsc(const cbh_mat* C) {
     }
     return 0;
   };
+  advise_huge(d->ir, sizeof(IT) * (size_t)nnz);  // first-touch faults of the fresh arrays (take callback)
+  advise_huge(d->numx, sizeof(NT) * (size_t)nnz);
   int rc = cbh_mat_download_chunks(context(), C, cp, jc, 0, take, &dst);
   if (rc != CBH_OK) die(context(), rc, "cbh_mat_download_chunks");
   if (!std::is_same<IT, int64_t>::value) {

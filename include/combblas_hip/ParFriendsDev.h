@@ -184,6 +184,7 @@ inline cbh_mat* mcl_prune_block(const cbh_mat* A, MPI_Comm colworld, double hard
 // the exchange inside start (MPI is synchronous here). COMBBLAS_HIP_TRACE=1 prints when each half
 // is issued (the rehearsal's evidence of the schedule).
 struct FiberExchange {
+  cbh_mat* P = nullptr;  // the layer partial: the pieces are views of it (cbh_mat_col_view), freed last
   std::vector<cbh_mat*> send, recv;
   std::vector<int64_t> ress;
   int me = 0, L = 1;
@@ -218,12 +219,15 @@ inline FiberExchange fiber_exchange_start(cbh_semiring sr, cbh_mat* P, const std
   X.width = div[me];
   X.send.assign(L, nullptr);
   X.recv.assign(L, nullptr);
+  // the pieces are views of P (rows and values not copied: a scale-22 layer partial at 1x1x2 is
+  // ~180 GB); P lives until the exchange is finished and merged
+  X.P = P;
   int64_t c0 = 0;
   for (int j = 0; j < L; ++j) {
-    X.send[j] = col_slice(P, c0, c0 + div[j]);
+    int rc = cbh_mat_col_view(context(), P, c0, c0 + div[j], &X.send[j]);
+    if (rc != CBH_OK) die(context(), rc, "cbh_mat_col_view");
     c0 += div[j];
   }
-  cbh_mat_free(context(), P);
   std::vector<int64_t> sess(4 * (size_t)L);
   X.ress.assign(4 * (size_t)L, 0);
   for (int j = 0; j < L; ++j) {
@@ -304,20 +308,49 @@ inline cbh_mat* fiber_exchange_finish(FiberExchange& X) {
   for (cbh_mat* m : X.send)
     if (m) cbh_mat_free(context(), m);
   X.send.clear();
+  cbh_mat* own = X.recv[X.me];  // a view of P
   std::vector<cbh_mat*> nonempty;
-  for (int j = 0; j < X.L; ++j) {
+  for (int j = 0; j < X.L; ++j)
     if (essentials(X.recv[j])[0] > 0) nonempty.push_back(X.recv[j]);
-    else cbh_mat_free(context(), X.recv[j]);
-  }
-  X.recv.clear();
+  cbh_mat* C = nullptr;
   if (nonempty.empty()) {
-    cbh_mat* C = nullptr;
     int rc = cbh_mat_create(context(), X.ress[4 * X.me + 1], X.width, 0, 0, (cbh_dtype)X.dtype, X.vbytes, &C);
     if (rc != CBH_OK) die(context(), rc, "cbh_mat_create");
-    return C;
+  } else if (nonempty.size() == 1 && nonempty[0] != own) {
+    C = nonempty[0];  // a received block: owned
+  } else if (nonempty.size() == 1) {
+    int rc = cbh_mat_clone(context(), own, &C);  // the view must not outlive P
+    if (rc != CBH_OK) die(context(), rc, "cbh_mat_clone");
+  } else {
+    // (cbh_merge of the pieces, 16 at a time as merge_all, without freeing the inputs here)
+    std::vector<cbh_mat*> cur(nonempty.begin(), nonempty.end());
+    std::vector<cbh_mat*> made;
+    while (cur.size() > 1) {
+      std::vector<cbh_mat*> next;
+      for (size_t g = 0; g < cur.size(); g += 16) {
+        const size_t k = std::min<size_t>(16, cur.size() - g);
+        if (k == 1) {
+          next.push_back(cur[g]);
+          continue;
+        }
+        cbh_mat* r = nullptr;
+        int rc = cbh_merge(context(), X.sr, (int)k, cur.data() + g, &r);
+        if (rc != CBH_OK) die(context(), rc, "cbh_merge");
+        made.push_back(r);
+        next.push_back(r);
+      }
+      cur.swap(next);
+    }
+    C = cur[0];
+    for (cbh_mat* m : made)
+      if (m != C) cbh_mat_free(context(), m);
   }
-  if (nonempty.size() == 1) return nonempty[0];
-  return merge_all(X.sr, nonempty);
+  for (int j = 0; j < X.L; ++j)
+    if (X.recv[j] != C) cbh_mat_free(context(), X.recv[j]);
+  X.recv.clear();
+  cbh_mat_free(context(), X.P);  // (stream-ordered after the merge that read its views)
+  X.P = nullptr;
+  return C;
 }
 inline cbh_mat* fiber_reduce_scatter(cbh_semiring sr, cbh_mat* P, const std::vector<int64_t>& div, MPI_Comm fiber,
                                      int dtype, int64_t vbytes) {

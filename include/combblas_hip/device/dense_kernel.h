@@ -84,14 +84,19 @@ struct DenseCfg {
   // (int16 slot ids) reuses the compacted arrays
   static constexpr int TH0 = ((int)((TB - 32) / (sizeof(int32_t) + sizeof(acc_t))) - kGuard) / 64 * 64;
   static constexpr int THQ = ((int)((o_own - o_cstart) / 2) - kGuard) / 64 * 64;  // the queue's bound
-  static constexpr int TH = TH0 < THQ ? TH0 : THQ;
+  static constexpr int TH1 = TH0 < THQ ? TH0 : THQ;
+#ifdef CBH_HASH2_TH_MAX  // (A/B hook: the task kernel's 2048-slot table on this kernel)
+  static constexpr int TH = TH1 < CBH_HASH2_TH_MAX ? TH1 : CBH_HASH2_TH_MAX;
+#else
+  static constexpr int TH = TH1;
+#endif
   static constexpr int TA = TH + kGuard;
   static constexpr size_t o_hvals = al(sizeof(int32_t) * TA);  // (relative to o_win)
   static_assert(KIND != KHASH || (o_hvals + sizeof(acc_t) * TA <= TB && 2 * TA <= o_own - o_cstart && TA < 32768),
                 "hash table and commit queue fit");
   static_assert(NWB <= 32767, "int16 window prefixes");
   static_assert(bytes <= 163840, "one workgroup's LDS");
-  static_assert(EL == BS, "one entry per thread per chunk");
+  static_assert(EL <= BS && EL % 64 == 0, "at most one entry per thread per chunk");
   static_assert(U >= 1 && U <= 8, "a lane's owner counts are the 8 bytes of one word");
 };
 
@@ -271,7 +276,7 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 4 : 6) void dense_kernel(TaskArgs 
       int len = 0;
       int64_t cur0 = 0;
       b_t scale{};
-      if (i < ne) {
+      if (tid < EL && i < ne) {
         Ent e;
         if (!chunked) {
           e.cur = scur[tid];

@@ -244,7 +244,11 @@ struct TSym2 {
 #endif
 #ifndef CBH_HASH2_BS  // (A/B hooks: build variants only)
 #define CBH_HASH2_BS 1024
-#define CBH_HASH2_EL 1024
+#endif
+#ifndef CBH_HASH2_EL
+#define CBH_HASH2_EL CBH_HASH2_BS
+#endif
+#ifndef CBH_HASH2_LDS
 #define CBH_HASH2_LDS 163776
 #endif
 struct THash2 {

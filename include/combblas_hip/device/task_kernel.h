@@ -182,13 +182,19 @@ __device__ __forceinline__ int64_t gallop64(const int32_t* __restrict__ rows, in
 #ifndef CBH_STOP_TABLE_FIRST
 #define CBH_STOP_TABLE_FIRST 1
 #endif
+#ifndef CBH_STOP_PREFETCH  // (A/B hook) the next sub-tile's hub table pairs loaded during the current one
+#define CBH_STOP_PREFETCH 0
+#endif
+// pf_key / pf: the table pair of block boundary pf_key when the caller prefetched it (the task
+// kernel loads the NEXT sub-tile's pair of every hub entry during the current sub-tile, so the
+// one-load stop costs no round trip when its sub-tile comes; CBH_STOP_PREFETCH)
 template <int W>
 __device__ __forceinline__ int64_t stop_search(const int32_t* __restrict__ rows, int64_t lo, int64_t hi, int32_t key,
                                                const int2* __restrict__ blk, int64_t base, int32_t RB,
-                                               int32_t& row_at) {
+                                               int32_t& row_at, int32_t pf_key = -1, int2 pf = int2{0, 0}) {
 #if CBH_STOP_TABLE_FIRST
   if (blk != nullptr && key % RB == 0) {  // a row-block boundary (aligned sub-tiles): one table load
-    const int2 e = blk[key / RB];
+    const int2 e = key == pf_key ? pf : blk[key / RB];
     const int64_t s0 = base + e.x;
     const int64_t stop = s0 < lo ? lo : (s0 > hi ? hi : s0);
     row_at = stop >= hi ? kNoRow : (stop == s0 ? e.y : rows[stop]);
@@ -212,7 +218,7 @@ __device__ __forceinline__ int64_t stop_search(const int32_t* __restrict__ rows,
   lo += W;
   int64_t stop;
   if (blk != nullptr && key % RB == 0) {  // a row-block boundary (aligned sub-tiles): one table load
-    const int2 e = blk[key / RB];
+    const int2 e = key == pf_key ? pf : blk[key / RB];
     const int64_t s0 = base + e.x;
     stop = s0 < lo ? lo : (s0 > hi ? hi : s0);
     row_at = stop >= hi ? kNoRow : (stop == s0 ? e.y : rows[stop]);
@@ -672,7 +678,12 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
   // segment of every entry inside [lo, hi) (idle entries -- next row >= hi -- cost one LDS read),
   // then the exclusive scan of the segment lengths; epos becomes the gather base (cursor - offset).
   // Returns the sub-tile's product count P.
-  auto segments = [&](int nec, int32_t hi, bool hi_is_end) -> int {
+  // hi_next: the next sub-tile's end when it is a row-block boundary inside the task (-1: none).
+  // Entries kept in LDS (one per thread: unchunked tasks) then load the hub table pair of that
+  // boundary now, into registers, so the next sub-tile's stop search finds it there.
+  int32_t pf_key = -1;
+  int2 pf_e = int2{0, 0};
+  auto segments = [&](int nec, int32_t hi, bool hi_is_end, int32_t hi_next) -> int {
 #ifdef CBH_STAMPS
     if (tid == 0) atomicAdd(&g_stamps[16], (unsigned long long)nec);
 #endif
@@ -681,6 +692,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
       const int64_t p = epos[i];
       int64_t stop = p;
       int32_t nx2 = nx;
+      const int32_t h = MERGE ? -1 : ecol[i];
       if (nx < hi) {
 #ifdef CBH_STAMPS
         dg_active++;
@@ -690,11 +702,17 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
           stop = end;
           nx2 = kNoRow;
         } else {
-          const int32_t h = MERGE ? -1 : ecol[i];
           const int2* blk = h >= 0 ? hub_tab(h) : nullptr;
-          stop = stop_search<8>(rowsA, nx == kUnknownRow ? p : p + 1, end, hi, blk, p - ecoff[i], a.RB, nx2);
+          stop = stop_search<8>(rowsA, nx == kUnknownRow ? p : p + 1, end, hi, blk, p - ecoff[i], a.RB, nx2, pf_key,
+                                pf_e);
         }
       }
+#if CBH_STOP_PREFETCH
+      if (!MERGE && !chunked && hi_next > 0 && h >= 0 && nx2 < hi_next) {  // still has rows before hi_next
+        pf_e = hub_tab(h)[hi_next / a.RB];
+        pf_key = hi_next;
+      }
+#endif
       eoff[i] = (int32_t)(stop - p);
       enext2[i] = nx2;
 #ifdef CBH_STAMPS
@@ -909,7 +927,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
             load_entries(first, nec, lo, hi, lo == tlo && (full & 1), inited);
             __syncthreads();
           }
-          const int P = segments(nec, hi, hi == thi);
+          const int P = segments(nec, hi, hi == thi, -1);
           CBH_STAMP(3);
           if (chunked) {  // this chunk's cursors after the window, into the other buffer
             int64_t* gn = par ? a.gcur0 : a.gcur1;
@@ -970,6 +988,12 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
     }
     const int32_t hi = (int32_t)(he < thi ? he : thi);
     const bool hi_is_end = hi == thi;  // entry ends are clamped to the task (load_entries)
+    // the next nominal sub-tile's end, when it is an interior row-block boundary (stop prefetch)
+    int32_t hi_next = -1;
+    if (align && !hi_is_end) {
+      const int64_t hn = ((int64_t)hi / a.RB + wblk) * a.RB;
+      if (hn < thi) hi_next = (int32_t)hn;
+    }
     const uint32_t tw = (uint32_t)(hi - lo);
     const uint64_t scale = ((uint64_t)T << 32) / (uint64_t)tw;  // numeric order-preserving slot map
     const int nwd = (int)((tw + 31) >> 5);
@@ -994,7 +1018,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
         load_entries(first, nec, lo, hi, lo == tlo && (full & 1), lo != tlo);
         __syncthreads();
       }
-      const int P = segments(nec, hi, hi_is_end);
+      const int P = segments(nec, hi, hi_is_end, hi_next);
 #ifdef CBH_STAMPS
       if (tid == 0) {
         atomicAdd(&g_stamps[13], 1ull);

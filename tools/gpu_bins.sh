@@ -20,7 +20,7 @@ for PMC in "FETCH_SIZE TCC_HIT_sum" "WRITE_SIZE TCC_MISS_sum GRBM_GUI_ACTIVE" \
   step "pmc pass $i: $PMC"
   timeout -s KILL 300 rocprofv3 --pmc $PMC --kernel-include-regex 'task_kernel|dense_kernel' --output-format csv -d "$OUT/bins/pmc$i" -o run -- \
     python3 "$R/tools/phase_timing.py" "$SCALE" 1 > "$OUT/bins/pmc$i.log" 2>&1 || { tail -20 "$OUT/bins/pmc$i.log"; exit 1; }
-  timeout -s KILL 300 rocprofv3 --pmc $PMC --kernel-include-regex 'task_kernel.*true' --output-format csv -d "$OUT/bins/pmcm$i" -o run -- \
+  timeout -s KILL 300 rocprofv3 --pmc $PMC --kernel-include-regex 'task_kernel.*true|merge2_kernel' --output-format csv -d "$OUT/bins/pmcm$i" -o run -- \
     python3 "$R/tools/merge_sample.py" "$SCALE" 0.0625 1 > "$OUT/bins/pmcm$i.log" 2>&1 || { tail -20 "$OUT/bins/pmcm$i.log"; exit 1; }
 done
 python3 "$R/tools/pmc_bins.py" "$OUT/bins" "$OUT/ks.log" "$R/profiles/pmc_calib.json" "$OUT/pmc_bins.json"

@@ -23,6 +23,8 @@ MODES = {0: "sym", 1: "num", 2: "dense"}
 
 
 def bin_of(name):
+    if "merge2_kernel<" in name:  # device/merge2.h (round 6): two-list merge path, count / write pass
+        return "merge_num" if ", true," in name else "merge_sym"
     if "dense_kernel<" in name:  # device/dense_kernel.h (round 5): numeric dense / symbolic bitmap
         m = re.search(r"dense_kernel<.*, (\d+)>", name.split("(")[0])
         kind = m.group(1) if m else "?"
