@@ -48,6 +48,9 @@ constexpr int kSymWords = 12160;  // bitmap words of the large symbolic configur
 // numeric sub-tile: planned outputs, in eighths of the T home slots (3/8 and 5/8 measured slower:
 // 97.6 and 93.5 vs 98.6 GFLOP/s at scale 22 with T 4096; 5/8 again with T 2048: hash 434 vs 360 ms)
 constexpr int kFill8 = 4;
+#ifndef CBH_FILL16  // (A/B hook) numeric sub-tile plan in sixteenths of T (8 = kFill8 / 8 = 1/2)
+#define CBH_FILL16 8
+#endif
 // symbolic key-hash sub-tiles: keys, in eighths of TA (6/8 measured flat: symbolic 197 vs 193 ms)
 constexpr int kSymFill8 = 4;
 // dense numeric sub-tile capacity in quarters of T: 3 = 3072 values for T = 4096 (2 and 4
@@ -181,6 +184,9 @@ __device__ __forceinline__ int64_t gallop64(const int32_t* __restrict__ rows, in
 // 299 ms -- the extra dependent round trip of the long segments costs more than the table lines.
 #ifndef CBH_STOP_TABLE_FIRST
 #define CBH_STOP_TABLE_FIRST 1
+#endif
+#ifndef CBH_LAZY_CLEAR  // (A/B hook) see the sub-tile loop of task_kernel
+#define CBH_LAZY_CLEAR 0
 #endif
 #ifndef CBH_STOP_PREFETCH  // (A/B hook) the next sub-tile's hub table pairs loaded during the current one
 #define CBH_STOP_PREFETCH 0
@@ -538,7 +544,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
   const bool store = !NUM && a.bmp != nullptr && a.boff[task + 1] > a.boff[task];
   int64_t R = 1;
   if constexpr (!dense) {
-    constexpr int64_t cap = NUM ? (int64_t)T * kFill8 / 8 : (int64_t)TA * kSymFill8 / 8;  // outputs (keys) per sub-tile
+    constexpr int64_t cap = NUM ? (int64_t)T * CBH_FILL16 / 16 : (int64_t)TA * kSymFill8 / 8;  // outputs (keys) per sub-tile
     R = (work + cap - 1) / cap;
     if constexpr (!NUM) {
       const int64_t Rb = (span + 32ll * TA - 1) / (32ll * TA);
@@ -976,6 +982,11 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
     }
   }
   int64_t w = wnom;
+  // CBH_LAZY_CLEAR (A/B hook): a committed hash sub-tile resets only its occupied slots (listed in
+  // the commit queue) instead of the next sub-tile clearing all T + 64 slots
+  constexpr bool LAZY = CBH_LAZY_CLEAR && NUM && !LOCKED && !MERGE;
+  bool table_clean = false;
+  int lazy_q = 0;
   while (!dense && lo < thi) {
     int64_t he = (int64_t)lo + w;
     if (align) {
@@ -999,12 +1010,13 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
     const int nwd = (int)((tw + 31) >> 5);
     if (!NUM && bitmap) {
       for (int s = tid; s < nwd; s += BS) words[s] = 0u;
-    } else {
+    } else if (!(LAZY && table_clean)) {
       for (int s = tid; s < TA; s += BS) {
         keys[s] = kEmpty;
         if constexpr (NUM && !LOCKED) vals[s] = SR::identity();
       }
     }
+    if constexpr (LAZY) table_clean = false;  // (a retried sub-tile leaves the table dirty)
     if (tid == 0) __hip_atomic_store(&s_ovf, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const int count_before = my_count;
     __syncthreads();
@@ -1194,6 +1206,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
         }
       }
       out_pos += qtot;
+      if constexpr (LAZY) lazy_q = qtot;
 #ifdef CBH_STAMPS
       if (tid == 0) atomicAdd(&g_stamps[20], (unsigned long long)qtot);
 #endif
@@ -1201,6 +1214,15 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
     lo = hi;
     w = wnom;
     __syncthreads();
+    if constexpr (LAZY) {  // (after the commit's barrier: every read of the table is done)
+      const int16_t* Q = reinterpret_cast<const int16_t*>(own);
+      for (int q = tid; q < lazy_q; q += BS) {
+        const int sl = Q[q];
+        keys[sl] = kEmpty;
+        vals[sl] = SR::identity();
+      }
+      table_clean = true;  // (the next sub-tile's first barrier orders these before its inserts)
+    }
     CBH_STAMP(6);
   }
   if constexpr (!NUM) {
