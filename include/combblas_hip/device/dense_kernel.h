@@ -38,6 +38,12 @@
 
 namespace cbh {
 
+// bitmap words per int16 window prefix: 2 (round 6) -- a 64-bit word per rank lookup, 5 instead
+// of 6 bytes of LDS per word, so a window spans ~10 % more rows at the dense tasks' density (dense
+// 262.5 -> 254.5 ms per scale-22 product); 1 and 4 for A/B
+#ifndef CBH_DENSE_PAIRS
+#define CBH_DENSE_PAIRS 2
+#endif
 // registers per thread that prefetch the next window's first words (the rest load at its start)
 #ifndef CBH_DENSE2_PREFETCH
 #define CBH_DENSE2_PREFETCH 8
@@ -606,8 +612,15 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 4 : 6) void dense_kernel(TaskArgs 
     }
     const uint32_t* __restrict__ tb = a.bmp + bw0;
     constexpr int64_t TB = (int64_t)C::TB;
-    int64_t wdes = TB * nwt / ((int64_t)sizeof(acc_t) * work + 6 * nwt);  // words whose outputs fill the rest
-    wdes = wdes < 64 ? 64 : (wdes > C::NWB ? C::NWB : wdes);
+    // G bitmap words per int16 prefix (CBH_DENSE_PAIRS: 2, a 64-bit word per rank lookup): 4 + 2 / G
+    // bytes of LDS per word, so a window spans more rows for the same values
+    constexpr int G = CBH_DENSE_PAIRS;
+    static_assert(G == 1 || G == 2 || G == 4, "bitmap words per prefix");
+    constexpr int64_t kWB2 = 4 * G + 2;  // bytes per G words (words + prefix)
+    constexpr int NWBG = (int)((TB - 64) * G / kWB2) / 8 * 8;
+    int64_t wdes = TB * nwt * G / ((int64_t)sizeof(acc_t) * work * G + kWB2 * nwt);  // words whose outputs fill the rest
+    wdes = wdes < 64 ? 64 : (wdes > NWBG ? NWBG : wdes);
+    wdes &= ~int64_t(G - 1);
     const bool dalign = kAlignSubtiles && a.RB > 0 && (a.RB & 31) == 0 && (tlo & 31) == 0;
     const int64_t dbw = dalign ? a.RB / 32 : 1;  // words per row block
     constexpr int KW0 = (C::NWB + BS - 1) / BS;
@@ -618,11 +631,41 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 4 : 6) void dense_kernel(TaskArgs 
     __syncthreads();
     while (w0 < nwt) {
       const int wl = (int)((nwt - w0) < wdes ? (nwt - w0) : wdes);
-      const int dbase = (int)((TB - 6 * wl) & ~int64_t(15));
+      const int ng = (wl + G - 1) / G;  // prefix groups of the window (an odd last word padded)
+      const int dbase = (int)((TB - 4 * G * ng - 2 * ng) & ~int64_t(15));
       uint32_t* dw = reinterpret_cast<uint32_t*>(win + dbase);
-      int16_t* dp = reinterpret_cast<int16_t*>(win + dbase + 4 * wl);
+      int16_t* dp = reinterpret_cast<int16_t*>(win + dbase + 4 * G * ng);
+      // group g: its G words (one LDS load of 4 G bytes); its popcount; the set bits below `bit`
+      auto gpop = [&](int g) -> int {
+        if constexpr (G == 4) {
+          const uint4 v = reinterpret_cast<const uint4*>(dw)[g];
+          return __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+        } else if constexpr (G == 2) {
+          return __popcll(reinterpret_cast<const uint64_t*>(dw)[g]);
+        } else {
+          return __popc(dw[g]);
+        }
+      };
+      auto grank = [&](int g, uint32_t bit, bool& set) -> int {
+        if constexpr (G == 4) {
+          const uint4 v = reinterpret_cast<const uint4*>(dw)[g];
+          const uint32_t wi = bit >> 5, b = bit & 31u;
+          const uint32_t w = wi == 0 ? v.x : (wi == 1 ? v.y : (wi == 2 ? v.z : v.w));
+          set = (w >> b) & 1u;
+          return (wi > 0 ? __popc(v.x) : 0) + (wi > 1 ? __popc(v.y) : 0) + (wi > 2 ? __popc(v.z) : 0) +
+                 __popc(w & ((1u << b) - 1u));
+        } else if constexpr (G == 2) {
+          const uint64_t w = reinterpret_cast<const uint64_t*>(dw)[g];
+          set = (w >> bit) & 1ull;
+          return (int)__popcll(w & ((1ull << bit) - 1ull));
+        } else {
+          const uint32_t w = dw[g];
+          set = (w >> bit) & 1u;
+          return __popc(w & ((1u << bit) - 1u));
+        }
+      };
       const int capv = dbase / (int)sizeof(acc_t);
-      const int kw = (wl + BS - 1) / BS;
+      const int kw = (ng + BS - 1) / BS;
       {
         int x = tid;
         if (pre_w0 == w0) {
@@ -632,33 +675,36 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 4 : 6) void dense_kernel(TaskArgs 
           x += KW * BS;
         }
         for (; x < wl; x += BS) dw[x] = tb[w0 + x];
+        if (tid < ng * G - wl) dw[wl + tid] = 0u;  // (the last group's missing words)
       }
-      if (tid == 0) s_cut = wl;
+      if (tid == 0) s_cut = ng;
       __syncthreads();
       int tsum = 0;
       for (int k = 0; k < kw; ++k) {
         const int x = tid * kw + k;
-        tsum += x < wl ? __popc(dw[x]) : 0;
+        tsum += x < ng ? gpop(x) : 0;
       }
       int wtotal = 0;
       int ex = block_excl_sum<BS>(tsum, red, wtotal);
       for (int k = 0; k < kw; ++k) {
         const int x = tid * kw + k;
-        if (x < wl) {
-          const int pc = __popc(dw[x]);
+        if (x < ng) {
+          const int pc = gpop(x);
           dp[x] = (int16_t)(ex < 32767 ? ex : 32767);
           if (ex <= capv && ex + pc > capv) s_cut = x;
           ex += pc;
         }
       }
       __syncthreads();
-      int cut = __builtin_amdgcn_readfirstlane(s_cut);  // (block-uniform values kept in SGPRs)
+      const int cutg = __builtin_amdgcn_readfirstlane(s_cut);  // (block-uniform values kept in SGPRs)
+      int cut = cutg * G < wl ? cutg * G : wl;  // in words
       if (dalign && tlo + 32 * (w0 + cut) < thi) {  // window ends snap down to absolute row blocks
         const int64_t tw0 = tlo / 32;
-        const int64_t cb = (tw0 + w0 + cut) / dbw * dbw - tw0 - w0;
+        int64_t cb = (tw0 + w0 + cut) / dbw * dbw - tw0 - w0;
+        cb &= ~int64_t(G - 1);
         if (cb > 0 && cb * 4 >= 3ll * cut) cut = (int)cb;
       }
-      const int dtotal = __builtin_amdgcn_readfirstlane(cut < wl ? (int)dp[cut] : wtotal);
+      const int dtotal = __builtin_amdgcn_readfirstlane(cut < wl ? (int)dp[cut / G] : wtotal);
       // the next window's words, loaded before this window's commit (not before its products: KW
       // registers live across the product phase spilled)
       auto prefetch_next = [&]() {
@@ -683,9 +729,10 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 4 : 6) void dense_kernel(TaskArgs 
             bad |= 1 << 8;
             return;
           }
-          const uint32_t wv = dw[d >> 5];
-          if (!((wv >> (d & 31)) & 1u)) bad |= 1 << 11;  // a product row the symbolic pass did not mark
-          const int slot = dp[d >> 5] + __popc(wv & ((1u << (d & 31)) - 1u));
+          constexpr int SH = G == 4 ? 7 : (G == 2 ? 6 : 5);
+          bool set = false;
+          const int slot = dp[d >> SH] + grank((int)(d >> SH), d & (32u * G - 1u), set);
+          if (!set) bad |= 1 << 11;  // a product row the symbolic pass did not mark
           SR::lds_acc(&vals[slot], SR::multiply(av, cscale[e]));
         });
         inited = true;
@@ -696,12 +743,16 @@ __global__ __launch_bounds__(BS, BS >= 1024 ? 4 : 6) void dense_kernel(TaskArgs 
         } else {
           for (int q = tid; q < dtotal; q += BS)
             reinterpret_cast<val_t*>(a.Cnum)[out_pos + q] = SR::finalize(vals[q]);
-          for (int x = tid; x < cut; x += BS) {
-            uint32_t wv = dw[x];
+          const int cg = (cut + G - 1) / G;
+          for (int x = tid; x < cg; x += BS) {
             int32_t* cr = a.Cir + out_pos + dp[x];
-            while (wv) {
-              *cr++ = lo + 32 * x + __builtin_ctz(wv);
-              wv &= wv - 1u;
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+              uint32_t wv = dw[G * x + k];
+              while (wv) {
+                *cr++ = lo + 32 * (G * x + k) + __builtin_ctz(wv);
+                wv &= wv - 1u;
+              }
             }
           }
         }
