@@ -42,10 +42,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
 KERNELS = {"num_large": "cbh::task_kernel<cbh::PlusTimesD<double>, 2048, 512, 512, 4, 1, false>",
            # round 5: the dense tasks' kernel (device/dense_kernel.h; CBH_DENSE_V2=0 builds the round-4
            # "cbh::task_kernel<cbh::PlusTimesD<double>, 4096, 512, 512, 8, 2, false>")
-           "num_dense": "cbh::dense_kernel<cbh::PlusTimesD<double>, 1024, 1024, 8, 163776, 0>",
+           "num_dense": "cbh::dense_kernel<cbh::PlusTimesD<double>, 1024, 512, 8, 163776, 0>",
            "sym_large": "cbh::task_kernel<cbh::PlusTimesD<long>, 8192, 512, 512, 16, 0, false>",
            # round 5: the symbolic pass's large bitmap tasks (device/dense_kernel.h, SYM)
-           "sym_bmp": "cbh::dense_kernel<cbh::PlusTimesD<long>, 1024, 1024, 8, 163776, 1>"}
+           "sym_bmp": "cbh::dense_kernel<cbh::PlusTimesD<long>, 1024, 512, 8, 163776, 1>"}
 # every task-kernel class of the f64 PlusTimes product (the application lines pick their dominant one)
 ALL_KERNELS = dict(KERNELS, **{
     "num_mid": "cbh::task_kernel<cbh::PlusTimesD<double>, 2048, 256, 256, 4, 1, false>",

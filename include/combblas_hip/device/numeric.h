@@ -206,8 +206,11 @@ constexpr uint32_t plan_flags() {
 #ifndef CBH_DENSE2_LDS
 #define CBH_DENSE2_LDS 163776  // 160 KiB less the kernel's static LDS (s_cut)
 #endif
+#ifndef CBH_DENSE2_EL  // B entries per chunk (LDS-resident entry state); tasks with more keep it in HBM
+#define CBH_DENSE2_EL 512  // round 6 (r6n/r6o, profiles/r06/el_ab): 1024 -> 512 frees entry-state LDS
+#endif                     // for wider windows, dense 255.3 -> 250.3 ms; 256 is slower (271.7 ms)
 struct TDense2 {
-  static constexpr int BS = CBH_DENSE2_BS, EL = CBH_DENSE2_BS, U = CBH_DENSE2_U, LDSB = CBH_DENSE2_LDS;
+  static constexpr int BS = CBH_DENSE2_BS, EL = CBH_DENSE2_EL, U = CBH_DENSE2_U, LDSB = CBH_DENSE2_LDS;
 };
 template <class SR>
 hipError_t launch_dense_numeric(const TaskArgs& a, int64_t first, int64_t count, hipStream_t s) {
@@ -227,8 +230,11 @@ hipError_t launch_dense_numeric(const TaskArgs& a, int64_t first, int64_t count,
 #ifndef CBH_SYM2_U  // (A/B hook: build variants only)
 #define CBH_SYM2_U 8
 #endif
+#ifndef CBH_SYM2_EL  // B entries per chunk of the symbolic bitmap kernel: 512 (round 6) widens
+#define CBH_SYM2_EL 512  // its windows, so more tasks take it: sym_bmp + sym_large 172.1 -> 170.8 ms
+#endif
 struct TSym2 {
-  static constexpr int BS = 1024, EL = 1024, U = CBH_SYM2_U, LDSB = 163776;
+  static constexpr int BS = 1024, EL = CBH_SYM2_EL, U = CBH_SYM2_U, LDSB = 163776;
 };
 // The numeric hash tasks of the large bin on the same kernel (KHASH: ~7.4 K-slot order-preserving
 // table, sub-tiles of ~3.7 K outputs instead of task_kernel's 1 K; U 4: U 8 spills at the 128-VGPR
