@@ -1327,7 +1327,20 @@ static int run_numeric(cbh_ctx* ctx, Scratch& S, const cbh_mat* A, const cbh_mat
       CBH_HIP(ctx, hipMemcpyAsync(hw.data(), P.twork + t0, nt * 8, hipMemcpyDeviceToHost, ctx->stream));
       CBH_HIP(ctx, hipMemcpyAsync(hlo.data(), P.tlo + t0, nt * 4, hipMemcpyDeviceToHost, ctx->stream));
       CBH_HIP(ctx, hipMemcpyAsync(hhi.data(), P.thi + t0, nt * 4, hipMemcpyDeviceToHost, ctx->stream));
+      std::vector<int64_t> hb(P.bmp ? nt + 1 : 0);
+      if (P.bmp) CBH_HIP(ctx, hipMemcpyAsync(hb.data(), P.boff + t0, (nt + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
       CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      if (P.bmp) {  // stored bitmap words the numeric split uses, and those of tasks it sends to hash
+        double used = 0, unused = 0, unused_tasks = 0;
+        for (int64_t t = 0; t < nt; ++t) {
+          const double w = (double)(hb[t + 1] - hb[t]);
+          if (w <= 0) continue;
+          if (hd[t] > 0) used += w;
+          else unused += w, unused_tasks += 1;
+        }
+        std::fprintf(stderr, "[cbh diag] stored bitmap words: dense %.4g GB, to hash %.4g GB (%.0f tasks)\n",
+                     used * 4e-9, unused * 4e-9, unused_tasks);
+      }
       const char* names[4] = {"wave (<=256 out)", "mid (<=1024 out)", "hash large", "dense"};
       double st[4][4] = {{0}};  // tasks, outputs, flops, span
       for (int64_t t = 0; t < nt; ++t) {
