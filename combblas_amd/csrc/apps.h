@@ -208,11 +208,13 @@ __device__ __forceinline__ bool dot_lists(const DotArgs& a, int64_t p, int64_t& 
 }
 
 // class of every mask entry: 0 = empty intersection for sure (a list is empty: flag 0 written
-// here), 1 = thread, 2 = long (pieces). Waves append their entries to the class lists with one
-// atomic per class; npiece[x] = pieces of long entry x.
+// here), 1 = thread, 2 = long (pieces), 3 = hub candidate (hub_min > 0 and the longer list more
+// than kDotMergeRatio x the shorter: counted into its group, gcount[key]). Waves append their
+// entries to the class lists with one atomic per class; npiece[x] = pieces of long entry x.
 __global__ __launch_bounds__(256) void dot_classify_kernel(DotArgs a, int32_t* __restrict__ lthr,
                                                            int32_t* __restrict__ llong, int64_t* __restrict__ npiece,
-                                                           unsigned long long* __restrict__ counts) {
+                                                           unsigned long long* __restrict__ counts, int hub_min,
+                                                           int32_t* __restrict__ gcount, int32_t* __restrict__ lcand) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
   int cls = -1;
@@ -220,25 +222,34 @@ __global__ __launch_bounds__(256) void dot_classify_kernel(DotArgs a, int32_t* _
   if (p < a.nnzM) {
     int64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
     if (!dot_lists(a, p, a0, a1, b0, b1)) atomicOr(&a.err[2], 1);
-    ls = (a1 - a0) < (b1 - b0) ? (a1 - a0) : (b1 - b0);
+    const bool a_short = (a1 - a0) <= (b1 - b0);
+    ls = a_short ? (a1 - a0) : (b1 - b0);
+    const int64_t ll = a_short ? (b1 - b0) : (a1 - a0);
     cls = ls <= 0 ? 0 : (ls <= kDotThread ? 1 : 2);
     if (cls == 0) a.Tflag[p] = 0;
+    if (cls == 2 && hub_min > 0 && ll > kDotMergeRatio * ls) {
+      cls = 3;
+      atomicAdd(&gcount[a_short ? (int64_t)a.Mcol[p] : a.nB + (int64_t)a.Mir[p]], 1);
+    }
   }
   const uint64_t lt = (1ull << lane) - 1ull;
-  const uint64_t m1 = __ballot(cls == 1), m2 = __ballot(cls == 2);
-  unsigned long long base1 = 0, base2 = 0;
+  const uint64_t m1 = __ballot(cls == 1), m2 = __ballot(cls == 2), m3 = __ballot(cls == 3);
+  unsigned long long base1 = 0, base2 = 0, base3 = 0;
   if (lane == 0) {
     if (m1) base1 = atomicAdd(&counts[0], (unsigned long long)__popcll(m1));
     if (m2) base2 = atomicAdd(&counts[1], (unsigned long long)__popcll(m2));
+    if (m3) base3 = atomicAdd(&counts[2], (unsigned long long)__popcll(m3));
   }
   base1 = __shfl(base1, 0);
   base2 = __shfl(base2, 0);
+  base3 = __shfl(base3, 0);
   if (cls == 1) lthr[base1 + __popcll(m1 & lt)] = (int32_t)p;
   if (cls == 2) {
     const int64_t x = (int64_t)base2 + __popcll(m2 & lt);
     llong[x] = (int32_t)p;
     npiece[x] = (ls + kDotPiece - 1) / kDotPiece;
   }
+  if (cls == 3) lcand[base3 + __popcll(m3 & lt)] = (int32_t)p;
 }
 
 // thread per short entry: the shorter list drives, the longer one is galloped through
@@ -423,6 +434,199 @@ __global__ __launch_bounds__(256) void dot_fold_kernel(DotArgs a, const int32_t*
   const int64_t p = llong[x];
   a.Tflag[p] = hit ? 1 : 0;
   if (hit) reinterpret_cast<val_t*>(a.Tnum)[p] = acc;
+}
+
+// ---- hub groups (round 6): the entries whose longer list is more than kDotMergeRatio x the
+// shorter (dot_piece's binary-search branch) share their longer list with many other entries when
+// it is a hub's: the mask column j of a long B(:, j) holds |M(:, j)| entries that all intersect it,
+// and the mask row i of a long A(i, :) as many. Such entries are grouped by their longer list (key
+// j, or nB + i) when at least hub_min of them share it. A workgroup takes a chunk of up to kHubECh
+// entries of one group (kHubEPT per thread, their cursors, partials and hit flags in registers)
+// and walks the group's longer list in windows of kHubWin rows: each window is staged in LDS with a
+// bucket directory over its row range, and every thread advances each of its entries' shorter-list
+// cursor through the window's row range, looking every element up in LDS (one directory read and
+// ~1-2 row reads) instead of binary-searching the longer list in HBM. Products fold in ascending k
+// (windows in order, elements in order inside a window).
+constexpr int kHubWin = 8192;   // longer-list rows per window (LDS: 32 KB rows + 16 KB directory)
+constexpr int kHubBS = 512;     // threads per hub workgroup
+constexpr int kHubEPT = 8;      // entries per thread
+constexpr int kHubECh = kHubBS * kHubEPT;  // entries per work item
+constexpr int kHubBatch = 8;    // shorter-list elements a thread loads at once
+
+__device__ __forceinline__ int64_t dot_hub_key(const DotArgs& a, int64_t p, bool& ok) {
+  int64_t a0, a1, b0, b1;
+  ok = dot_lists(a, p, a0, a1, b0, b1);
+  if (!ok) return 0;
+  return (a1 - a0) <= (b1 - b0) ? (int64_t)a.Mcol[p] : a.nB + (int64_t)a.Mir[p];
+}
+// the longer list of group key: B(:, j) for key j < nB, else A(i, :) = AT(:, i)
+__device__ __forceinline__ void dot_hub_list(const DotArgs& a, int64_t key, int64_t& l0, int64_t& l1,
+                                             const int32_t*& lrow) {
+  if (key < a.nB) {
+    l0 = a.Bd[key];
+    l1 = a.Bd[key + 1];
+    lrow = a.Bir;
+  } else {
+    l0 = a.ATd[key - a.nB];
+    l1 = a.ATd[key - a.nB + 1];
+    lrow = a.ATir;
+  }
+}
+
+// per group key: entries (glen: count when >= hub_min, else 0) and work items (entry chunks)
+__global__ __launch_bounds__(256) void dot_hub_sizes_kernel(const int32_t* __restrict__ gcount, int64_t K, int hub_min,
+                                                            int64_t* __restrict__ glen, int64_t* __restrict__ gitems) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  const int64_t c = gcount[k] >= hub_min ? gcount[k] : 0;
+  glen[k] = c;
+  gitems[k] = (c + kHubECh - 1) / kHubECh;
+}
+
+// hub candidates: into their group (goff + a per-group cursor) when the group has >= hub_min
+// entries, else back to the long list (pieces of the wave kernel)
+__global__ __launch_bounds__(256) void dot_hub_route_kernel(DotArgs a, const int32_t* __restrict__ lcand, int64_t n,
+                                                            const int32_t* __restrict__ gcount, int hub_min,
+                                                            const int64_t* __restrict__ goff, int32_t* __restrict__ gcur,
+                                                            int32_t* __restrict__ hs, int32_t* __restrict__ llong,
+                                                            int64_t* __restrict__ npiece,
+                                                            unsigned long long* __restrict__ counts) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  bool back = false;
+  int64_t p = 0, ls = 0;
+  if (x < n) {
+    p = lcand[x];
+    bool ok;
+    const int64_t key = dot_hub_key(a, p, ok);
+    if (ok && gcount[key] >= hub_min) {
+      hs[goff[key] + atomicAdd(&gcur[key], 1)] = (int32_t)p;
+    } else {
+      int64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+      dot_lists(a, p, a0, a1, b0, b1);
+      ls = (a1 - a0) < (b1 - b0) ? (a1 - a0) : (b1 - b0);
+      back = true;
+    }
+  }
+  const uint64_t m = __ballot(back);
+  unsigned long long base = 0;
+  if (lane == 0 && m) base = atomicAdd(&counts[1], (unsigned long long)__popcll(m));
+  base = __shfl(base, 0);
+  if (back) {
+    const int64_t y = (int64_t)base + __popcll(m & ((1ull << lane) - 1ull));
+    llong[y] = (int32_t)p;
+    npiece[y] = (ls + kDotPiece - 1) / kDotPiece;
+  }
+}
+
+// one workgroup per (group, entry chunk), grid-strided over the work items
+template <class SR>
+__global__ __launch_bounds__(kHubBS) void dot_hub_kernel(DotArgs a, const int64_t* __restrict__ ioff, int64_t K,
+                                                         int64_t nitems, const int64_t* __restrict__ goff,
+                                                         const int32_t* __restrict__ hs) {
+  using val_t = typename SR::val_t;
+  __shared__ int32_t s_rows[kHubWin];
+  __shared__ uint16_t s_dir[kHubWin + 1];
+  const val_t* __restrict__ av = reinterpret_cast<const val_t*>(a.ATnum);
+  const val_t* __restrict__ bv = reinterpret_cast<const val_t*>(a.Bnum);
+  for (int64_t it = blockIdx.x; it < nitems; it += gridDim.x) {
+    // the group: last key with ioff[key] <= it (keys without items have ioff[key] == ioff[key + 1])
+    int64_t lo = 0, hi = K;
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (ioff[mid] <= it) lo = mid;
+      else hi = mid;
+    }
+    const int64_t key = lo;
+    int64_t l0, l1;
+    const int32_t* lrow;
+    dot_hub_list(a, key, l0, l1, lrow);
+    const bool b_long = key < a.nB;  // the shorter lists are A(i, :) = AT(:, i), else B(:, j)
+    const int32_t* __restrict__ srow = b_long ? a.ATir : a.Bir;
+    const int64_t* __restrict__ sd = b_long ? a.ATd : a.Bd;
+    const int64_t g0 = goff[key], ge = goff[key + 1] - g0;
+    const int64_t ebase = (it - ioff[key]) * kHubECh;
+    int64_t cur[kHubEPT], send[kHubEPT];
+    val_t acc[kHubEPT];
+    bool hit[kHubEPT];
+    const int32_t first = lrow[l0];
+#pragma unroll
+    for (int j = 0; j < kHubEPT; ++j) {
+      const int64_t e = ebase + j * kHubBS + threadIdx.x;
+      cur[j] = send[j] = 0;
+      acc[j] = val_t{};
+      hit[j] = false;
+      if (e < ge) {
+        const int64_t p = hs[g0 + e];
+        const int64_t sid = b_long ? (int64_t)a.Mir[p] : (int64_t)a.Mcol[p];
+        send[j] = sd[sid + 1];
+        cur[j] = lb_rows64(srow, sd[sid], send[j], first);
+      }
+    }
+    for (int64_t w0 = l0; w0 < l1; w0 += kHubWin) {
+      const int n = (int)((l1 - w0) < kHubWin ? (l1 - w0) : kHubWin);
+      __syncthreads();  // the previous window's readers are done with the LDS
+      for (int t = threadIdx.x; t < n; t += kHubBS) s_rows[t] = lrow[w0 + t];
+      __syncthreads();
+      const int32_t r_lo = s_rows[0], r_hi = s_rows[n - 1];
+      const int64_t span = (int64_t)r_hi - r_lo + 1;
+      // buckets over [r_lo, r_hi]: bucket(k) = (k - r_lo) * n / span; s_dir[b] = first row index
+      // whose bucket >= b (b in [0, n]): element t fills (bucket(t - 1), bucket(t)]
+      auto bucket = [&](int32_t k) -> int { return (int)(((int64_t)(k - r_lo) * n) / span); };
+      for (int t = threadIdx.x; t <= n; t += kHubBS) {
+        const int bt = t < n ? bucket(s_rows[t]) : n;
+        const int bp = t > 0 ? bucket(s_rows[t - 1]) : -1;
+        for (int b = bp + 1; b <= bt; ++b) s_dir[b] = (uint16_t)t;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < kHubEPT; ++j) {
+        int64_t s = cur[j];
+        bool more = s < send[j];
+        while (more) {
+          // kHubBatch elements per step, loaded together (independent loads, mostly one line)
+          int32_t kk[kHubBatch];
+#pragma unroll
+          for (int u = 0; u < kHubBatch; ++u) kk[u] = s + u < send[j] ? srow[s + u] : INT32_MAX;
+          int used = kHubBatch;
+#pragma unroll
+          for (int u = 0; u < kHubBatch; ++u) {
+            const int32_t k = kk[u];
+            if (used < kHubBatch) continue;
+            if (k > r_hi) {  // past the window (or the list: INT32_MAX)
+              used = u;
+              continue;
+            }
+            if (k < r_lo) continue;  // (between the previous window's last row and this one's first)
+            const int b = bucket(k);
+            for (int q = s_dir[b], qe = s_dir[b + 1]; q < qe; ++q) {
+              const int32_t r = s_rows[q];
+              if (r < k) continue;
+              if (r == k) {
+                const int64_t qg = w0 + q, sq = s + u;
+                const val_t pr = b_long ? SR::multiply(av[sq], bv[qg]) : SR::multiply(av[qg], bv[sq]);
+                acc[j] = hit[j] ? SR::add(acc[j], pr) : pr;
+                hit[j] = true;
+              }
+              break;
+            }
+          }
+          s += used;
+          more = used == kHubBatch && s < send[j];
+        }
+        cur[j] = s < send[j] ? s : send[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kHubEPT; ++j) {
+      const int64_t e = ebase + j * kHubBS + threadIdx.x;
+      if (e < ge) {
+        const int64_t p = hs[g0 + e];
+        a.Tflag[p] = hit[j] ? 1 : 0;
+        if (hit[j]) reinterpret_cast<val_t*>(a.Tnum)[p] = acc[j];
+      }
+    }
+  }
 }
 
 // hits per mask column (wave per slot) and, with WRITE, the compaction of the hit entries in

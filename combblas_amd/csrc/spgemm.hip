@@ -2779,6 +2779,16 @@ extern "C" int cbh_transpose(cbh_ctx* ctx, const cbh_mat* A, cbh_mat** AT) {
   return cbh_tuples_to_dcsc(ctx, A->n, A->m, A->nnz, trow, tcol, A->num, (cbh_dtype)A->dtype, 0, AT);
 }
 
+// entries sharing one longer list that make it a hub group (apps.h); CBH_DOT_HUB_MIN overrides
+// (read per call), 0 keeps every long entry on the wave kernel's binary search. Measured at R-MAT
+// scale 24 (C4, profiles/r06/tc_hub): 16 / 128 / 512 / 2048 / 4096 / 16384 -> 7.81 / 7.64 / 7.59 /
+// 7.53 / 7.67 / 8.00 s per step against 8.11 s without groups: a group needs enough entries to
+// fill its workgroups' threads over every window of its longer list
+static int dot_hub_min() {
+  const char* e = std::getenv("CBH_DOT_HUB_MIN");
+  return e ? std::max(0, std::atoi(e)) : 2048;
+}
+
 // C = (A*B) .* M, dot form (apps.h, "masked SpGEMM, dot form")
 template <class SR>
 static int masked_dot(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, const cbh_mat* M, bool pattern, cbh_mat** C) {
@@ -2804,7 +2814,7 @@ static int masked_dot(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, const cb
   CBH_TRY(S.get(&lthr, nm));
   CBH_TRY(S.get(&llong, nm));
   CBH_TRY(S.get(&npiece, nm + 1));
-  CBH_TRY(S.get(&counts, 2));
+  CBH_TRY(S.get(&counts, 3));
   CBH_TRY(S.get(&Tnum, nm));
   CBH_TRY(S.get(&Tflag, nm));
   hipLaunchKernelGGL(densify_cp_kernel, dim3(blocks_for(A->m + 1, 256)), dim3(256), 0, ctx->stream, AT->jc, AT->cp,
@@ -2812,16 +2822,60 @@ static int masked_dot(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, const cb
   hipLaunchKernelGGL(densify_cp_kernel, dim3(blocks_for(B->n + 1, 256)), dim3(256), 0, ctx->stream, B->jc, B->cp,
                      B->nzc, B->n, B->nnz, Bd);
   hipLaunchKernelGGL(expand_cols_kernel, dim3(blocks_for(nzc, 4)), dim3(256), 0, ctx->stream, M->jc, M->cp, nzc, Mcol);
-  CBH_HIP(ctx, hipMemsetAsync(counts, 0, 2 * sizeof(unsigned long long), ctx->stream));
+  CBH_HIP(ctx, hipMemsetAsync(counts, 0, 3 * sizeof(unsigned long long), ctx->stream));
   DotArgs a{ATd, AT->ir, AT->num, Bd, B->ir, B->num, Mcol, M->ir, nm, A->m, B->n, Tnum, Tflag, ctx->d_err};
+  // hub groups (apps.h): entries of the binary-search branch grouped by their longer list
+  const int hub_min = dot_hub_min();
+  const int64_t K = B->n + A->m;  // group keys: j < nB (B(:, j) longer), nB + i (A(i, :) longer)
+  int32_t *gcount = nullptr, *lcand = nullptr;
+  if (hub_min > 0) {
+    CBH_TRY(S.get(&gcount, K));
+    CBH_TRY(S.get(&lcand, nm));
+    CBH_HIP(ctx, hipMemsetAsync(gcount, 0, sizeof(int32_t) * K, ctx->stream));
+  }
   hipLaunchKernelGGL(dot_classify_kernel, dim3(blocks_for(nm, 256)), dim3(256), 0, ctx->stream, a, lthr, llong, npiece,
-                     counts);
+                     counts, hub_min, gcount, lcand);
   CBH_HIP(ctx, hipGetLastError());
-  unsigned long long cnt[2];
+  unsigned long long cnt[3];
   CBH_HIP(ctx, hipMemcpyAsync(cnt, counts, sizeof(cnt), hipMemcpyDeviceToHost, ctx->stream));
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   CBH_TRY(check_err(ctx));
-  const int64_t nthr = (int64_t)cnt[0], nlong = (int64_t)cnt[1];
+  const int64_t nthr = (int64_t)cnt[0], ncand = (int64_t)cnt[2];
+  int64_t nlong = (int64_t)cnt[1], nh = 0, nhitems = 0;
+  int64_t *goff = nullptr, *ioff = nullptr;
+  int32_t* hs = nullptr;
+  if (ncand > 0) {
+    int64_t *glen, *gitems;
+    int32_t* gcur;
+    CBH_TRY(S.get(&glen, K + 1));
+    CBH_TRY(S.get(&gitems, K + 1));
+    CBH_TRY(S.get(&goff, K + 1));
+    CBH_TRY(S.get(&ioff, K + 1));
+    CBH_TRY(S.get(&gcur, K));
+    CBH_TRY(S.get(&hs, ncand));
+    hipLaunchKernelGGL(dot_hub_sizes_kernel, dim3(blocks_for(K, 256)), dim3(256), 0, ctx->stream, gcount, K, hub_min,
+                       glen, gitems);
+    CBH_HIP(ctx, hipMemsetAsync(glen + K, 0, sizeof(int64_t), ctx->stream));
+    CBH_HIP(ctx, hipMemsetAsync(gitems + K, 0, sizeof(int64_t), ctx->stream));
+    CBH_TRY(exclusive_scan_i64(ctx, S, glen, goff, K + 1));
+    CBH_TRY(exclusive_scan_i64(ctx, S, gitems, ioff, K + 1));
+    CBH_HIP(ctx, hipMemsetAsync(gcur, 0, sizeof(int32_t) * K, ctx->stream));
+    hipLaunchKernelGGL(dot_hub_route_kernel, dim3(blocks_for(ncand, 256)), dim3(256), 0, ctx->stream, a, lcand, ncand,
+                       gcount, hub_min, goff, gcur, hs, llong, npiece, counts);
+    CBH_HIP(ctx, hipGetLastError());
+    int64_t h2[2];
+    CBH_HIP(ctx, hipMemcpyAsync(&h2[0], goff + K, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(&h2[1], ioff + K, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(cnt, counts, sizeof(cnt), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    nh = h2[0];
+    nhitems = h2[1];
+    if (nh + ((int64_t)cnt[1] - nlong) != ncand) return fail(ctx, CBH_E_INTERNAL, "dot-form hub routing lost entries");
+    nlong = (int64_t)cnt[1];
+    if (diag_enabled())
+      std::fprintf(stderr, "[cbh diag] dot hub: %lld candidates, %lld grouped (%lld work items), %lld long\n",
+                   (long long)ncand, (long long)nh, (long long)nhitems, (long long)nlong);
+  }
   if (nthr > 0)
     hipLaunchKernelGGL(dot_thread_kernel<SR>, dim3(blocks_for(nthr, 256)), dim3(256), 0, ctx->stream, a, lthr, nthr);
   if (nlong > 0) {
@@ -2845,6 +2899,9 @@ static int masked_dot(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, const cb
     hipLaunchKernelGGL(dot_fold_kernel<SR>, dim3(blocks_for(nlong, 256)), dim3(256), 0, ctx->stream, a, llong, poff,
                        nlong, pval, phit);
   }
+  if (nh > 0)
+    hipLaunchKernelGGL(dot_hub_kernel<SR>, dim3((unsigned)std::min<int64_t>(nhitems, 1 << 20)), dim3(kHubBS), 0,
+                       ctx->stream, a, ioff, K, nhitems, goff, hs);
   CBH_HIP(ctx, hipGetLastError());
   CBH_TRY(S.get(&hits, nzc + 1));
   CBH_TRY(S.get(&off, nzc + 1));

@@ -77,11 +77,18 @@ def test_tc_device_lower_vs_reference_digest(ctx, scale, method):
 
 @pytest.mark.parametrize("tag", ["pt_i64", "pt_f64", "max_i64", "min_i64", "bool"])
 @pytest.mark.parametrize("pattern", [False, True])
-def test_masked_dot_vs_oracle(ctx, oracle, tag, pattern):
+@pytest.mark.parametrize("hub", [None, "0", "1"])
+def test_masked_dot_vs_oracle(ctx, oracle, tag, pattern, hub, monkeypatch):
     """the dot form on a rectangular product with long rows of A and long columns of B (pieces of
-    the wave kernel), every semiring, explicit zeros, empty mask columns"""
+    the wave kernel), every semiring, explicit zeros, empty mask columns; hub: the entries of the
+    binary-search branch grouped by their longer list (apps.h hub groups: B's dense column 11 and A's
+    dense rows 7 and 123) at the default group size (None: groups of 20-30 entries stay on the
+    binary search), never ("0"), always ("1")"""
     from combblas_amd.apps import MaskedSpGEMM
     from combblas_amd.semirings import ALL
+
+    if hub is not None:
+        monkeypatch.setenv("CBH_DOT_HUB_MIN", hub)
 
     rng = np.random.default_rng(17)
 
