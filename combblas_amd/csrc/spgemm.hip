@@ -897,6 +897,9 @@ __global__ void dense_split_kernel(const int64_t* __restrict__ tcnt, const int32
   wd[t] = d ? w : 0;
   wh[t] = d ? 0 : (w > 0 && w <= smallcap && flops && flops[t] > wavemax ? smallcap + 1 : w);
 }
+#ifndef CBH_SYM_SPLIT4  // (A/B hook) bitmap sub-tiles allowed per hash sub-tile, in quarters
+#define CBH_SYM_SPLIT4 4
+#endif
 // symbolic tasks split between the one-workgroup-per-CU bitmap kernel (dense_kernel.h, SYM) and
 // the task kernels: wb / wh = the task's flops in the kernel it goes to, 0 in the other. A large
 // task (flops > midcap) runs the bitmap kernel when it stores its bitmap (a dense candidate) or when
@@ -912,7 +915,7 @@ __global__ void sym_split_kernel(const int64_t* __restrict__ twork, const int32_
   bool b = false;
   if (w > midcap && span > 0) {
     const bool store = boff != nullptr && boff[t + 1] > boff[t];
-    b = store || (span + nws_rows - 1) / nws_rows <= (w + hashcap - 1) / hashcap;
+    b = store || 4 * ((span + nws_rows - 1) / nws_rows) <= CBH_SYM_SPLIT4 * ((w + hashcap - 1) / hashcap);
   }
   wb[t] = b ? w : 0;
   wh[t] = b ? 0 : w;
