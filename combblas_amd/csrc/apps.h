@@ -209,12 +209,13 @@ __device__ __forceinline__ bool dot_lists(const DotArgs& a, int64_t p, int64_t& 
 
 // class of every mask entry: 0 = empty intersection for sure (a list is empty: flag 0 written
 // here), 1 = thread, 2 = long (pieces), 3 = hub candidate (hub_min > 0 and the longer list more
-// than kDotMergeRatio x the shorter: counted into its group, gcount[key]). Waves append their
+// than hub_ratio x the shorter: counted into its group, gcount[key]). Waves append their
 // entries to the class lists with one atomic per class; npiece[x] = pieces of long entry x.
 __global__ __launch_bounds__(256) void dot_classify_kernel(DotArgs a, int32_t* __restrict__ lthr,
                                                            int32_t* __restrict__ llong, int64_t* __restrict__ npiece,
                                                            unsigned long long* __restrict__ counts, int hub_min,
-                                                           int32_t* __restrict__ gcount, int32_t* __restrict__ lcand) {
+                                                           int hub_ratio, int32_t* __restrict__ gcount,
+                                                           int32_t* __restrict__ lcand) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
   int cls = -1;
@@ -227,7 +228,7 @@ __global__ __launch_bounds__(256) void dot_classify_kernel(DotArgs a, int32_t* _
     const int64_t ll = a_short ? (b1 - b0) : (a1 - a0);
     cls = ls <= 0 ? 0 : (ls <= kDotThread ? 1 : 2);
     if (cls == 0) a.Tflag[p] = 0;
-    if (cls == 2 && hub_min > 0 && ll > kDotMergeRatio * ls) {
+    if (cls == 2 && hub_min > 0 && ll > hub_ratio * ls) {
       cls = 3;
       atomicAdd(&gcount[a_short ? (int64_t)a.Mcol[p] : a.nB + (int64_t)a.Mir[p]], 1);
     }

@@ -2792,6 +2792,13 @@ static int dot_hub_min() {
   return e ? std::max(0, std::atoi(e)) : 2048;
 }
 
+// longer / shorter list length above which a long entry is a hub candidate (CBH_DOT_HUB_RATIO,
+// read per call; default kDotMergeRatio: exactly the wave kernel's binary-search entries)
+static int dot_hub_ratio() {
+  const char* e = std::getenv("CBH_DOT_HUB_RATIO");
+  return e ? std::max(1, std::atoi(e)) : kDotMergeRatio;
+}
+
 // C = (A*B) .* M, dot form (apps.h, "masked SpGEMM, dot form")
 template <class SR>
 static int masked_dot(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, const cbh_mat* M, bool pattern, cbh_mat** C) {
@@ -2837,7 +2844,7 @@ static int masked_dot(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, const cb
     CBH_HIP(ctx, hipMemsetAsync(gcount, 0, sizeof(int32_t) * K, ctx->stream));
   }
   hipLaunchKernelGGL(dot_classify_kernel, dim3(blocks_for(nm, 256)), dim3(256), 0, ctx->stream, a, lthr, llong, npiece,
-                     counts, hub_min, gcount, lcand);
+                     counts, hub_min, dot_hub_ratio(), gcount, lcand);
   CBH_HIP(ctx, hipGetLastError());
   unsigned long long cnt[3];
   CBH_HIP(ctx, hipMemcpyAsync(cnt, counts, sizeof(cnt), hipMemcpyDeviceToHost, ctx->stream));
