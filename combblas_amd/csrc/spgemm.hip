@@ -2910,7 +2910,7 @@ static int masked_dot(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, const cb
                        nlong, pval, phit);
   }
   if (nh > 0)
-    hipLaunchKernelGGL(dot_hub_kernel<SR>, dim3((unsigned)std::min<int64_t>(nhitems, 1 << 20)), dim3(kHubBS), 0,
+    hipLaunchKernelGGL(dot_hub_kernel<SR>, dim3((unsigned)std::min<int64_t>(nhitems, wave_grid_cap())), dim3(kHubBS), 0,
                        ctx->stream, a, ioff, K, nhitems, goff, hs);
   CBH_HIP(ctx, hipGetLastError());
   CBH_TRY(S.get(&hits, nzc + 1));

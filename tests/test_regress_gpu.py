@@ -134,13 +134,16 @@ def test_hash_commit_queue_only_overflow(ctx, oracle, nentries, dtype):
 
 
 @pytest.mark.parametrize("scale", [12, 14])
-def test_tc_dot_grid_cap_strides(ctx, scale, monkeypatch):
+@pytest.mark.parametrize("hub", [None, "1"])
+def test_tc_dot_grid_cap_strides(ctx, scale, hub, monkeypatch):
     from combblas_amd.apps import MaskedSpGEMM, TCLower
     from combblas_amd.semirings import PlusTimesSRing
 
     with open(os.path.join(H.GOLDEN, "tc.json")) as f:
         ref = json.load(f)["scales"][str(scale)]
     monkeypatch.setenv("CBH_TEST_GRID_CAP", "1")  # 4 waves stride over every piece
+    if hub is not None:  # every binary-search entry in a hub group: one workgroup strides over them
+        monkeypatch.setenv("CBH_DOT_HUB_MIN", hub)
     L, L2 = TCLower(ctx, scale), TCLower(ctx, scale)
     C = MaskedSpGEMM(PlusTimesSRing, L, L2, L, method="dot")
     h = C.to_host()
