@@ -31,6 +31,14 @@
 #pragma once
 
 // CBH_GATHER_PIN (default 1): pin the window gathers before the updates (sweep() below)
+// CBH_HASH_BATCH (A/B hook, default 0): the numeric hash issues the first probe of all U products
+// of a batch before using any result, instead of probing each product to completion before the
+// next one starts. Measured slower (round 6, profiles/r06/hash_batch: hash 236.7 -> 251.2 ms per
+// scale-22 product): the kernel is issue-bound, not latency-bound, and the per-product pending
+// flags cost more SALU mask arithmetic than the overlapped probes save
+#ifndef CBH_HASH_BATCH
+#define CBH_HASH_BATCH 0
+#endif
 #ifndef CBH_GATHER_PIN
 #define CBH_GATHER_PIN 1
 #endif
@@ -739,7 +747,9 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
   val_t av[U];  // numeric: A value * B value (the product), once values are gathered
   // One sweep over the windows of the current entry set: owner map, gather U products per
   // thread (all loads in flight), then `upd(u)` for every product this thread holds.
-  auto sweep = [&](int nec, int P, bool with_vals, auto&& upd) {
+  // upd(u) updates the table with product u of the current batch; a non-null `batch(wn)` replaces
+  // the per-product calls (the numeric hash's batched first probes, CBH_HASH_BATCH)
+  auto sweep = [&](int nec, int P, bool with_vals, auto&& upd, auto&& batch) {
     int carry = -1;  // owner of the product just before the window
     for (int w0 = 0; w0 < P; w0 += WIN) {
       const int wn = (P - w0) < WIN ? (P - w0) : WIN;
@@ -799,9 +809,13 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
         }
       }
 #endif
+      if constexpr (std::is_same<std::decay_t<decltype(batch)>, std::nullptr_t>::value) {
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (tid + u * BS < wn) upd(u);
+        for (int u = 0; u < U; ++u)
+          if (tid + u * BS < wn) upd(u);
+      } else {
+        batch(wn);
+      }
       __syncthreads();
       CBH_STAMP(5);
     }
@@ -944,7 +958,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
             }
             // no store wait: the thread that wrote an entry's cursor is the one that reloads it
           }
-          sweep(nec, P, true, place);  // ends with a barrier: the entry state may be reloaded
+          sweep(nec, P, true, place, nullptr);  // ends with a barrier: the entry state may be reloaded
         }
         // commit: values are in row order (rank q = output out_pos + q: coalesced); the rows are
         // read off the bitmap, word x's set bits being ranks dp[x]..
@@ -1039,10 +1053,58 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
 #endif
       CBH_STAMP(3);
       if (!NUM && bitmap) {
-        sweep(nec, P, false, [&](int u) {
-          const uint32_t d = (uint32_t)(r[u] - lo);
-          if (d >= tw) bad |= 1 << 8;
-          else atomicOr(&words[d >> 5], 1u << (d & 31));
+        sweep(
+            nec, P, false,
+            [&](int u) {
+              const uint32_t d = (uint32_t)(r[u] - lo);
+              if (d >= tw) bad |= 1 << 8;
+              else atomicOr(&words[d >> 5], 1u << (d & 31));
+            },
+            nullptr);
+      } else if constexpr (NUM && !LOCKED && CBH_HASH_BATCH) {
+        // every product's first probe issued before any result is used (U CAS in flight per
+        // thread instead of U dependent probe chains); the products whose home slot holds another
+        // row probe on afterwards, one by one
+        sweep(nec, P, true, [&](int) {}, [&](int wn) {
+          uint32_t hs[U];
+          int32_t hk[U];
+          bool need[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            need[u] = false;
+            hs[u] = 0;
+            if (tid + u * BS < wn) {
+              const uint32_t d = (uint32_t)(r[u] - lo);
+              if (d >= tw) bad |= 1 << 8;
+              else {
+                hs[u] = (uint32_t)(((uint64_t)d * scale) >> 32);
+                need[u] = true;
+              }
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) hk[u] = need[u] ? atomicCAS(&keys[hs[u]], kEmpty, r[u]) : kEmpty;
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (need[u] && (hk[u] == kEmpty || hk[u] == r[u])) {
+              SR::lds_acc(&vals[hs[u]], av[u]);
+              need[u] = false;
+            }
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (need[u]) {
+              bool ok = false;
+              uint32_t sl = hs[u] + 1;
+              for (int probe = 1; probe < kPmax && sl < (uint32_t)TA; ++probe, ++sl) {
+                const int32_t k = atomicCAS(&keys[sl], kEmpty, r[u]);
+                if (k == kEmpty || k == r[u]) {
+                  SR::lds_acc(&vals[sl], av[u]);
+                  ok = true;
+                  break;
+                }
+              }
+              if (!ok) set_ovf();
+            }
         });
       } else if constexpr (NUM) {
         sweep(nec, P, true, [&](int u) {
@@ -1071,7 +1133,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
             }
           }
           if (!ok) set_ovf();
-        });
+        }, nullptr);
       } else {
         sweep(nec, P, false, [&](int u) {
           const uint32_t d = (uint32_t)(r[u] - lo);
@@ -1092,7 +1154,7 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
             }
           }
           if (!ok) set_ovf();
-        });
+        }, nullptr);
       }
       if (__hip_atomic_load(&s_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
         for (int i = tid; i < nec; i += BS) epos[i] += eoff[i];  // back to the cursors
