@@ -208,13 +208,14 @@ __device__ __forceinline__ bool dot_lists(const DotArgs& a, int64_t p, int64_t& 
 }
 
 // class of every mask entry: 0 = empty intersection for sure (a list is empty: flag 0 written
-// here), 1 = thread, 2 = long (pieces), 3 = hub candidate (hub_min > 0 and the longer list more
-// than hub_ratio x the shorter: counted into its group, gcount[key]). Waves append their
+// here), 1 = thread, 2 = long (pieces), 3 = hub candidate (hub_min > 0 and the longer list at most
+// hub_wave x the shorter -- a wave-mode group, key + nB + mA -- or more than hub_ratio x the
+// shorter -- a thread-mode group, key: counted into its group, gcount[key]). Waves append their
 // entries to the class lists with one atomic per class; npiece[x] = pieces of long entry x.
 __global__ __launch_bounds__(256) void dot_classify_kernel(DotArgs a, int32_t* __restrict__ lthr,
                                                            int32_t* __restrict__ llong, int64_t* __restrict__ npiece,
                                                            unsigned long long* __restrict__ counts, int hub_min,
-                                                           int hub_ratio, int32_t* __restrict__ gcount,
+                                                           int hub_ratio, int hub_wave, int32_t* __restrict__ gcount,
                                                            int32_t* __restrict__ lcand) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
@@ -228,9 +229,13 @@ __global__ __launch_bounds__(256) void dot_classify_kernel(DotArgs a, int32_t* _
     const int64_t ll = a_short ? (b1 - b0) : (a1 - a0);
     cls = ls <= 0 ? 0 : (ls <= kDotThread ? 1 : 2);
     if (cls == 0) a.Tflag[p] = 0;
-    if (cls == 2 && hub_min > 0 && ll > hub_ratio * ls) {
-      cls = 3;
-      atomicAdd(&gcount[a_short ? (int64_t)a.Mcol[p] : a.nB + (int64_t)a.Mir[p]], 1);
+    if (cls == 2 && hub_min > 0) {
+      const bool wave = hub_wave > 0 && ll <= (int64_t)hub_wave * ls;
+      if (wave || ll > hub_ratio * ls) {
+        cls = 3;
+        const int64_t key = a_short ? (int64_t)a.Mcol[p] : a.nB + (int64_t)a.Mir[p];
+        atomicAdd(&gcount[key + (wave ? a.nB + a.mA : 0)], 1);
+      }
     }
   }
   const uint64_t lt = (1ull << lane) - 1ull;
@@ -453,16 +458,23 @@ constexpr int kHubBS = 512;     // threads per hub workgroup
 constexpr int kHubEPT = 8;      // entries per thread
 constexpr int kHubECh = kHubBS * kHubEPT;  // entries per work item
 constexpr int kHubBatch = 8;    // shorter-list elements a thread loads at once
+constexpr int kHubEPW = 8;      // wave mode: entries per wave
+constexpr int kHubWCh = (kHubBS / 64) * kHubEPW;  // wave mode: entries per work item
 
-__device__ __forceinline__ int64_t dot_hub_key(const DotArgs& a, int64_t p, bool& ok) {
+// group key of a hub candidate: j (B(:, j) longer) or nB + i (A(i, :) longer), + nB + mA in wave mode
+__device__ __forceinline__ int64_t dot_hub_key(const DotArgs& a, int64_t p, int hub_wave, bool& ok) {
   int64_t a0, a1, b0, b1;
   ok = dot_lists(a, p, a0, a1, b0, b1);
   if (!ok) return 0;
-  return (a1 - a0) <= (b1 - b0) ? (int64_t)a.Mcol[p] : a.nB + (int64_t)a.Mir[p];
+  const bool a_short = (a1 - a0) <= (b1 - b0);
+  const int64_t ls = a_short ? (a1 - a0) : (b1 - b0), ll = a_short ? (b1 - b0) : (a1 - a0);
+  const bool wave = hub_wave > 0 && ll <= (int64_t)hub_wave * ls;
+  return (a_short ? (int64_t)a.Mcol[p] : a.nB + (int64_t)a.Mir[p]) + (wave ? a.nB + a.mA : 0);
 }
-// the longer list of group key: B(:, j) for key j < nB, else A(i, :) = AT(:, i)
+// the longer list of group key (either mode): B(:, j) for j < nB, else A(i, :) = AT(:, i)
 __device__ __forceinline__ void dot_hub_list(const DotArgs& a, int64_t key, int64_t& l0, int64_t& l1,
                                              const int32_t*& lrow) {
+  if (key >= a.nB + a.mA) key -= a.nB + a.mA;
   if (key < a.nB) {
     l0 = a.Bd[key];
     l1 = a.Bd[key + 1];
@@ -474,20 +486,24 @@ __device__ __forceinline__ void dot_hub_list(const DotArgs& a, int64_t key, int6
   }
 }
 
-// per group key: entries (glen: count when >= hub_min, else 0) and work items (entry chunks)
+// per group key (K thread-mode keys, then K wave-mode keys): entries (glen: count when >= hub_min,
+// else 0) and work items (entry chunks of the mode)
 __global__ __launch_bounds__(256) void dot_hub_sizes_kernel(const int32_t* __restrict__ gcount, int64_t K, int hub_min,
-                                                            int64_t* __restrict__ glen, int64_t* __restrict__ gitems) {
+                                                            int hub_wmin, int64_t* __restrict__ glen,
+                                                            int64_t* __restrict__ gitems) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K) return;
-  const int64_t c = gcount[k] >= hub_min ? gcount[k] : 0;
+  if (k >= 2 * K) return;
+  const int64_t c = gcount[k] >= (k < K ? hub_min : hub_wmin) ? gcount[k] : 0;
+  const int64_t ch = k < K ? kHubECh : kHubWCh;
   glen[k] = c;
-  gitems[k] = (c + kHubECh - 1) / kHubECh;
+  gitems[k] = (c + ch - 1) / ch;
 }
 
 // hub candidates: into their group (goff + a per-group cursor) when the group has >= hub_min
 // entries, else back to the long list (pieces of the wave kernel)
 __global__ __launch_bounds__(256) void dot_hub_route_kernel(DotArgs a, const int32_t* __restrict__ lcand, int64_t n,
-                                                            const int32_t* __restrict__ gcount, int hub_min,
+                                                            const int32_t* __restrict__ gcount, int hub_min, int hub_wmin,
+                                                            int hub_wave,
                                                             const int64_t* __restrict__ goff, int32_t* __restrict__ gcur,
                                                             int32_t* __restrict__ hs, int32_t* __restrict__ llong,
                                                             int64_t* __restrict__ npiece,
@@ -499,8 +515,8 @@ __global__ __launch_bounds__(256) void dot_hub_route_kernel(DotArgs a, const int
   if (x < n) {
     p = lcand[x];
     bool ok;
-    const int64_t key = dot_hub_key(a, p, ok);
-    if (ok && gcount[key] >= hub_min) {
+    const int64_t key = dot_hub_key(a, p, hub_wave, ok);
+    if (ok && gcount[key] >= (key < a.nB + a.mA ? hub_min : hub_wmin)) {
       hs[goff[key] + atomicAdd(&gcur[key], 1)] = (int32_t)p;
     } else {
       int64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
@@ -625,6 +641,118 @@ __global__ __launch_bounds__(kHubBS) void dot_hub_kernel(DotArgs a, const int64_
         const int64_t p = hs[g0 + e];
         a.Tflag[p] = hit[j] ? 1 : 0;
         if (hit[j]) reinterpret_cast<val_t*>(a.Tnum)[p] = acc[j];
+      }
+    }
+  }
+}
+
+// wave mode (the entries whose longer list is at most hub_wave x the shorter): one wave per entry,
+// kHubEPW entries per wave, the lanes taking 64 consecutive shorter-list elements per step
+// (coalesced) and looking them up in the staged window; the elements inside a window are a prefix
+// of the rest of the (sorted) list, so a step advances the cursor by the ballot's count. Lane
+// partials are folded in lane order at the end (as dot_piece's).
+template <class SR>
+__global__ __launch_bounds__(kHubBS) void dot_hub_wave_kernel(DotArgs a, const int64_t* __restrict__ ioff, int64_t K,
+                                                              int64_t it0, int64_t it1, const int64_t* __restrict__ goff,
+                                                              const int32_t* __restrict__ hs) {
+  using val_t = typename SR::val_t;
+  __shared__ int32_t s_rows[kHubWin];
+  __shared__ uint16_t s_dir[kHubWin + 1];
+  const val_t* __restrict__ av = reinterpret_cast<const val_t*>(a.ATnum);
+  const val_t* __restrict__ bv = reinterpret_cast<const val_t*>(a.Bnum);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int64_t it = it0 + blockIdx.x; it < it1; it += gridDim.x) {
+    int64_t lo = K, hi = 2 * K;  // the group: last wave-mode key with ioff[key] <= it
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (ioff[mid] <= it) lo = mid;
+      else hi = mid;
+    }
+    const int64_t gkey = lo;
+    int64_t l0, l1;
+    const int32_t* lrow;
+    dot_hub_list(a, gkey, l0, l1, lrow);
+    const bool b_long = gkey - K < a.nB;  // the shorter lists are A(i, :) = AT(:, i), else B(:, j)
+    const int32_t* __restrict__ srow = b_long ? a.ATir : a.Bir;
+    const int64_t* __restrict__ sd = b_long ? a.ATd : a.Bd;
+    const int64_t g0 = goff[gkey], ge = goff[gkey + 1] - g0;
+    const int64_t ebase = (it - ioff[gkey]) * kHubWCh;
+    int64_t cur[kHubEPW], send[kHubEPW];
+    val_t acc[kHubEPW];
+    bool hit[kHubEPW];
+    const int32_t first = lrow[l0];
+#pragma unroll
+    for (int j = 0; j < kHubEPW; ++j) {
+      const int64_t e = ebase + j * (kHubBS / 64) + wid;
+      cur[j] = send[j] = 0;
+      acc[j] = val_t{};
+      hit[j] = false;
+      if (e < ge) {  // (wave-uniform)
+        const int64_t p = hs[g0 + e];
+        const int64_t sid = b_long ? (int64_t)a.Mir[p] : (int64_t)a.Mcol[p];
+        send[j] = sd[sid + 1];
+        cur[j] = lb_rows64(srow, sd[sid], send[j], first);
+      }
+    }
+    for (int64_t w0 = l0; w0 < l1; w0 += kHubWin) {
+      const int n = (int)((l1 - w0) < kHubWin ? (l1 - w0) : kHubWin);
+      __syncthreads();
+      for (int t = threadIdx.x; t < n; t += kHubBS) s_rows[t] = lrow[w0 + t];
+      __syncthreads();
+      const int32_t r_lo = s_rows[0], r_hi = s_rows[n - 1];
+      const int64_t span = (int64_t)r_hi - r_lo + 1;
+      auto bucket = [&](int32_t k) -> int { return (int)(((int64_t)(k - r_lo) * n) / span); };
+      for (int t = threadIdx.x; t <= n; t += kHubBS) {
+        const int bt = t < n ? bucket(s_rows[t]) : n;
+        const int bp = t > 0 ? bucket(s_rows[t - 1]) : -1;
+        for (int b = bp + 1; b <= bt; ++b) s_dir[b] = (uint16_t)t;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < kHubEPW; ++j) {
+        int64_t s = cur[j];
+        while (s < send[j]) {
+          const int64_t q = s + lane;
+          const int32_t k = q < send[j] ? srow[q] : INT32_MAX;
+          const bool in = k <= r_hi;
+          const int nin = __popcll(__ballot(in));
+          if (in && k >= r_lo) {
+            const int b = bucket(k);
+            for (int x = s_dir[b], xe = s_dir[b + 1]; x < xe; ++x) {
+              const int32_t r = s_rows[x];
+              if (r < k) continue;
+              if (r == k) {
+                const int64_t qg = w0 + x;
+                const val_t pr = b_long ? SR::multiply(av[q], bv[qg]) : SR::multiply(av[qg], bv[q]);
+                acc[j] = hit[j] ? SR::add(acc[j], pr) : pr;
+                hit[j] = true;
+              }
+              break;
+            }
+          }
+          s += nin;
+          if (nin < 64) break;
+        }
+        cur[j] = s;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kHubEPW; ++j) {
+      val_t v = acc[j];
+      bool h = hit[j];
+      for (int d = 1; d < 64; d <<= 1) {  // lane l absorbs lane l + d: lanes in order
+        const val_t o = shfl_down_val(v, d);
+        const int oh = __shfl_down((int)h, d);
+        if ((lane & (2 * d - 1)) == 0 && lane + d < 64 && oh) {
+          v = h ? SR::add(v, o) : o;
+          h = true;
+        }
+      }
+      const int64_t e = ebase + j * (kHubBS / 64) + wid;
+      if (lane == 0 && e < ge) {
+        const int64_t p = hs[g0 + e];
+        a.Tflag[p] = h ? 1 : 0;
+        if (h) reinterpret_cast<val_t*>(a.Tnum)[p] = v;
       }
     }
   }

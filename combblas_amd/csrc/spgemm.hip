@@ -2799,6 +2799,20 @@ static int dot_hub_ratio() {
   return e ? std::max(1, std::atoi(e)) : kDotMergeRatio;
 }
 
+// longer / shorter list length at or below which a long entry is a wave-mode hub candidate
+// (CBH_DOT_HUB_WAVE, read per call; 0 = no wave mode). C4 at scale 24 (profiles/r06/tc_hub):
+// 0 / 2 / 8 / 12 / 16 / 24 / 32 / 64 -> 7.56 / 7.58 / 7.24 / 6.66 / 6.66 / 6.53 / 6.77 / 6.77 s
+static int dot_hub_wave() {
+  const char* e = std::getenv("CBH_DOT_HUB_WAVE");
+  return e ? std::max(0, std::atoi(e)) : 24;
+}
+
+// entries per wave-mode hub group (CBH_DOT_HUB_WMIN, read per call; default: the thread mode's)
+static int dot_hub_wmin(int hub_min) {
+  const char* e = std::getenv("CBH_DOT_HUB_WMIN");
+  return e ? std::max(1, std::atoi(e)) : hub_min;
+}
+
 // C = (A*B) .* M, dot form (apps.h, "masked SpGEMM, dot form")
 template <class SR>
 static int masked_dot(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, const cbh_mat* M, bool pattern, cbh_mat** C) {
@@ -2837,54 +2851,59 @@ static int masked_dot(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, const cb
   // hub groups (apps.h): entries of the binary-search branch grouped by their longer list
   const int hub_min = dot_hub_min();
   const int64_t K = B->n + A->m;  // group keys: j < nB (B(:, j) longer), nB + i (A(i, :) longer)
-  int32_t *gcount = nullptr, *lcand = nullptr;
+  const int hub_wave = dot_hub_wave();
+  const int hub_wmin = dot_hub_wmin(hub_min);
+  int32_t *gcount = nullptr, *lcand = nullptr;  // K thread-mode keys, then K wave-mode keys
   if (hub_min > 0) {
-    CBH_TRY(S.get(&gcount, K));
+    CBH_TRY(S.get(&gcount, 2 * K));
     CBH_TRY(S.get(&lcand, nm));
-    CBH_HIP(ctx, hipMemsetAsync(gcount, 0, sizeof(int32_t) * K, ctx->stream));
+    CBH_HIP(ctx, hipMemsetAsync(gcount, 0, sizeof(int32_t) * 2 * K, ctx->stream));
   }
   hipLaunchKernelGGL(dot_classify_kernel, dim3(blocks_for(nm, 256)), dim3(256), 0, ctx->stream, a, lthr, llong, npiece,
-                     counts, hub_min, dot_hub_ratio(), gcount, lcand);
+                     counts, hub_min, dot_hub_ratio(), hub_wave, gcount, lcand);
   CBH_HIP(ctx, hipGetLastError());
   unsigned long long cnt[3];
   CBH_HIP(ctx, hipMemcpyAsync(cnt, counts, sizeof(cnt), hipMemcpyDeviceToHost, ctx->stream));
   CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   CBH_TRY(check_err(ctx));
   const int64_t nthr = (int64_t)cnt[0], ncand = (int64_t)cnt[2];
-  int64_t nlong = (int64_t)cnt[1], nh = 0, nhitems = 0;
+  int64_t nlong = (int64_t)cnt[1], nh = 0, nhitems = 0, nhthr = 0;
   int64_t *goff = nullptr, *ioff = nullptr;
   int32_t* hs = nullptr;
   if (ncand > 0) {
     int64_t *glen, *gitems;
     int32_t* gcur;
-    CBH_TRY(S.get(&glen, K + 1));
-    CBH_TRY(S.get(&gitems, K + 1));
-    CBH_TRY(S.get(&goff, K + 1));
-    CBH_TRY(S.get(&ioff, K + 1));
-    CBH_TRY(S.get(&gcur, K));
+    const int64_t K2 = 2 * K;
+    CBH_TRY(S.get(&glen, K2 + 1));
+    CBH_TRY(S.get(&gitems, K2 + 1));
+    CBH_TRY(S.get(&goff, K2 + 1));
+    CBH_TRY(S.get(&ioff, K2 + 1));
+    CBH_TRY(S.get(&gcur, K2));
     CBH_TRY(S.get(&hs, ncand));
-    hipLaunchKernelGGL(dot_hub_sizes_kernel, dim3(blocks_for(K, 256)), dim3(256), 0, ctx->stream, gcount, K, hub_min,
-                       glen, gitems);
-    CBH_HIP(ctx, hipMemsetAsync(glen + K, 0, sizeof(int64_t), ctx->stream));
-    CBH_HIP(ctx, hipMemsetAsync(gitems + K, 0, sizeof(int64_t), ctx->stream));
-    CBH_TRY(exclusive_scan_i64(ctx, S, glen, goff, K + 1));
-    CBH_TRY(exclusive_scan_i64(ctx, S, gitems, ioff, K + 1));
-    CBH_HIP(ctx, hipMemsetAsync(gcur, 0, sizeof(int32_t) * K, ctx->stream));
+    hipLaunchKernelGGL(dot_hub_sizes_kernel, dim3(blocks_for(K2, 256)), dim3(256), 0, ctx->stream, gcount, K, hub_min,
+                       hub_wmin, glen, gitems);
+    CBH_HIP(ctx, hipMemsetAsync(glen + K2, 0, sizeof(int64_t), ctx->stream));
+    CBH_HIP(ctx, hipMemsetAsync(gitems + K2, 0, sizeof(int64_t), ctx->stream));
+    CBH_TRY(exclusive_scan_i64(ctx, S, glen, goff, K2 + 1));
+    CBH_TRY(exclusive_scan_i64(ctx, S, gitems, ioff, K2 + 1));
+    CBH_HIP(ctx, hipMemsetAsync(gcur, 0, sizeof(int32_t) * K2, ctx->stream));
     hipLaunchKernelGGL(dot_hub_route_kernel, dim3(blocks_for(ncand, 256)), dim3(256), 0, ctx->stream, a, lcand, ncand,
-                       gcount, hub_min, goff, gcur, hs, llong, npiece, counts);
+                       gcount, hub_min, hub_wmin, hub_wave, goff, gcur, hs, llong, npiece, counts);
     CBH_HIP(ctx, hipGetLastError());
-    int64_t h2[2];
-    CBH_HIP(ctx, hipMemcpyAsync(&h2[0], goff + K, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
-    CBH_HIP(ctx, hipMemcpyAsync(&h2[1], ioff + K, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    int64_t h3[3];
+    CBH_HIP(ctx, hipMemcpyAsync(&h3[0], goff + K2, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(&h3[1], ioff + K, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    CBH_HIP(ctx, hipMemcpyAsync(&h3[2], ioff + K2, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
     CBH_HIP(ctx, hipMemcpyAsync(cnt, counts, sizeof(cnt), hipMemcpyDeviceToHost, ctx->stream));
     CBH_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    nh = h2[0];
-    nhitems = h2[1];
+    nh = h3[0];
+    nhthr = h3[1];
+    nhitems = h3[2];
     if (nh + ((int64_t)cnt[1] - nlong) != ncand) return fail(ctx, CBH_E_INTERNAL, "dot-form hub routing lost entries");
     nlong = (int64_t)cnt[1];
     if (diag_enabled())
-      std::fprintf(stderr, "[cbh diag] dot hub: %lld candidates, %lld grouped (%lld work items), %lld long\n",
-                   (long long)ncand, (long long)nh, (long long)nhitems, (long long)nlong);
+      std::fprintf(stderr, "[cbh diag] dot hub: %lld candidates, %lld grouped (%lld thread-mode + %lld wave-mode work items), %lld long\n",
+                   (long long)ncand, (long long)nh, (long long)nhthr, (long long)(nhitems - nhthr), (long long)nlong);
   }
   if (nthr > 0)
     hipLaunchKernelGGL(dot_thread_kernel<SR>, dim3(blocks_for(nthr, 256)), dim3(256), 0, ctx->stream, a, lthr, nthr);
@@ -2909,9 +2928,12 @@ static int masked_dot(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, const cb
     hipLaunchKernelGGL(dot_fold_kernel<SR>, dim3(blocks_for(nlong, 256)), dim3(256), 0, ctx->stream, a, llong, poff,
                        nlong, pval, phit);
   }
-  if (nh > 0)
-    hipLaunchKernelGGL(dot_hub_kernel<SR>, dim3((unsigned)std::min<int64_t>(nhitems, wave_grid_cap())), dim3(kHubBS), 0,
-                       ctx->stream, a, ioff, K, nhitems, goff, hs);
+  if (nhthr > 0)
+    hipLaunchKernelGGL(dot_hub_kernel<SR>, dim3((unsigned)std::min<int64_t>(nhthr, wave_grid_cap())), dim3(kHubBS), 0,
+                       ctx->stream, a, ioff, K, nhthr, goff, hs);
+  if (nhitems > nhthr)
+    hipLaunchKernelGGL(dot_hub_wave_kernel<SR>, dim3((unsigned)std::min<int64_t>(nhitems - nhthr, wave_grid_cap())),
+                       dim3(kHubBS), 0, ctx->stream, a, ioff, K, nhthr, nhitems, goff, hs);
   CBH_HIP(ctx, hipGetLastError());
   CBH_TRY(S.get(&hits, nzc + 1));
   CBH_TRY(S.get(&off, nzc + 1));

@@ -11,7 +11,7 @@ timeout -k 10 400 python -u -m pytest tests/test_apps_gpu.py "tests/test_fullsiz
   --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 for v in ${VARIANTS:-"CBH_DOT_HUB_MIN=0" "CBH_DOT_HUB_MIN=16" "CBH_DOT_HUB_MIN=64"}; do
-  env $v CBH_DIAG=1 timeout -k 10 300 python -u bench_tc.py --no-cpu-baseline --steps 2 "$@" > $OUT/tc_$v.json 2> $OUT/tc_$v.err \
+  env ${v//,/ } CBH_DIAG=1 timeout -k 10 300 python -u bench_tc.py --no-cpu-baseline --steps 2 "$@" > $OUT/tc_$v.json 2> $OUT/tc_$v.err \
     || { tail -20 $OUT/tc_$v.err; exit 1; }
   echo "[$v] $(python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(d['value'], d['ms_per_step'], d['check']['ok'], d['check']['digest'])" $OUT/tc_$v.json)"
   grep "dot hub" $OUT/tc_$v.err | tail -1
