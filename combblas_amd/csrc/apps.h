@@ -587,9 +587,12 @@ __global__ __launch_bounds__(kHubBS) void dot_hub_kernel(DotArgs a, const int64_
       __syncthreads();
       const int32_t r_lo = s_rows[0], r_hi = s_rows[n - 1];
       const int64_t span = (int64_t)r_hi - r_lo + 1;
-      // buckets over [r_lo, r_hi]: bucket(k) = (k - r_lo) * n / span; s_dir[b] = first row index
-      // whose bucket >= b (b in [0, n]): element t fills (bucket(t - 1), bucket(t)]
-      auto bucket = [&](int32_t k) -> int { return (int)(((int64_t)(k - r_lo) * n) / span); };
+      // buckets over [r_lo, r_hi]: bucket(k) ~ (k - r_lo) * n / span (monotone in k); s_dir[b] =
+      // first row index whose bucket >= b (b in [0, n]): element t fills (bucket(t - 1), bucket(t)]
+      // (k - r_lo) * n / span by a 32.32 reciprocal (no 64-bit division per element; span >= n as
+      // the rows are distinct, so the product stays below 2^63 and the bucket below n)
+      const uint64_t bscale = ((uint64_t)n << 32) / (uint64_t)span;
+      auto bucket = [&](int32_t k) -> int { return (int)(((uint64_t)(uint32_t)(k - r_lo) * bscale) >> 32); };
       for (int t = threadIdx.x; t <= n; t += kHubBS) {
         const int bt = t < n ? bucket(s_rows[t]) : n;
         const int bp = t > 0 ? bucket(s_rows[t - 1]) : -1;
@@ -701,7 +704,10 @@ __global__ __launch_bounds__(kHubBS) void dot_hub_wave_kernel(DotArgs a, const i
       __syncthreads();
       const int32_t r_lo = s_rows[0], r_hi = s_rows[n - 1];
       const int64_t span = (int64_t)r_hi - r_lo + 1;
-      auto bucket = [&](int32_t k) -> int { return (int)(((int64_t)(k - r_lo) * n) / span); };
+      // (k - r_lo) * n / span by a 32.32 reciprocal (no 64-bit division per element; span >= n as
+      // the rows are distinct, so the product stays below 2^63 and the bucket below n)
+      const uint64_t bscale = ((uint64_t)n << 32) / (uint64_t)span;
+      auto bucket = [&](int32_t k) -> int { return (int)(((uint64_t)(uint32_t)(k - r_lo) * bscale) >> 32); };
       for (int t = threadIdx.x; t <= n; t += kHubBS) {
         const int bt = t < n ? bucket(s_rows[t]) : n;
         const int bp = t > 0 ? bucket(s_rows[t - 1]) : -1;
@@ -711,11 +717,14 @@ __global__ __launch_bounds__(kHubBS) void dot_hub_wave_kernel(DotArgs a, const i
 #pragma unroll
       for (int j = 0; j < kHubEPW; ++j) {
         int64_t s = cur[j];
+        // one step ahead: the next 64 elements load while this step looks its elements up
+        int32_t kn = s + lane < send[j] ? srow[s + lane] : INT32_MAX;
         while (s < send[j]) {
           const int64_t q = s + lane;
-          const int32_t k = q < send[j] ? srow[q] : INT32_MAX;
+          const int32_t k = kn;
           const bool in = k <= r_hi;
           const int nin = __popcll(__ballot(in));
+          kn = nin == 64 && q + 64 < send[j] ? srow[q + 64] : INT32_MAX;
           if (in && k >= r_lo) {
             const int b = bucket(k);
             for (int x = s_dir[b], xe = s_dir[b + 1]; x < xe; ++x) {

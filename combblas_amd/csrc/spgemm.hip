@@ -2783,13 +2783,14 @@ extern "C" int cbh_transpose(cbh_ctx* ctx, const cbh_mat* A, cbh_mat** AT) {
 }
 
 // entries sharing one longer list that make it a hub group (apps.h); CBH_DOT_HUB_MIN overrides
-// (read per call), 0 keeps every long entry on the wave kernel's binary search. Measured at R-MAT
-// scale 24 (C4, profiles/r06/tc_hub): 16 / 128 / 512 / 2048 / 4096 / 16384 -> 7.81 / 7.64 / 7.59 /
-// 7.53 / 7.67 / 8.00 s per step against 8.11 s without groups: a group needs enough entries to
-// fill its workgroups' threads over every window of its longer list
+// (read per call), 0 keeps every long entry on the wave kernel's merge / binary search. C4 at
+// R-MAT scale 24 (profiles/r06/tc_hub), final kernels: 2048 / 512 / 256 / 128 -> 4.80 / 4.52 /
+// 4.50 / 4.45 s per step (8.11 s without groups); the thread mode alone measured best at 2048
+// before the reciprocal buckets (a group needs entries enough to fill its workgroups' threads
+// over every window of its longer list)
 static int dot_hub_min() {
   const char* e = std::getenv("CBH_DOT_HUB_MIN");
-  return e ? std::max(0, std::atoi(e)) : 2048;
+  return e ? std::max(0, std::atoi(e)) : 128;
 }
 
 // longer / shorter list length above which a long entry is a hub candidate (CBH_DOT_HUB_RATIO,
