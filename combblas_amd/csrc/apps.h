@@ -537,8 +537,11 @@ __global__ __launch_bounds__(256) void dot_hub_route_kernel(DotArgs a, const int
 }
 
 // one workgroup per (group, entry chunk), grid-strided over the work items
+#ifndef CBH_HUB_MINB  // (A/B hook) workgroups per CU the hub kernels' register budget is sized for
+#define CBH_HUB_MINB 1
+#endif
 template <class SR>
-__global__ __launch_bounds__(kHubBS) void dot_hub_kernel(DotArgs a, const int64_t* __restrict__ ioff, int64_t K,
+__global__ __launch_bounds__(kHubBS, CBH_HUB_MINB) void dot_hub_kernel(DotArgs a, const int64_t* __restrict__ ioff, int64_t K,
                                                          int64_t nitems, const int64_t* __restrict__ goff,
                                                          const int32_t* __restrict__ hs) {
   using val_t = typename SR::val_t;
@@ -567,19 +570,27 @@ __global__ __launch_bounds__(kHubBS) void dot_hub_kernel(DotArgs a, const int64_
     val_t acc[kHubEPT];
     bool hit[kHubEPT];
     const int32_t first = lrow[l0];
+    // each level of loads issued for all entries before the next (see the wave mode)
+    int64_t pe[kHubEPT], sid[kHubEPT];
 #pragma unroll
     for (int j = 0; j < kHubEPT; ++j) {
       const int64_t e = ebase + j * kHubBS + threadIdx.x;
-      cur[j] = send[j] = 0;
+      pe[j] = e < ge ? (int64_t)hs[g0 + e] : -1;
       acc[j] = val_t{};
       hit[j] = false;
-      if (e < ge) {
-        const int64_t p = hs[g0 + e];
-        const int64_t sid = b_long ? (int64_t)a.Mir[p] : (int64_t)a.Mcol[p];
-        send[j] = sd[sid + 1];
-        cur[j] = lb_rows64(srow, sd[sid], send[j], first);
-      }
     }
+#pragma unroll
+    for (int j = 0; j < kHubEPT; ++j) sid[j] = pe[j] < 0 ? 0 : (b_long ? (int64_t)a.Mir[pe[j]] : (int64_t)a.Mcol[pe[j]]);
+#pragma unroll
+    for (int j = 0; j < kHubEPT; ++j) {
+      cur[j] = pe[j] < 0 ? 0 : sd[sid[j]];
+      send[j] = pe[j] < 0 ? 0 : sd[sid[j] + 1];
+    }
+    // (thread mode: the shorter list is much shorter than the longer one; a bisection to the first
+    // window's first row saves the walk over the elements below it)
+#pragma unroll
+    for (int j = 0; j < kHubEPT; ++j)
+      if (pe[j] >= 0) cur[j] = lb_rows64(srow, cur[j], send[j], first);
     for (int64_t w0 = l0; w0 < l1; w0 += kHubWin) {
       const int n = (int)((l1 - w0) < kHubWin ? (l1 - w0) : kHubWin);
       __syncthreads();  // the previous window's readers are done with the LDS
@@ -655,7 +666,7 @@ __global__ __launch_bounds__(kHubBS) void dot_hub_kernel(DotArgs a, const int64_
 // of the rest of the (sorted) list, so a step advances the cursor by the ballot's count. Lane
 // partials are folded in lane order at the end (as dot_piece's).
 template <class SR>
-__global__ __launch_bounds__(kHubBS) void dot_hub_wave_kernel(DotArgs a, const int64_t* __restrict__ ioff, int64_t K,
+__global__ __launch_bounds__(kHubBS, CBH_HUB_MINB) void dot_hub_wave_kernel(DotArgs a, const int64_t* __restrict__ ioff, int64_t K,
                                                               int64_t it0, int64_t it1, const int64_t* __restrict__ goff,
                                                               const int32_t* __restrict__ hs) {
   using val_t = typename SR::val_t;
@@ -683,19 +694,22 @@ __global__ __launch_bounds__(kHubBS) void dot_hub_wave_kernel(DotArgs a, const i
     int64_t cur[kHubEPW], send[kHubEPW];
     val_t acc[kHubEPW];
     bool hit[kHubEPW];
-    const int32_t first = lrow[l0];
+    // the entries' shorter lists, each level of loads issued for all entries before the next; the
+    // cursors start at the lists' heads (elements below the first window are skipped by the walk)
+    int64_t pe[kHubEPW], sid[kHubEPW];
 #pragma unroll
     for (int j = 0; j < kHubEPW; ++j) {
       const int64_t e = ebase + j * (kHubBS / 64) + wid;
-      cur[j] = send[j] = 0;
+      pe[j] = e < ge ? (int64_t)hs[g0 + e] : -1;  // (wave-uniform)
       acc[j] = val_t{};
       hit[j] = false;
-      if (e < ge) {  // (wave-uniform)
-        const int64_t p = hs[g0 + e];
-        const int64_t sid = b_long ? (int64_t)a.Mir[p] : (int64_t)a.Mcol[p];
-        send[j] = sd[sid + 1];
-        cur[j] = lb_rows64(srow, sd[sid], send[j], first);
-      }
+    }
+#pragma unroll
+    for (int j = 0; j < kHubEPW; ++j) sid[j] = pe[j] < 0 ? 0 : (b_long ? (int64_t)a.Mir[pe[j]] : (int64_t)a.Mcol[pe[j]]);
+#pragma unroll
+    for (int j = 0; j < kHubEPW; ++j) {
+      cur[j] = pe[j] < 0 ? 0 : sd[sid[j]];
+      send[j] = pe[j] < 0 ? 0 : sd[sid[j] + 1];
     }
     for (int64_t w0 = l0; w0 < l1; w0 += kHubWin) {
       const int n = (int)((l1 - w0) < kHubWin ? (l1 - w0) : kHubWin);
@@ -714,11 +728,14 @@ __global__ __launch_bounds__(kHubBS) void dot_hub_wave_kernel(DotArgs a, const i
         for (int b = bp + 1; b <= bt; ++b) s_dir[b] = (uint16_t)t;
       }
       __syncthreads();
+      // the first step of entry 0, then of every next entry, loads while the previous one is walked
+      int32_t knext = cur[0] + lane < send[0] ? srow[cur[0] + lane] : INT32_MAX;
 #pragma unroll
       for (int j = 0; j < kHubEPW; ++j) {
         int64_t s = cur[j];
         // one step ahead: the next 64 elements load while this step looks its elements up
-        int32_t kn = s + lane < send[j] ? srow[s + lane] : INT32_MAX;
+        int32_t kn = knext;
+        if (j + 1 < kHubEPW) knext = cur[j + 1] + lane < send[j + 1] ? srow[cur[j + 1] + lane] : INT32_MAX;
         while (s < send[j]) {
           const int64_t q = s + lane;
           const int32_t k = kn;
