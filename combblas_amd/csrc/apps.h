@@ -545,7 +545,7 @@ __global__ __launch_bounds__(kHubBS, CBH_HUB_MINB) void dot_hub_kernel(DotArgs a
                                                          int64_t nitems, const int64_t* __restrict__ goff,
                                                          const int32_t* __restrict__ hs) {
   using val_t = typename SR::val_t;
-  __shared__ int32_t s_rows[kHubWin];
+  __shared__ int32_t s_rows[kHubWin + 1];  // + a sentinel above every row
   __shared__ uint16_t s_dir[kHubWin + 1];
   const val_t* __restrict__ av = reinterpret_cast<const val_t*>(a.ATnum);
   const val_t* __restrict__ bv = reinterpret_cast<const val_t*>(a.Bnum);
@@ -595,15 +595,17 @@ __global__ __launch_bounds__(kHubBS, CBH_HUB_MINB) void dot_hub_kernel(DotArgs a
       const int n = (int)((l1 - w0) < kHubWin ? (l1 - w0) : kHubWin);
       __syncthreads();  // the previous window's readers are done with the LDS
       for (int t = threadIdx.x; t < n; t += kHubBS) s_rows[t] = lrow[w0 + t];
+      if (threadIdx.x == 0) s_rows[n] = INT32_MAX;
       __syncthreads();
       const int32_t r_lo = s_rows[0], r_hi = s_rows[n - 1];
       const int64_t span = (int64_t)r_hi - r_lo + 1;
       // buckets over [r_lo, r_hi]: bucket(k) ~ (k - r_lo) * n / span (monotone in k); s_dir[b] =
       // first row index whose bucket >= b (b in [0, n]): element t fills (bucket(t - 1), bucket(t)]
-      // (k - r_lo) * n / span by a 32.32 reciprocal (no 64-bit division per element; span >= n as
-      // the rows are distinct, so the product stays below 2^63 and the bucket below n)
-      const uint64_t bscale = ((uint64_t)n << 32) / (uint64_t)span;
-      auto bucket = [&](int32_t k) -> int { return (int)(((uint64_t)(uint32_t)(k - r_lo) * bscale) >> 32); };
+      // ~(k - r_lo) * n / span by a 0.32 reciprocal and one __umulhi (span >= n as the rows are
+      // distinct, so the scale is at most 2^32, clamped to 2^32 - 1: monotone, below n)
+      const uint64_t bs64 = ((uint64_t)n << 32) / (uint64_t)span;
+      const uint32_t bscale = bs64 > 0xffffffffull ? 0xffffffffu : (uint32_t)bs64;
+      auto bucket = [&](int32_t k) -> int { return (int)__umulhi((uint32_t)(k - r_lo), bscale); };
       for (int t = threadIdx.x; t <= n; t += kHubBS) {
         const int bt = t < n ? bucket(s_rows[t]) : n;
         const int bp = t > 0 ? bucket(s_rows[t - 1]) : -1;
@@ -629,17 +631,15 @@ __global__ __launch_bounds__(kHubBS, CBH_HUB_MINB) void dot_hub_kernel(DotArgs a
               continue;
             }
             if (k < r_lo) continue;  // (between the previous window's last row and this one's first)
-            const int b = bucket(k);
-            for (int q = s_dir[b], qe = s_dir[b + 1]; q < qe; ++q) {
-              const int32_t r = s_rows[q];
-              if (r < k) continue;
-              if (r == k) {
-                const int64_t qg = w0 + q, sq = s + u;
-                const val_t pr = b_long ? SR::multiply(av[sq], bv[qg]) : SR::multiply(av[qg], bv[sq]);
-                acc[j] = hit[j] ? SR::add(acc[j], pr) : pr;
-                hit[j] = true;
-              }
-              break;
+            // the first row >= k from the bucket's first row on (the sentinel ends the walk)
+            int q = s_dir[bucket(k)];
+            int32_t r = s_rows[q];
+            while (r < k) r = s_rows[++q];
+            if (r == k) {
+              const int64_t qg = w0 + q, sq = s + u;
+              const val_t pr = b_long ? SR::multiply(av[sq], bv[qg]) : SR::multiply(av[qg], bv[sq]);
+              acc[j] = hit[j] ? SR::add(acc[j], pr) : pr;
+              hit[j] = true;
             }
           }
           s += used;
@@ -670,7 +670,7 @@ __global__ __launch_bounds__(kHubBS, CBH_HUB_MINB) void dot_hub_wave_kernel(DotA
                                                               int64_t it0, int64_t it1, const int64_t* __restrict__ goff,
                                                               const int32_t* __restrict__ hs) {
   using val_t = typename SR::val_t;
-  __shared__ int32_t s_rows[kHubWin];
+  __shared__ int32_t s_rows[kHubWin + 1];  // + a sentinel above every row
   __shared__ uint16_t s_dir[kHubWin + 1];
   const val_t* __restrict__ av = reinterpret_cast<const val_t*>(a.ATnum);
   const val_t* __restrict__ bv = reinterpret_cast<const val_t*>(a.Bnum);
@@ -715,13 +715,15 @@ __global__ __launch_bounds__(kHubBS, CBH_HUB_MINB) void dot_hub_wave_kernel(DotA
       const int n = (int)((l1 - w0) < kHubWin ? (l1 - w0) : kHubWin);
       __syncthreads();
       for (int t = threadIdx.x; t < n; t += kHubBS) s_rows[t] = lrow[w0 + t];
+      if (threadIdx.x == 0) s_rows[n] = INT32_MAX;
       __syncthreads();
       const int32_t r_lo = s_rows[0], r_hi = s_rows[n - 1];
       const int64_t span = (int64_t)r_hi - r_lo + 1;
-      // (k - r_lo) * n / span by a 32.32 reciprocal (no 64-bit division per element; span >= n as
-      // the rows are distinct, so the product stays below 2^63 and the bucket below n)
-      const uint64_t bscale = ((uint64_t)n << 32) / (uint64_t)span;
-      auto bucket = [&](int32_t k) -> int { return (int)(((uint64_t)(uint32_t)(k - r_lo) * bscale) >> 32); };
+      // ~(k - r_lo) * n / span by a 0.32 reciprocal and one __umulhi (span >= n as the rows are
+      // distinct, so the scale is at most 2^32, clamped to 2^32 - 1: monotone, below n)
+      const uint64_t bs64 = ((uint64_t)n << 32) / (uint64_t)span;
+      const uint32_t bscale = bs64 > 0xffffffffull ? 0xffffffffu : (uint32_t)bs64;
+      auto bucket = [&](int32_t k) -> int { return (int)__umulhi((uint32_t)(k - r_lo), bscale); };
       for (int t = threadIdx.x; t <= n; t += kHubBS) {
         const int bt = t < n ? bucket(s_rows[t]) : n;
         const int bp = t > 0 ? bucket(s_rows[t - 1]) : -1;
@@ -743,17 +745,15 @@ __global__ __launch_bounds__(kHubBS, CBH_HUB_MINB) void dot_hub_wave_kernel(DotA
           const int nin = __popcll(__ballot(in));
           kn = nin == 64 && q + 64 < send[j] ? srow[q + 64] : INT32_MAX;
           if (in && k >= r_lo) {
-            const int b = bucket(k);
-            for (int x = s_dir[b], xe = s_dir[b + 1]; x < xe; ++x) {
-              const int32_t r = s_rows[x];
-              if (r < k) continue;
-              if (r == k) {
-                const int64_t qg = w0 + x;
-                const val_t pr = b_long ? SR::multiply(av[q], bv[qg]) : SR::multiply(av[qg], bv[q]);
-                acc[j] = hit[j] ? SR::add(acc[j], pr) : pr;
-                hit[j] = true;
-              }
-              break;
+            // the first row >= k from the bucket's first row on (the sentinel ends the walk)
+            int x = s_dir[bucket(k)];
+            int32_t r = s_rows[x];
+            while (r < k) r = s_rows[++x];
+            if (r == k) {
+              const int64_t qg = w0 + x;
+              const val_t pr = b_long ? SR::multiply(av[q], bv[qg]) : SR::multiply(av[qg], bv[q]);
+              acc[j] = hit[j] ? SR::add(acc[j], pr) : pr;
+              hit[j] = true;
             }
           }
           s += nin;
