@@ -2850,8 +2850,9 @@ static int masked_dot(cbh_ctx* ctx, const cbh_mat* A, const cbh_mat* B, const cb
   CBH_HIP(ctx, hipMemsetAsync(counts, 0, 3 * sizeof(unsigned long long), ctx->stream));
   DotArgs a{ATd, AT->ir, AT->num, Bd, B->ir, B->num, Mcol, M->ir, nm, A->m, B->n, Tnum, Tflag, ctx->d_err};
   // hub groups (apps.h): entries of the binary-search branch grouped by their longer list
-  const int hub_min = dot_hub_min();
   const int64_t K = B->n + A->m;  // group keys: j < nB (B(:, j) longer), nB + i (A(i, :) longer)
+  // (the group tables take ~40 B per key and mode: skipped for masks far sparser than their shape)
+  const int hub_min = K <= 8 * nm + (int64_t(1) << 20) ? dot_hub_min() : 0;
   const int hub_wave = dot_hub_wave();
   const int hub_wmin = dot_hub_wmin(hub_min);
   int32_t *gcount = nullptr, *lcand = nullptr;  // K thread-mode keys, then K wave-mode keys
