@@ -39,6 +39,12 @@
 #ifndef CBH_HASH_BATCH
 #define CBH_HASH_BATCH 0
 #endif
+#ifndef CBH_PROBE_BOUND
+#define CBH_PROBE_BOUND 0
+#endif
+#ifndef CBH_GUARD_BRANCHLESS  // the numeric hash's per-product range guard as flag + clamp, not a
+#define CBH_GUARD_BRANCHLESS 1  // branch (round 6: hash 229.4 -> 227.1 ms; on the dense kernel flat)
+#endif
 #ifndef CBH_GATHER_PIN
 #define CBH_GATHER_PIN 1
 #endif
@@ -1109,11 +1115,18 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
       } else if constexpr (NUM) {
         sweep(nec, P, true, [&](int u) {
           const val_t vv = av[u];
-          const uint32_t d = (uint32_t)(r[u] - lo);
+          uint32_t d = (uint32_t)(r[u] - lo);
+#if CBH_GUARD_BRANCHLESS
+          // a row outside the sub-tile (never, unless the plan is inconsistent) is flagged and
+          // clamped into it instead of branching around the insert: the flag fails the call
+          bad |= d >= tw ? 1 << 8 : 0;
+          d = d < tw ? d : 0u;
+#else
           if (d >= tw) {
             bad |= 1 << 8;
             return;
           }
+#endif
           uint32_t s = (uint32_t)(((uint64_t)d * scale) >> 32);
           bool ok = false;
           if constexpr (LOCKED) {
@@ -1123,7 +1136,11 @@ __global__ __launch_bounds__(BS, (task_waves_per_eu<BS, TaskCfg<SR, T, BS, EMAX,
                 break;
               }
           } else {
-            for (int probe = 0; probe < kPmax && s < (uint32_t)TA; ++probe, ++s) {
+            // (s < T + kPmax - 1 <= TA for every probe: no end-of-table test -- round 6, hash 237.4
+            // -> 229.2 ms per scale-22 product, the kernel being issue-bound; CBH_PROBE_BOUND=1
+            // restores it for A/B)
+            static_assert(kGuard >= kPmax, "forward probes stay inside the guard slots");
+            for (int probe = 0; probe < kPmax && (!CBH_PROBE_BOUND || s < (uint32_t)TA); ++probe, ++s) {
               const int32_t k = atomicCAS(&keys[s], kEmpty, r[u]);
               if (k == kEmpty || k == r[u]) {
                 SR::lds_acc(&vals[s], vv);
